@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""Headline benchmark: aggregate VAE samples/s across K concurrent HPO trials.
+
+Metric / config from BASELINE.json: the global world (one process per MI355X)
+is carved into K trial groups (default K = N: one trial per GPU, BASELINE
+config #3 shape "8 subgroups x 1 GPU"; ``--ngroups`` gives e.g. 4x2 with
+intra-group gradient all-reduce). Every trial trains the reference MLP-VAE
+(784-400-20, /root/reference/vae-hpo.py:19-45, fp32 like the reference) with
+Adam(lr=1e-3) at batch 128 on its DistributedSampler shard of a synthetic
+MNIST-shaped dataset, with its own (lr, beta) hyper-parameters.
+
+A step = one full training iteration (fwd + bwd + [all-reduce] + Adam) of every
+trial. Timing: W warm-up steps (also captures the hipGraphs), then a barrier +
+device sync, exactly K steps, barrier + device sync; the max over ranks is
+reported. ``value`` = Σ_trials (batch x steps) / max_time (samples are counted
+once per trial, not per replica — SURVEY.md §6 metric definition).
+
+Run: python bench.py --gpus N --steps K --warmup W   (N>1 via torch.distributed.run)
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+# Reference hot training step measured on the survey box (BASELINE.md row
+# "Reference hot step (fwd+bwd+DDP+Adam), B=128, 1 rank": 32.9k samples/s per
+# trial). Used per trial: baseline(K) = K x 32.9k (generous to the reference,
+# which measured sub-linear on 2 trials).
+REF_SAMPLES_PER_S_PER_TRIAL = 32900.0
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch-size", type=int, default=128)
+    ap.add_argument("--ngroups", type=int, default=None, help="trials K (default: world size)")
+    ap.add_argument("--model", default="mlp", choices=["mlp"])
+    ap.add_argument("--graph-steps", type=int, default=10)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--backend", default=None, help="hip|torch (default: hip on GPU)")
+    ap.add_argument("--json-out", default=None)
+    a = ap.parse_args(argv)
+
+    from multidisttorch_amd.runtime import setup_ddp, global_barrier, control_group
+    from multidisttorch_amd.parallel.groups import setup_ddp_groups
+    from multidisttorch_amd.hpo.trial import default_sweep
+    from multidisttorch_amd.data.datasets import mnist_like
+    from multidisttorch_amd.data.sampler import shard_indices
+    from multidisttorch_amd.models.mlp_trainer import MlpVaeTrainer
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+
+    world, rank = setup_ddp(verbose=False)
+    K = a.ngroups or world
+    handles = setup_ddp_groups(K, verbose=False)
+    ctrl = control_group()
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    n_per = world // K
+    gid = rank // n_per if rank < K * n_per else None
+    specs = default_sweep(K)
+
+    trainer = None
+    if gid is not None:
+        pg = handles[gid]
+        grank = dist.get_rank(pg)
+        spec = specs[gid]
+        trainer = MlpVaeTrainer(batch_size=a.batch_size, device=dev, backend=a.backend,
+                                seed=spec.seed, lr=spec.lr, kl_beta=spec.beta, rng_stream=grank,
+                                use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
+        # replicas of a group start from group rank 0's weights (DDP broadcast)
+        if n_per > 1:
+            dist.broadcast(trainer.params, src=dist.get_global_rank(pg, 0), group=pg)
+            trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, [0, trainer.split, trainer.numel]))
+        train = mnist_like(True, synthetic=True, device=dev)
+        idx = shard_indices(len(train), K, gid)
+        trainer.bind_train_data(train.data, idx)
+        trainer.set_cursor(0, idx.numel() // a.batch_size)  # full batches only
+        trainer.train_steps(a.warmup)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    global_barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if trainer is not None:
+        trainer.train_steps(a.steps)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    global_barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctrl)
+        dt = float(t.item())
+    samples = K * a.batch_size * a.steps
+    value = samples / dt
+    # sanity: training actually progressed and the loss is finite
+    ok = True
+    if trainer is not None:
+        st = trainer.read_state()
+        hist = trainer.loss_history()
+        last = float(hist[(st["step"] - 1) % len(hist)])
+        ok = st["step"] == a.warmup + a.steps and last == last and last < 1e9
+    flag = torch.tensor([1.0 if ok else 0.0])
+    if world > 1:
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ctrl)
+    if rank == 0:
+        out = {
+            "metric": "aggregate VAE samples/sec across K concurrent HPO trials",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / (REF_SAMPLES_PER_S_PER_TRIAL * K), 2),
+            "dtype": "fp32",
+            "data": "synthetic (MNIST-shaped 60000x1x28x28, random-init weights)",
+            "config": {
+                "model": "MLP-VAE 784-400-20 (reference vae-hpo.py topology)",
+                "global_batch": a.batch_size * K,
+                "per_trial_batch": a.batch_size,
+                "seq_len": None,
+                "parallelism": f"groups{K}x{n_per}",
+                "trials": K,
+                "backend": trainer.backend if trainer is not None else None,
+                "graphs": (not a.no_graphs),
+                "valid": bool(flag.item() > 0),
+            },
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,259 @@
+#include "vae_engine.h"
+
+#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+
+#include <cstring>
+#include <stdexcept>
+
+#include "../kernels/vae_mlp.h"
+
+extern "C" int mdt_adam_step(float* p, const float* g, float* m, float* v, long long n,
+                             const mdt::HParams* hp, mdt::TrainState* st, const float* partials,
+                             int nkld, int nbce, int advance, int decoupled_wd, int max_blocks,
+                             hipStream_t s);
+extern "C" int mdt_loss_finalize(const mdt::HParams* hp, mdt::TrainState* st,
+                                 const float* partials, int nkld, int nbce, int advance,
+                                 hipStream_t s);
+
+namespace mdt {
+
+static inline int64_t align64(int64_t v) { return (v + 63) / 64 * 64; }
+
+static void check_rc(int rc, const char* what) {
+  if (rc != 0) {
+    throw std::runtime_error(std::string("mdt: ") + what + " failed with code " +
+                             std::to_string(rc));
+  }
+}
+
+MlpVaeEngine::MlpVaeEngine(int64_t batch, int64_t D, int64_t H, int64_t Z, int64_t device_index)
+    : B_(batch), D_(D), H_(H), Z_(Z) {
+  TORCH_CHECK(batch > 0 && batch <= kMaxBatch, "batch must be in [1, ", kMaxBatch, "]");
+  TORCH_CHECK(Z > 0 && Z <= 32, "latent size must be in [1, 32]");
+  TORCH_CHECK(D % 4 == 0 && H % 4 == 0, "D and H must be multiples of 4");
+  int64_t off = 0;
+  auto add = [&](const std::string& n, std::vector<int64_t> shape, int64_t numel) {
+    layout_.push_back({n, off, shape});
+    off = align64(off + numel);
+  };
+  // head: everything whose gradient becomes final at the END of backward
+  add("fc1.weight", {H, D}, H * D);
+  add("fc1.bias", {H}, H);
+  const int64_t w2 = off;
+  off = align64(off + 2 * Z * H);
+  const int64_t b2 = off;
+  off = align64(off + 2 * Z);
+  layout_.push_back({"fc21.weight", w2, {Z, H}});
+  layout_.push_back({"fc22.weight", w2 + Z * H, {Z, H}});
+  layout_.push_back({"fc21.bias", b2, {Z}});
+  layout_.push_back({"fc22.bias", b2 + Z, {Z}});
+  add("fc3.weight", {H, Z}, H * Z);
+  add("fc3.bias", {H}, H);
+  split_ = off;  // tail bucket: fc4 (ready first in backward)
+  add("fc4.weight", {D, H}, D * H);
+  add("fc4.bias", {D}, D);
+  total_ = off;
+
+  auto fopt = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device_index);
+  params = torch::zeros({total_}, fopt);
+  grads = torch::zeros({total_}, fopt);
+  exp_avg = torch::zeros({total_}, fopt);
+  exp_avg_sq = torch::zeros({total_}, fopt);
+
+  int64_t a = 0;
+  auto act_add = [&](const char* n, int64_t per_row) {
+    act_off_.push_back({n, a});
+    a = align64(a + B_ * per_row);
+  };
+  act_add("h1", H); act_add("mulv", 2 * Z); act_add("eps", Z); act_add("z", Z);
+  act_add("h3", H); act_add("dlog", D); act_add("dh3", H); act_add("dmulv", 2 * Z);
+  act_add("dh1", H); act_add("recon", D);
+  acts = torch::zeros({a}, fopt);
+  partials = torch::zeros({kPartials}, fopt);
+  auto bopt = torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device_index);
+  const int64_t st_bytes = align64((int64_t)sizeof(TrainState));
+  train_state = torch::zeros({st_bytes}, bopt);
+  eval_state = torch::zeros({st_bytes}, bopt);
+  hparams = torch::zeros({align64((int64_t)sizeof(HParams))}, bopt);
+  set_hparams(1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0, 1.0, 0);
+}
+
+std::vector<std::tuple<std::string, int64_t, std::vector<int64_t>>> MlpVaeEngine::layout() const {
+  std::vector<std::tuple<std::string, int64_t, std::vector<int64_t>>> out;
+  for (auto& e : layout_) out.emplace_back(e.name, e.offset, e.shape);
+  return out;
+}
+
+static int64_t off_of(const std::vector<LayoutEntry>& l, const char* n) {
+  for (auto& e : l)
+    if (e.name == n) return e.offset;
+  throw std::runtime_error(std::string("mdt: no layout entry ") + n);
+}
+
+at::Tensor MlpVaeEngine::act(const std::string& name, int64_t M) {
+  for (auto& p : act_off_) {
+    if (p.first == name) {
+      int64_t per = 0;
+      if (name == "h1" || name == "h3" || name == "dh3" || name == "dh1") per = H_;
+      else if (name == "mulv" || name == "dmulv") per = 2 * Z_;
+      else if (name == "eps" || name == "z") per = Z_;
+      else per = D_;
+      return acts.narrow(0, p.second, M * per).view({M, per});
+    }
+  }
+  throw std::runtime_error("mdt: unknown activation " + name);
+}
+
+void MlpVaeEngine::set_hparams(double lr, double beta1, double beta2, double eps,
+                               double weight_decay, double kl_beta, double grad_scale,
+                               int64_t seed) {
+  HParams h;
+  std::memset(&h, 0, sizeof(h));
+  h.lr = (float)lr; h.beta1 = (float)beta1; h.beta2 = (float)beta2; h.eps = (float)eps;
+  h.weight_decay = (float)weight_decay; h.kl_beta = (float)kl_beta;
+  h.grad_scale = (float)grad_scale;
+  h.seed_lo = (uint32_t)((uint64_t)seed & 0xffffffffu);
+  h.seed_hi = (uint32_t)((uint64_t)seed >> 32);
+  auto cpu = torch::empty({(int64_t)sizeof(HParams)}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), &h, sizeof(h));
+  hparams.narrow(0, 0, sizeof(HParams)).copy_(cpu);
+}
+
+void MlpVaeEngine::set_cursor(bool eval, int64_t cursor, int64_t nbatches) {
+  at::Tensor& s = eval ? eval_state : train_state;
+  int32_t v[2] = {(int32_t)cursor, (int32_t)nbatches};
+  auto cpu = torch::empty({8}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), v, 8);
+  s.narrow(0, offsetof(TrainState, cursor), 8).copy_(cpu);
+}
+
+void MlpVaeEngine::set_step(int64_t step) {
+  auto cpu = torch::empty({8}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), &step, 8);
+  train_state.narrow(0, offsetof(TrainState, step), 8).copy_(cpu);
+}
+
+void MlpVaeEngine::reset_loss(bool eval) {
+  at::Tensor& s = eval ? eval_state : train_state;
+  s.narrow(0, offsetof(TrainState, epoch_loss), 16).zero_();
+}
+
+std::vector<double> MlpVaeEngine::read_state(bool eval) {
+  at::Tensor& s = eval ? eval_state : train_state;
+  auto cpu = s.narrow(0, 0, offsetof(TrainState, loss_hist)).to(torch::kCPU);
+  TrainState h;
+  std::memcpy(&h, cpu.data_ptr(), offsetof(TrainState, loss_hist));
+  return {(double)h.step, (double)h.cursor, (double)h.nbatches, h.epoch_loss, h.epoch_count};
+}
+
+at::Tensor MlpVaeEngine::loss_history(bool eval) {
+  at::Tensor& s = eval ? eval_state : train_state;
+  return s.narrow(0, offsetof(TrainState, loss_hist), sizeof(float) * kLossHist)
+      .to(torch::kCPU)
+      .view(torch::kFloat32);
+}
+
+void MlpVaeEngine::fill_args(void* out, const at::Tensor& X, const at::Tensor& idx, int64_t M,
+                             bool train, bool eval, int64_t rng_stream, bool want_recon) {
+  TORCH_CHECK(X.is_cuda() && X.scalar_type() == torch::kFloat32 && X.is_contiguous() &&
+                  X.dim() == 2 && X.size(1) == D_,
+              "X must be a contiguous CUDA float32 [N, D] tensor");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == torch::kInt32 && idx.is_contiguous(),
+              "idx must be a contiguous CUDA int32 tensor");
+  TORCH_CHECK(M > 0 && M <= B_, "M must be in [1, B]");
+  VaeArgs& a = *reinterpret_cast<VaeArgs*>(out);
+  std::memset(&a, 0, sizeof(a));
+  a.M = (int)M; a.B = (int)B_; a.D = (int)D_; a.H = (int)H_; a.Z = (int)Z_;
+  a.rng_stream = (uint32_t)rng_stream;
+  a.train = train ? 1 : 0;
+  a.X = X.data_ptr<float>();
+  a.idx = idx.data_ptr<int32_t>();
+  float* P = params.data_ptr<float>();
+  float* G = grads.data_ptr<float>();
+  const int64_t oW1 = off_of(layout_, "fc1.weight"), ob1 = off_of(layout_, "fc1.bias");
+  const int64_t oW2 = off_of(layout_, "fc21.weight"), ob2 = off_of(layout_, "fc21.bias");
+  const int64_t oW3 = off_of(layout_, "fc3.weight"), ob3 = off_of(layout_, "fc3.bias");
+  const int64_t oW4 = off_of(layout_, "fc4.weight"), ob4 = off_of(layout_, "fc4.bias");
+  a.W1 = P + oW1; a.b1 = P + ob1; a.W2 = P + oW2; a.b2 = P + ob2;
+  a.W3 = P + oW3; a.b3 = P + ob3; a.W4 = P + oW4; a.b4 = P + ob4;
+  a.gW1 = G + oW1; a.gb1 = G + ob1; a.gW2 = G + oW2; a.gb2 = G + ob2;
+  a.gW3 = G + oW3; a.gb3 = G + ob3; a.gW4 = G + oW4; a.gb4 = G + ob4;
+  float* A = acts.data_ptr<float>();
+  auto ap = [&](const char* n) {
+    for (auto& p : act_off_)
+      if (p.first == n) return A + p.second;
+    throw std::runtime_error("mdt: act");
+  };
+  a.h1 = ap("h1"); a.mulv = ap("mulv"); a.eps = ap("eps"); a.z = ap("z"); a.h3 = ap("h3");
+  a.dlog = ap("dlog"); a.dh3 = ap("dh3"); a.dmulv = ap("dmulv"); a.dh1 = ap("dh1");
+  a.recon = want_recon ? ap("recon") : nullptr;
+  a.partials = partials.data_ptr<float>();
+  a.st = reinterpret_cast<TrainState*>((eval ? eval_state : train_state).data_ptr<uint8_t>());
+  a.hp = reinterpret_cast<const HParams*>(hparams.data_ptr<uint8_t>());
+}
+
+void MlpVaeEngine::forward(const at::Tensor& X, const at::Tensor& idx, int64_t M, bool train,
+                           bool eval, int64_t rng_stream, bool want_recon) {
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
+  VaeArgs a;
+  fill_args(&a, X, idx, M, train, eval, rng_stream, want_recon);
+  const VaeGrid g = vae_grid(a.M, a.D, a.H, a.Z);
+  last_f2_blocks_ = g.f2;
+  last_f3_blocks_ = g.f3;
+  check_rc(mdt_vae_forward(&a, c10::hip::getCurrentHIPStream().stream()), "vae forward");
+}
+
+void MlpVaeEngine::backward(const at::Tensor& X, const at::Tensor& idx, int64_t M, int64_t part) {
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
+  VaeArgs a;
+  fill_args(&a, X, idx, M, true, false, 0, false);
+  check_rc(mdt_vae_backward(&a, c10::hip::getCurrentHIPStream().stream(), (int)part),
+           "vae backward");
+}
+
+void MlpVaeEngine::adam(bool decoupled_wd) {
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
+  check_rc(mdt_adam_step(params.data_ptr<float>(), grads.data_ptr<float>(),
+                         exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(), total_,
+                         reinterpret_cast<const HParams*>(hparams.data_ptr<uint8_t>()),
+                         reinterpret_cast<TrainState*>(train_state.data_ptr<uint8_t>()),
+                         partials.data_ptr<float>(), last_f2_blocks_, last_f3_blocks_, 3,
+                         decoupled_wd ? 1 : 0, 0, c10::hip::getCurrentHIPStream().stream()),
+           "adam");
+}
+
+void MlpVaeEngine::loss_finalize(bool eval) {
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
+  check_rc(mdt_loss_finalize(reinterpret_cast<const HParams*>(hparams.data_ptr<uint8_t>()),
+                             reinterpret_cast<TrainState*>(
+                                 (eval ? eval_state : train_state).data_ptr<uint8_t>()),
+                             partials.data_ptr<float>(), last_f2_blocks_, last_f3_blocks_,
+                             eval ? 3 : 0, c10::hip::getCurrentHIPStream().stream()),
+           "loss finalize");
+}
+
+at::Tensor MlpVaeEngine::decode(const at::Tensor& z) {
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
+  TORCH_CHECK(z.is_cuda() && z.scalar_type() == torch::kFloat32 && z.is_contiguous() &&
+                  z.dim() == 2 && z.size(1) == Z_ && z.size(0) <= B_,
+              "z must be a contiguous CUDA float32 [M<=B, Z] tensor");
+  VaeArgs a;
+  // X/idx are unused by the decode kernels; pass the parameter arena as a dummy
+  // dataset view of the right width is not possible, so fill by hand.
+  std::memset(&a, 0, sizeof(a));
+  a.M = (int)z.size(0); a.B = (int)B_; a.D = (int)D_; a.H = (int)H_; a.Z = (int)Z_;
+  float* P = params.data_ptr<float>();
+  a.W3 = P + off_of(layout_, "fc3.weight"); a.b3 = P + off_of(layout_, "fc3.bias");
+  a.W4 = P + off_of(layout_, "fc4.weight"); a.b4 = P + off_of(layout_, "fc4.bias");
+  float* A = acts.data_ptr<float>();
+  for (auto& p : act_off_) {
+    if (p.first == "h3") a.h3 = A + p.second;
+    if (p.first == "recon") a.recon = A + p.second;
+  }
+  check_rc(mdt_vae_decode(&a, z.data_ptr<float>(), c10::hip::getCurrentHIPStream().stream()),
+           "vae decode");
+  return act("recon", a.M).clone();
+}
+
+}  // namespace mdt

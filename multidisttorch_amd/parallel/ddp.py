@@ -1,0 +1,239 @@
+"""Intra-group data parallelism over a flat gradient arena.
+
+Reference: ``DistributedDataParallel(model, process_group=group)``
+(/root/reference/vae-hpo.py:130) with torch's defaults — 25 MiB buckets, a
+1 MiB first bucket, per-parameter copies into bucket storage and back into
+``.grad`` after the all-reduce.
+
+MI355X-first design:
+  * gradients live in ONE contiguous arena; each ``param.grad`` is a view into
+    it, so buckets are [begin, end) slices and RCCL reduces them in place;
+  * bucket boundaries come from an xGMI cost model (``plan_buckets``): in a
+    group of s GPUs on a fully connected 8-GPU xGMI mesh a ring uses ONE
+    ~153 GB/s link per GPU, so per-bucket time is alpha + 2(s-1)/s * bytes/BW;
+    buckets are sized so each one's transfer hides behind the backward compute
+    that follows it, and tiny models get 1-2 buckets (latency-bound regime);
+  * the collectives are issued by the native C++ ``BucketReducer`` (csrc/
+    runtime/reducer.cpp) on the c10d process group of the trial: RCCL on GPU
+    (own stream, AVG as pre-mul-sum, graph-capturable), gloo on CPU tests.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from ..ops import native
+
+__all__ = ["XgmiModel", "plan_buckets", "make_arena_reducer", "PyBucketReducer", "ArenaDDP",
+           "broadcast_params"]
+
+
+class XgmiModel:
+    """Cost model of a ring all-reduce inside a contiguous group on 8x MI355X."""
+
+    def __init__(self, link_gbps: float = 153.0, alpha_us: float = 12.0, channels: int = 1):
+        self.link = link_gbps * 1e9
+        self.alpha = alpha_us * 1e-6
+        self.channels = channels
+
+    def allreduce_s(self, nbytes: int, group_size: int) -> float:
+        if group_size <= 1:
+            return 0.0
+        s = group_size
+        # RCCL on a full mesh can run several rings over distinct links; a
+        # single ring is per-link bound. `channels` = usable disjoint rings.
+        bw = self.link * max(1, min(self.channels, s - 1))
+        return 2 * (s - 1) * self.alpha / max(1, s - 1) + 2 * (s - 1) / s * nbytes / bw
+
+
+def plan_buckets(param_bytes: Sequence[int], group_size: int, bwd_compute_s: Optional[Sequence[float]] = None,
+                 cap_bytes: int = 8 << 20, first_bytes: int = 1 << 20,
+                 model: Optional[XgmiModel] = None) -> List[List[int]]:
+    """Group parameter indices (in gradient-READY order) into buckets.
+
+    Greedy: close a bucket when it reaches the cap, or when the remaining
+    backward compute after this point can no longer hide a bigger transfer.
+    Without compute estimates: torch-like first bucket, then `cap_bytes`.
+    """
+    model = model or XgmiModel()
+    n = len(param_bytes)
+    buckets, cur, cur_b = [], [], 0
+    remaining = list(bwd_compute_s) if bwd_compute_s is not None else None
+    for i, b in enumerate(param_bytes):
+        cur.append(i)
+        cur_b += b
+        limit = first_bytes if not buckets else cap_bytes
+        close = cur_b >= limit
+        if remaining is not None and not close:
+            rest = sum(remaining[i + 1:])
+            # stop growing once this bucket's comm would exceed what is left to hide behind
+            close = model.allreduce_s(cur_b, group_size) >= rest and cur_b >= (256 << 10)
+        if close:
+            buckets.append(cur)
+            cur, cur_b = [], 0
+    if cur:
+        buckets.append(cur)
+    return buckets
+
+
+class PyBucketReducer:
+    """Pure-Python reducer with the BucketReducer API (fallback when _C is absent)."""
+
+    def __init__(self, pg, flat: torch.Tensor, bounds: Sequence[int], average: bool):
+        self.pg, self.flat, self._bounds, self.average = pg, flat, list(bounds), average
+        self.world = dist.get_world_size(pg)
+        self.work = [None] * (len(self._bounds) - 1)
+        self.param_bucket, self.need, self.have = [], [], []
+        self._launched = 0
+        self.use_avg = average and flat.is_cuda
+
+    def num_buckets(self):
+        return len(self._bounds) - 1
+
+    def bounds(self):
+        return list(self._bounds)
+
+    def launch(self, b):
+        if self.world == 1:
+            return
+        assert self.work[b] is None, f"bucket {b} launched twice"
+        v = self.flat[self._bounds[b]:self._bounds[b + 1]]
+        op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
+        self.work[b] = dist.all_reduce(v, op=op, group=self.pg, async_op=True)
+        self._launched += 1
+
+    def wait(self, b):
+        w = self.work[b]
+        if w is None:
+            return
+        w.wait()
+        self.work[b] = None
+        if self.average and not self.use_avg:
+            self.flat[self._bounds[b]:self._bounds[b + 1]].div_(self.world)
+
+    def launch_all(self):
+        for b in range(self.num_buckets()):
+            if self.work[b] is None:
+                self.launch(b)
+
+    def wait_all(self):
+        for b in range(self.num_buckets()):
+            self.wait(b)
+
+    def set_param_map(self, pb):
+        self.param_bucket = list(pb)
+        self.need = [0] * self.num_buckets()
+        for b in pb:
+            self.need[b] += 1
+        self.have = [0] * self.num_buckets()
+
+    def mark_ready(self, p):
+        b = self.param_bucket[p]
+        self.have[b] += 1
+        if self.have[b] == self.need[b]:
+            self.launch(b)
+
+    def reset_iteration(self):
+        self.have = [0] * self.num_buckets()
+
+    def pending(self):
+        return sum(w is not None for w in self.work)
+
+    def launched_count(self):
+        return self._launched
+
+
+def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: bool = True,
+                       prefer_native: bool = True):
+    if prefer_native and native.available():
+        return native.require().BucketReducer(pg, flat, [int(b) for b in bounds], average)
+    if flat.is_cuda:
+        native.require()  # on GPU the native reducer is mandatory: fail loudly
+    return PyBucketReducer(pg, flat, bounds, average)
+
+
+@torch.no_grad()
+def broadcast_params(tensors: Iterable[torch.Tensor], pg, src_group_rank: int = 0):
+    """Sync replicas from group rank ``src`` (DDP's _sync_module_states)."""
+    if pg is None or dist.get_world_size(pg) == 1:
+        return
+    src = dist.get_global_rank(pg, src_group_rank)
+    for t in tensors:
+        dist.broadcast(t, src=src, group=pg)
+
+
+class ArenaDDP(nn.Module):
+    """Data-parallel wrapper for generic modules with arena gradients.
+
+    After construction every ``p.grad`` is a view into ``self.grad_arena``
+    (laid out in reverse registration order = gradient-ready order, as torch
+    DDP's rebuilt buckets). A post-accumulate hook per parameter marks it ready;
+    a bucket's all-reduce launches the moment its last gradient lands, while
+    autograd continues with earlier layers.
+    """
+
+    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 8.0,
+                 first_bucket_mb: float = 1.0, broadcast: bool = True, average: bool = True):
+        super().__init__()
+        self.module = module
+        self.pg = process_group
+        params = [p for p in module.parameters() if p.requires_grad]
+        self._params = params
+        order = list(reversed(range(len(params))))  # ready order
+        dev = params[0].device
+        dtype = params[0].dtype
+        sizes = [params[i].numel() for i in order]
+        offs, off = {}, 0
+        for i, n in zip(order, sizes):
+            offs[i] = off
+            off += (n + 63) // 64 * 64
+        self.grad_arena = torch.zeros(off, dtype=dtype, device=dev)
+        for i, p in enumerate(params):
+            p.grad = self.grad_arena[offs[i]:offs[i] + p.numel()].view_as(p)
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        buckets = plan_buckets([params[i].numel() * params[i].element_size() for i in order], self.world,
+                               cap_bytes=int(bucket_cap_mb * (1 << 20)),
+                               first_bytes=int(first_bucket_mb * (1 << 20)))
+        bounds = [0]
+        pb = [0] * len(params)
+        for bi, bk in enumerate(buckets):
+            for j in bk:
+                pb[order[j]] = bi
+            last = order[bk[-1]]
+            bounds.append(offs[last] + (params[last].numel() + 63) // 64 * 64)
+        bounds[-1] = off
+        self.bucket_bounds = bounds
+        self.param_bucket = pb
+        self.reducer = None
+        if self.world > 1:
+            if broadcast:
+                broadcast_params([p.data for p in params] + list(module.buffers()), process_group)
+            self.reducer = make_arena_reducer(process_group, self.grad_arena, bounds, average)
+            self.reducer.set_param_map(pb)
+            self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i))
+                           for i, p in enumerate(params)]
+
+    def _make_hook(self, i):
+        def hook(_p):
+            self.reducer.mark_ready(i)
+        return hook
+
+    def forward(self, *a, **k):
+        if self.reducer is not None:
+            self.reducer.reset_iteration()
+        return self.module(*a, **k)
+
+    def finish_gradient_sync(self):
+        """Launch any bucket whose params got no grad, then wait for all."""
+        if self.reducer is not None:
+            self.reducer.launch_all()
+            self.reducer.wait_all()
+
+    def zero_grad(self, set_to_none: bool = False):
+        # grads must stay arena views: zero in place
+        self.grad_arena.zero_()
