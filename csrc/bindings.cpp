@@ -6,9 +6,18 @@
 
 namespace py = pybind11;
 
+namespace mdt {
+void probe_clock(at::Tensor out, int64_t iters);
+void probe_latency(at::Tensor idx, int64_t hops, at::Tensor out);
+void probe_empty(int64_t blocks, int64_t threads);
+}  // namespace mdt
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "multidisttorch_amd native runtime: HIP/CDNA4 kernels + C++ reducer";
   m.attr("ARCH") = "gfx950";
+  m.def("probe_clock", &mdt::probe_clock);
+  m.def("probe_latency", &mdt::probe_latency);
+  m.def("probe_empty", &mdt::probe_empty);
 
   py::class_<mdt::MlpVaeEngine>(m, "MlpVaeEngine")
       .def(py::init<int64_t, int64_t, int64_t, int64_t, int64_t>(), py::arg("batch"),
@@ -18,7 +27,7 @@ PYBIND11_MODULE(_C, m) {
       .def("bucket_split", &mdt::MlpVaeEngine::bucket_split)
       .def("set_hparams", &mdt::MlpVaeEngine::set_hparams, py::arg("lr"), py::arg("beta1"),
            py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("kl_beta"),
-           py::arg("grad_scale"), py::arg("seed"))
+           py::arg("grad_scale"), py::arg("seed"), py::arg("decoupled_wd") = false)
       .def("set_cursor", &mdt::MlpVaeEngine::set_cursor)
       .def("set_step", &mdt::MlpVaeEngine::set_step)
       .def("reset_loss", &mdt::MlpVaeEngine::reset_loss)
@@ -27,11 +36,12 @@ PYBIND11_MODULE(_C, m) {
       .def("forward", &mdt::MlpVaeEngine::forward, py::arg("X"), py::arg("idx"), py::arg("M"),
            py::arg("train"), py::arg("eval"), py::arg("rng_stream"), py::arg("want_recon"))
       .def("backward", &mdt::MlpVaeEngine::backward, py::arg("X"), py::arg("idx"), py::arg("M"),
-           py::arg("part") = 0)
-      .def("adam", &mdt::MlpVaeEngine::adam, py::arg("decoupled_wd") = false)
+           py::arg("part") = 0, py::arg("fuse_adam") = false)
+      .def("adam", &mdt::MlpVaeEngine::adam)
       .def("loss_finalize", &mdt::MlpVaeEngine::loss_finalize, py::arg("eval"))
       .def("act", &mdt::MlpVaeEngine::act)
       .def("decode", &mdt::MlpVaeEngine::decode)
+      .def("set_stamps", &mdt::MlpVaeEngine::set_stamps)
       .def_readonly("params", &mdt::MlpVaeEngine::params)
       .def_readonly("grads", &mdt::MlpVaeEngine::grads)
       .def_readonly("exp_avg", &mdt::MlpVaeEngine::exp_avg)

@@ -1,0 +1,51 @@
+// Hardware probes used by the profiling tools (multidisttorch_amd/obs/probe.py):
+// shader clock under load, dependent-load latency, empty-kernel cost.
+#include "common.h"
+
+namespace mdt {
+
+// One wave: shader-clock cycles (s_memtime) vs 100 MHz wall ticks (s_memrealtime)
+// around `iters` dependent FMAs -> effective SCLK in MHz.
+__global__ void probe_clock(unsigned long long* out, int iters) {
+  float x = (float)threadIdx.x;
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; ++i) x = fmaf(x, 1.0000001f, 0.5f);
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    out[0] = c1 - c0;
+    out[1] = r1 - r0;
+    out[2] = (unsigned long long)(x > 1e30f);  // keep x live
+  }
+}
+
+// One lane: pointer chase over `idx` (n hops) -> cycles per dependent load.
+__global__ void probe_latency(const int* idx, int hops, unsigned long long* out) {
+  if (threadIdx.x != 0) return;
+  int j = 0;
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < hops; ++i) j = idx[j];
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+  out[0] = c1 - c0;
+  out[1] = (unsigned long long)j;
+}
+
+__global__ void probe_empty() {}
+
+}  // namespace mdt
+
+extern "C" int mdt_probe_clock(unsigned long long* out, int iters, hipStream_t s) {
+  hipLaunchKernelGGL(mdt::probe_clock, dim3(1), dim3(64), 0, s, out, iters);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mdt_probe_latency(const int* idx, int hops, unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(mdt::probe_latency, dim3(1), dim3(64), 0, s, idx, hops, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mdt_probe_empty(int blocks, int threads, hipStream_t s) {
+  hipLaunchKernelGGL(mdt::probe_empty, dim3(blocks), dim3(threads), 0, s);
+  return (int)hipGetLastError();
+}

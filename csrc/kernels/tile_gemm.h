@@ -2,192 +2,327 @@
 // training GEMMs (M = batch = 128, N/K in {20, 40, 400, 784}).
 //
 // Design (MI355X-first, see docs/KERNELS.md):
-//  * one wave owns one 16x16 output tile and runs v_mfma_f32_16x16x4_f32
-//    (exact f32, same numerics class as the reference's fp32 addmm);
-//  * the k axis is consumed 16 at a time: lane (r = l&15, q = l>>4) loads
+//  * one wave owns one 16x16 output tile (or NT tiles sharing the A operand)
+//    and runs v_mfma_f32_16x16x4_f32 (exact f32: same numerics class as the
+//    reference's fp32 addmm);
+//  * the k axis is consumed 16 at a time: lane (r = l&15, q = l>>4) holds
 //    A(i0+r, k0+4q .. +3) and B(k0+4q .. +3, j0+r), which feed four MFMAs
 //    whose local k index q maps to global k = k0 + 4q + t. Contiguous-k
 //    operands load as one dwordx4 per lane;
-//  * two accumulators alternate so the 40-cycle dependent MFMA latency hides
-//    behind the 32-cycle issue interval;
-//  * operands are L2/MALL-resident (the whole MLP-VAE step touches < 12 MB),
-//    so LDS staging would only add a round trip: the loads go straight to
-//    VGPRs and the next k-chunk is prefetched in registers;
-//  * a block is 4 waves; KSPLIT waves share a tile (split-K, reduced through
-//    LDS) so small-N problems still put >= 200 workgroups on the 256 CUs.
+//  * the whole step is L2/MALL resident (< 12 MB), so time is set by load
+//    LATENCY (~870 cycles to MALL, measured by obs/probe.py), not bandwidth:
+//    a wave issues the loads of all NCW k-chunks it owns back to back (one
+//    round trip), then runs the MFMAs. The chunk loop has a compile-time trip
+//    count and no branches: out-of-range chunks / rows / columns load a
+//    clamped in-bounds address and are zeroed by a 0/1 multiplier, so hipcc
+//    never branches around a load (cdna_hip_programming.md §5 trap (c));
+//  * KSPLIT waves share a tile (split-K over waves, combined through LDS) so
+//    a 128-row problem spreads over ~200 workgroups, one load round each;
+//  * no __syncthreads() after global stores anywhere on the hot path: on
+//    gfx950 the barrier's implied vmcnt(0) waits for store acknowledgements
+//    (measured ~3 us with obs/stamps.py), so reductions go through per-wave
+//    partial slots instead.
 #pragma once
 #include "common.h"
 
 namespace mdt {
 
-// ----------------------------- A operand loaders ---------------------------
-// A(i, k). `row(i)` binds the lane's row once; `load(c, k0, out)` fetches
-// A(i, k0..k0+3) with zero fill outside [0,M) x [0,K).
+struct Frag {  // a lane's bound operand row/column
+  const float* base;
+  float mask;
+};
 
-struct ARowMajor {  // A(i,k) = p[i*ld + k]     (k contiguous)
+// ----------------------------- A operand loaders ---------------------------
+// A(i, k): row(i) binds the lane's row; load(f, k0, m, o) -> m * A(i, k0..k0+3).
+
+struct ARowMajor {  // A(i,k) = p[i*ld + k]  (k contiguous; K % 4 == 0)
   const float* p; int ld, M, K;
-  __device__ __forceinline__ const float* row(int i) const { return i < M ? p + (size_t)i * ld : nullptr; }
-  __device__ __forceinline__ void load(const float* c, int k0, float o[4]) const {
-    if (c && k0 + 3 < K) {
-      const float4 v = *reinterpret_cast<const float4*>(c + k0);
-      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-    } else {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) o[t] = (c && k0 + t < K) ? c[k0 + t] : 0.f;
-    }
+  __device__ __forceinline__ Frag row(int i) const {
+    return {p + (size_t)min(i, M - 1) * ld, i < M ? 1.f : 0.f};
+  }
+  __device__ __forceinline__ void load(const Frag& f, int k0, float m, float o[4]) const {
+    const float4 v = *reinterpret_cast<const float4*>(f.base + min(k0, K - 4));
+    m = (k0 < K) ? m * f.mask : 0.f;
+    o[0] = v.x * m; o[1] = v.y * m; o[2] = v.z * m; o[3] = v.w * m;
   }
 };
 
 struct ARowGather {  // A(i,k) = p[rows[i]*ld + k]  (sampler-indexed batch rows)
   const float* p; const int* rows; int ld, M, K;
-  __device__ __forceinline__ const float* row(int i) const {
-    return i < M ? p + (size_t)rows[i] * ld : nullptr;
+  __device__ __forceinline__ Frag row(int i) const {
+    return {p + (size_t)rows[min(i, M - 1)] * ld, i < M ? 1.f : 0.f};
   }
-  __device__ __forceinline__ void load(const float* c, int k0, float o[4]) const {
-    if (c && k0 + 3 < K) {
-      const float4 v = *reinterpret_cast<const float4*>(c + k0);
-      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-    } else {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) o[t] = (c && k0 + t < K) ? c[k0 + t] : 0.f;
-    }
+  __device__ __forceinline__ void load(const Frag& f, int k0, float m, float o[4]) const {
+    const float4 v = *reinterpret_cast<const float4*>(f.base + min(k0, K - 4));
+    m = (k0 < K) ? m * f.mask : 0.f;
+    o[0] = v.x * m; o[1] = v.y * m; o[2] = v.z * m; o[3] = v.w * m;
   }
 };
 
-struct ATrans {  // A(i,k) = p[k*ld + i]     (i contiguous: dY^T in weight grads)
+struct ATrans {  // A(i,k) = p[k*ld + i]  (i contiguous: dY^T in weight grads)
   const float* p; int ld, M, K;
-  __device__ __forceinline__ const float* row(int i) const { return i < M ? p + i : nullptr; }
-  __device__ __forceinline__ void load(const float* c, int k0, float o[4]) const {
+  // single element for the 32x32x2 path: lanes of equal k read 128 contiguous bytes
+  __device__ __forceinline__ float load1(const Frag& f, int k, float m) const {
+    return f.base[(size_t)min(k, K - 1) * ld] * (k < K ? m * f.mask : 0.f);
+  }
+  __device__ __forceinline__ Frag row(int i) const { return {p + min(i, M - 1), i < M ? 1.f : 0.f}; }
+  __device__ __forceinline__ void load(const Frag& f, int k0, float m, float o[4]) const {
+    m *= f.mask;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) o[t] = (c && k0 + t < K) ? c[(size_t)(k0 + t) * ld] : 0.f;
+    for (int t = 0; t < 4; ++t) {
+      const int k = k0 + t;
+      o[t] = f.base[(size_t)min(k, K - 1) * ld] * (k < K ? m : 0.f);
+    }
   }
 };
 
 // ----------------------------- B operand loaders ---------------------------
-// B(k, j). `col(j)` binds the lane's column; `load(c, k0, out)` -> B(k0..k0+3, j).
+// B(k, j): col(j) binds the lane's column; load(f, k0, o) -> B(k0..k0+3, j).
 
-struct BWeightNT {  // B(k,j) = W[j*ld + k]   (torch Linear weight [N,K], forward)
+struct BWeightNT {  // B(k,j) = W[j*ld + k]  (torch Linear weight [N,K]; K % 4 == 0)
   const float* p; int ld, N, K;
-  __device__ __forceinline__ const float* col(int j) const { return j < N ? p + (size_t)j * ld : nullptr; }
-  __device__ __forceinline__ void load(const float* c, int k0, float o[4]) const {
-    if (c && k0 + 3 < K) {
-      const float4 v = *reinterpret_cast<const float4*>(c + k0);
-      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-    } else {
+  __device__ __forceinline__ Frag col(int j) const {
+    return {p + (size_t)min(j, N - 1) * ld, j < N ? 1.f : 0.f};
+  }
+  __device__ __forceinline__ void load(const Frag& f, int k0, float o[4]) const {
+    const float4 v = *reinterpret_cast<const float4*>(f.base + min(k0, K - 4));
+    const float m = k0 < K ? f.mask : 0.f;
+    o[0] = v.x * m; o[1] = v.y * m; o[2] = v.z * m; o[3] = v.w * m;
+  }
+};
+
+struct BRowMajor {  // B(k,j) = p[k*ld + j]  (j contiguous)
+  const float* p; int ld, N, K;
+  __device__ __forceinline__ float load1(const Frag& f, int k) const {
+    return f.base[(size_t)min(k, K - 1) * ld] * (k < K ? f.mask : 0.f);
+  }
+  __device__ __forceinline__ Frag col(int j) const { return {p + min(j, N - 1), j < N ? 1.f : 0.f}; }
+  __device__ __forceinline__ void load(const Frag& f, int k0, float o[4]) const {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) o[t] = (c && k0 + t < K) ? c[k0 + t] : 0.f;
+    for (int t = 0; t < 4; ++t) {
+      const int k = k0 + t;
+      o[t] = f.base[(size_t)min(k, K - 1) * ld] * (k < K ? f.mask : 0.f);
     }
   }
 };
 
-struct BRowMajor {  // B(k,j) = p[k*ld + j]   (j contiguous)
-  const float* p; int ld, N, K;
-  __device__ __forceinline__ const float* col(int j) const { return j < N ? p + j : nullptr; }
-  __device__ __forceinline__ void load(const float* c, int k0, float o[4]) const {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) o[t] = (c && k0 + t < K) ? c[(size_t)(k0 + t) * ld] : 0.f;
-  }
-};
-
-struct BRowGather {  // B(k,j) = p[rows[k]*ld + j]
-  const float* p; const int* rows; int ld, N, K;
-  __device__ __forceinline__ const float* col(int j) const { return j < N ? p + j : nullptr; }
-  __device__ __forceinline__ void load(const float* c, int k0, float o[4]) const {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) o[t] = (c && k0 + t < K) ? c[(size_t)rows[k0 + t] * ld] : 0.f;
-  }
-};
-
-struct BOnes {  // B(k,j) = [j == 0] : turns a weight-grad tile into the bias-grad row sum
-  int K;
-  __device__ __forceinline__ const float* col(int j) const {
-    return j == 0 ? reinterpret_cast<const float*>(1) : nullptr;
-  }
-  __device__ __forceinline__ void load(const float* c, int k0, float o[4]) const {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) o[t] = (c && k0 + t < K) ? 1.f : 0.f;
-  }
-};
-
-// One wave: acc(16x16) = sum_{k in chunks [kc0,kc1)} A(i0.., k) B(k, j0..).
-template <class AL, class BL>
-__device__ __forceinline__ f32x4 wave_tile(const AL& A, const BL& B, int i0, int j0, int kc0, int kc1) {
+// NT tiles (rows i0.., columns j0 + t*jstride) over k-chunks [kc0, kc1), at
+// most NCW chunks per round; the A fragment is shared by the NT tiles.
+// Rounds are uniform (wave-level) and usually exactly one. With ROWSUM the
+// lane also accumulates sum_k A(i0 + (lane&15), k) over ITS k values (the
+// caller reduces across the 4 lane quarters): bias gradients for free.
+template <int NT, int NCW, bool ROWSUM = false, class AL, class BL>
+__device__ __forceinline__ void wave_tiles(const AL& A, const BL& B, int i0, int j0, int jstride,
+                                           int kc0, int kc1, f32x4 (&acc)[NT], float* rowsum = nullptr) {
   const int lane = lane_id();
   const int r = lane & 15, q = lane >> 4;
-  const float* ca = A.row(i0 + r);
-  const float* cb = B.col(j0 + r);
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f};
-  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
-  if (kc0 >= kc1) return acc0;
-  float a[4], b[4];
-  A.load(ca, kc0 * 16 + 4 * q, a);
-  B.load(cb, kc0 * 16 + 4 * q, b);
-  for (int kc = kc0; kc < kc1; ++kc) {
-    float an[4], bn[4];
-    const bool more = kc + 1 < kc1;
-    if (more) {
-      A.load(ca, (kc + 1) * 16 + 4 * q, an);
-      B.load(cb, (kc + 1) * 16 + 4 * q, bn);
-    }
-    acc0 = mfma16x16x4(a[0], b[0], acc0);
-    acc1 = mfma16x16x4(a[1], b[1], acc1);
-    acc0 = mfma16x16x4(a[2], b[2], acc0);
-    acc1 = mfma16x16x4(a[3], b[3], acc1);
-    if (more) {
+  const Frag fa = A.row(i0 + r);
+  Frag fb[NT];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) { a[t] = an[t]; b[t] = bn[t]; }
+  for (int t = 0; t < NT; ++t) fb[t] = B.col(j0 + t * jstride + r);
+  f32x4 acc2[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float rs = 0.f;
+  for (int kc = kc0; kc < kc1; kc += NCW) {
+    float a[NCW][4], b[NT][NCW][4];
+#pragma unroll
+    for (int u = 0; u < NCW; ++u) {
+      const int c = kc + u;
+      const int k0 = min(c, kc1 - 1) * 16 + 4 * q;
+      A.load(fa, k0, c < kc1 ? 1.f : 0.f, a[u]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) B.load(fb[t], k0, b[t][u]);
+    }
+#pragma unroll
+    for (int u = 0; u < NCW; ++u) {
+      if constexpr (ROWSUM) rs += (a[u][0] + a[u][1]) + (a[u][2] + a[u][3]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t] = mfma16x16x4(a[u][0], b[t][u][0], acc[t]);
+        acc2[t] = mfma16x16x4(a[u][1], b[t][u][1], acc2[t]);
+        acc[t] = mfma16x16x4(a[u][2], b[t][u][2], acc[t]);
+        acc2[t] = mfma16x16x4(a[u][3], b[t][u][3], acc2[t]);
+      }
     }
   }
-  return acc0 + acc1;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] += acc2[t];
+  if constexpr (ROWSUM) {
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    *rowsum = rs;
+  }
 }
 
-// Block of 4 waves over a tiled problem. TPB tiles per block, KSPLIT = 4/TPB
-// waves per tile. Tile t -> (ti, tj) row-major over tiles_j columns; when
-// `bias_tj >= 0` the tile column `bias_tj` is a bias-grad column computed with
-// BOnes. Epilogue signature: float epi(i, j, v, is_bias) -> contribution to a
-// block-level sum (returned in wave 0 lane 0 by the caller's reduction).
-// `lds` must hold 4*256 floats.
-template <int TPB, class AL, class BL, class EPI>
+template <int NCW, class AL, class BL>
+__device__ __forceinline__ f32x4 wave_tile(const AL& A, const BL& B, int i0, int j0, int kc0, int kc1) {
+  f32x4 acc[1];
+  wave_tiles<1, NCW>(A, B, i0, j0, 0, kc0, kc1, acc);
+  return acc[0];
+}
+
+// Block of WAVES waves over a tiled problem. A wave job = (row tile ti, group
+// of NT adjacent 16-column tiles). TPB jobs per block, KSPLIT = WAVES/TPB
+// waves per job (split-K combined through LDS). Epilogue: a functor with
+// `template <int N> float run(const int (&rows)[N], int col, const float (&v)[N])`
+// called once per fragment column (all loads issued before any store, so the
+// fragment costs one memory round trip), and with ROWSUM (KSPLIT == 1 only)
+// run<1>({i}, -1, {rowsum}) once per row from the jobs of column group 0. Returns the wave's summed epilogue
+// contributions (leader waves only). `lds` must hold WAVES*256 floats; the
+// only barrier precedes every store.
+template <int WAVES, int TPB, int NT, int NCW, bool ROWSUM, class AL, class BL, class EPI>
 __device__ __forceinline__ float gemm_tiles(const AL& A, const BL& B, EPI& epi, int K, int tiles_i,
-                                            int tiles_j, int bias_tj, int blk, float* lds) {
-  constexpr int KSPLIT = 4 / TPB;
-  const int w = wave_id();
+                                            int tiles_j, int blk, float* lds) {
+  constexpr int KSPLIT = WAVES / TPB;
+  static_assert(KSPLIT * TPB == WAVES, "WAVES must be a multiple of TPB");
+  static_assert(!ROWSUM || KSPLIT == 1, "ROWSUM needs whole-K waves");
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
   const int lane = lane_id();
-  const int tile = blk * TPB + w / KSPLIT;
+  const int groups_j = (tiles_j + NT - 1) / NT;
+  const int njobs = tiles_i * groups_j;
+  const int job = blk * TPB + w / KSPLIT;
   const int ks = w % KSPLIT;
-  const int ntiles = tiles_i * tiles_j;
   const int nch = (K + 15) >> 4;
   const int kc0 = (ks * nch) / KSPLIT, kc1 = ((ks + 1) * nch) / KSPLIT;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  int ti = 0, tj = 0;
-  const bool live = tile < ntiles;
-  if (live) {
-    ti = tile / tiles_j;
-    tj = tile - ti * tiles_j;
-    if (tj == bias_tj) acc = wave_tile(A, BOnes{K}, ti * 16, 0, kc0, kc1);
-    else acc = wave_tile(A, B, ti * 16, tj * 16, kc0, kc1);
-  }
+  const bool live = job < njobs;
+  const int jj = live ? job : njobs - 1;  // dead waves compute a real job, never store it
+  const int ti = jj / groups_j;
+  const int tg = jj - ti * groups_j;
+  f32x4 acc[NT];
+  float rs = 0.f;
+  wave_tiles<NT, NCW, ROWSUM>(A, B, ti * 16, tg * NT * 16, 16, kc0, kc1, acc, &rs);
   if constexpr (KSPLIT > 1) {
-    float* mine = lds + w * 256 + lane * 4;
-    mine[0] = acc[0]; mine[1] = acc[1]; mine[2] = acc[2]; mine[3] = acc[3];
+    static_assert(NT == 1, "split-K reduction implemented for NT == 1");
+    *reinterpret_cast<f32x4*>(lds + w * 256 + lane * 4) = acc[0];
     __syncthreads();
     if (ks == 0) {
 #pragma unroll
-      for (int s = 1; s < KSPLIT; ++s) {
-        const float* o = lds + (w + s) * 256 + lane * 4;
-        acc[0] += o[0]; acc[1] += o[1]; acc[2] += o[2]; acc[3] += o[3];
-      }
+      for (int s = 1; s < KSPLIT; ++s) acc[0] += *reinterpret_cast<const f32x4*>(lds + (w + s) * 256 + lane * 4);
     }
   }
   float contrib = 0.f;
   if (live && ks == 0) {
-    const bool is_bias = (tj == bias_tj);
-    const int col = (is_bias ? 0 : tj * 16) + (lane & 15);
     const int row0 = ti * 16 + 4 * (lane >> 4);
+    const int rows[4] = {row0, row0 + 1, row0 + 2, row0 + 3};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) contrib += epi(row0 + r, col, acc[r], is_bias);
+    for (int t = 0; t < NT; ++t) {
+      const int col = (tg * NT + t) * 16 + (lane & 15);
+      const float v[4] = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
+      contrib += epi.template run<4>(rows, col, v);
+    }
+    if constexpr (ROWSUM) {
+      if (tg == 0 && (lane >> 4) == 0) {
+        const int rr[1] = {ti * 16 + (lane & 15)};
+        const float vv[1] = {rs};
+        contrib += epi.template run<1>(rr, -1, vv);
+      }
+    }
   }
   return contrib;
+}
+
+// ---------------------------------------------------------------------------
+// Weight-gradient GEMMs dW[i, j] = sum_k A(i, k) B(k, j) with k = batch: both
+// operands are batch-major (k is the SLOW index), so 16x16x4 fragments would
+// need 4 strided dword loads per chunk. v_mfma_f32_32x32x2_f32 takes ONE f32
+// per operand per lane with lanes 0-31 spanning i (resp. j) at fixed k: every
+// load instruction reads two fully used 128-byte rows. A wave owns a 32x32
+// tile over a k-slice of NPW pairs (2 k per MFMA); KSPLIT waves per tile are
+// combined through LDS. With ROWSUM the A values give the bias row sums.
+template <int NPW, bool ROWSUM, class AL, class BL>
+__device__ __forceinline__ f32x16 wave_tile32(const AL& A, const BL& B, int i0, int j0, int kp0, int kp1,
+                                              float* rowsum) {
+  const int lane = lane_id();
+  const int r = lane & 31, h = lane >> 5;
+  const Frag fa = A.row(i0 + r);
+  const Frag fb = B.col(j0 + r);
+  f32x16 acc0 = {}, acc1 = {};
+  float rs = 0.f;
+  for (int kp = kp0; kp < kp1; kp += NPW) {
+    float a[NPW], b[NPW];
+#pragma unroll
+    for (int u = 0; u < NPW; ++u) {
+      const int p = kp + u;
+      const int k = min(p, kp1 - 1) * 2 + h;
+      a[u] = A.load1(fa, k, p < kp1 ? 1.f : 0.f);
+      b[u] = B.load1(fb, k);
+    }
+#pragma unroll
+    for (int u = 0; u < NPW; u += 2) {
+      acc0 = mfma32x32x2(a[u], b[u], acc0);
+      if (u + 1 < NPW) acc1 = mfma32x32x2(a[u + 1], b[u + 1], acc1);
+    }
+    if constexpr (ROWSUM) {
+#pragma unroll
+      for (int u = 0; u < NPW; ++u) rs += a[u];
+    }
+  }
+  if constexpr (ROWSUM) {
+    rs += __shfl_xor(rs, 32, 64);
+    *rowsum = rs;
+  }
+  return acc0 + acc1;
+}
+
+// Block of WAVES waves: TPB 32x32 tiles per block, KSPLIT = WAVES/TPB waves
+// per tile. Epilogue run<16>(rows, col, v) per lane (see gemm_tiles); with
+// ROWSUM run<1>({i}, -1, {rowsum}) from the tiles of column 0. `lds` must hold WAVES*1024 floats.
+template <int WAVES, int TPB, int NPW, bool ROWSUM, class AL, class BL, class EPI>
+__device__ __forceinline__ void gemm_tiles32(const AL& A, const BL& B, EPI& epi, int K, int tiles_i,
+                                             int tiles_j, int blk, float* lds) {
+  constexpr int KSPLIT = WAVES / TPB;
+  static_assert(KSPLIT * TPB == WAVES, "WAVES must be a multiple of TPB");
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  const int lane = lane_id();
+  const int ntiles = tiles_i * tiles_j;
+  const int tile = blk * TPB + w / KSPLIT;
+  const int ks = w % KSPLIT;
+  const int npairs = (K + 1) >> 1;
+  const int kp0 = (ks * npairs) / KSPLIT, kp1 = ((ks + 1) * npairs) / KSPLIT;
+  const bool live = tile < ntiles;
+  const int tt = live ? tile : ntiles - 1;
+  const int ti = tt / tiles_j, tj = tt - ti * tiles_j;
+  float rs = 0.f;
+  f32x16 acc = wave_tile32<NPW, ROWSUM>(A, B, ti * 32, tj * 32, kp0, kp1, &rs);
+  if constexpr (KSPLIT > 1) {
+    float* mine = lds + w * 1024 + lane * 16;
+#pragma unroll
+    for (int v = 0; v < 16; v += 4) *reinterpret_cast<f32x4*>(mine + v) = f32x4{acc[v], acc[v + 1], acc[v + 2], acc[v + 3]};
+    if constexpr (ROWSUM) lds[WAVES * 1024 + w * 64 + lane] = rs;
+    __syncthreads();
+    if (ks == 0) {
+#pragma unroll
+      for (int s = 1; s < KSPLIT; ++s) {
+        const float* o = lds + (w + s) * 1024 + lane * 16;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[v] += o[v];
+        if constexpr (ROWSUM) rs += lds[WAVES * 1024 + (w + s) * 64 + lane];
+      }
+    }
+  }
+  if (live && ks == 0) {
+    const int col = tj * 32 + (lane & 31);
+    const int rb = ti * 32 + 4 * (lane >> 5);
+    int rows[16];
+    float vals[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      rows[v] = rb + (v & 3) + 8 * (v >> 2);
+      vals[v] = acc[v];
+    }
+    epi.template run<16>(rows, col, vals);
+    if constexpr (ROWSUM) {
+      if (tj == 0 && (lane >> 5) == 0) {
+        const int rr[1] = {ti * 32 + lane};
+        const float vv[1] = {rs};
+        epi.template run<1>(rr, -1, vv);
+      }
+    }
+  }
 }
 
 }  // namespace mdt

@@ -6,20 +6,25 @@
 namespace mdt {
 
 constexpr int kMaxBatch = 4096;
-constexpr int kKldPartial = 0;      // F2 blocks write [0, 256)
-constexpr int kBcePartial = 256;    // F3 blocks write [256, kPartials)
-constexpr int kPartials = 256 + 8192;
+constexpr int kKldPartial = 0;      // F2 waves write [0, 2048)  (8 per block)
+constexpr int kBcePartial = 2048;   // F3 waves write [2048, kPartials) (8 per block)
+constexpr int kPartials = 2048 + 65536;
 constexpr int kLossHist = 4096;     // per-step loss ring (host reads at log points)
 
-// Device-resident training state of one trial (64-byte aligned, memset to 0).
+// Device-resident training state of one trial (memset to 0 at creation).
+//
+// Advance protocol (no atomics, no extra launch): within one step
+//   F1 block 0 increments `step`   (F1 never reads step),
+//   F2 block 0 advances `cursor`   (F2 never reads cursor; F1 already copied
+//                                    the batch rows into the xb buffer that
+//                                    F3/B3 read).
+// So `step` counts steps started: the RNG counter of the running step is
+// step-1 and Adam's 1-based t is step.
 struct TrainState {
-  int64_t step;        // optimizer steps taken (Adam t = step + 1; RNG counter)
+  int64_t step;
   int32_t cursor;      // batch index within the epoch's index list
   int32_t nbatches;    // cursor wraps at this value
-  uint32_t ticket;     // arrival counter for the optimizer's last-block finalize
-  int32_t nparts_kld;  // partial slots written by the last forward (F2 blocks)
-  int32_t nparts_bce;  // partial slots written by the last forward (F3 blocks)
-  int32_t pad0;
+  double b1pow, b2pow; // beta1^step, beta2^step (Adam bias corrections; F1 advances them)
   double epoch_loss;   // running sum of per-batch losses since the host reset it
   double epoch_count;  // batches accumulated in epoch_loss
   float loss_hist[kLossHist];
@@ -28,32 +33,42 @@ struct TrainState {
 // Per-trial hyper-parameters, device-resident so a captured graph picks up
 // lr/beta changes (schedules, HPO perturbation) without re-capture.
 struct HParams {
-  float lr, beta1, beta2, eps, weight_decay, kl_beta, grad_scale, pad;
+  float lr, beta1, beta2, eps, weight_decay, kl_beta, grad_scale;
+  int32_t decoupled_wd;
   uint32_t seed_lo, seed_hi;
-  uint32_t pad2[6];
+  double lr_d, beta1_d, beta2_d;  // double copies: torch computes lr/bc1 in double
 };
 
 struct VaeArgs {
   int M, B, D, H, Z;
   uint32_t rng_stream;   // distinguishes replicas / eval draws
   int train;             // 1: write backward intermediates
-  int pad;
+  int fuse_adam;         // 1: B3 applies Adam in its epilogues (+ streams the rest)
   const float* X;        // dataset [N, D]
   const int* idx;        // epoch index list [nbatches * B] (+ tail)
   const float *W1, *b1, *W2, *b2, *W3, *b3, *W4, *b4;
   float *gW1, *gb1, *gW2, *gb2, *gW3, *gb3, *gW4, *gb4;
-  float *h1, *mulv, *eps, *z, *h3, *dlog, *dh3, *dmulv, *dh1;
+  float *h1, *mulv, *eps, *z, *h3, *dlog, *dh3, *dmulv, *dh1, *xb;
   float* recon;          // optional sigmoid output [M, D] (eval / images)
   float* partials;       // [kPartials]
   TrainState* st;
   const HParams* hp;
+  // optimizer arenas (fused Adam): param / grad / exp_avg / exp_avg_sq base
+  float *P, *G, *Mo, *Vo;
+  long long oW1, ob1, oW2, ob2;   // arena offsets of the epilogue-updated tensors
+  long long s_beg, s_end;         // arena range Adam-streamed by B3 (fc3, fc4)
+  unsigned long long* stamps;     // optional phase timestamps (profiling builds of a run)
 };
+
+// stamps[((kernel*kStampBlocks + block)*8 + wave)*8 + slot] = s_memrealtime (100 MHz)
+constexpr int kStampBlocks = 512;
+constexpr int kStampKernels = 6;
 
 struct VaeGrid {
-  int f1, f2, f3, b1, b1_dh3, b2, b2_rows, b3, b3_w2;
+  int f1, f2, f3, b1, b1_dh3, b2, b2_rows, b3, b3_w2, b3_w1, b3_stream;
 };
 
-VaeGrid vae_grid(int M, int D, int H, int Z);
+VaeGrid vae_grid(const VaeArgs& a);
 
 }  // namespace mdt
 

@@ -1,267 +1,391 @@
 // Fused MLP-VAE training step for MI355X (gfx950).
 //
 // Model (parity: /root/reference/vae-hpo.py:19-58): fc1 D->H, fc21/fc22 H->Z,
-// fc3 Z->H, fc4 H->D, ELBO = BCE(sum) + beta*KLD.  The whole step is seven
-// launches (captured in one hipGraph by the runtime):
+// fc3 Z->H, fc4 H->D, ELBO = BCE(sum) + beta*KLD. The whole step is six
+// launches (captured in one hipGraph by the runtime), 512-thread workgroups:
 //
-//   F1  h1    = relu(X[rows] W1^T + b1)                       MFMA f32, split-K 4
+//   F1  h1 = relu(X[rows] W1^T + b1) ; copy batch rows -> xb ; step++
 //   F2  [mu|lv] = h1 W2^T + b2 ; z = mu + eps*exp(lv/2) (Philox) ; KLD partial ;
-//       h3 = relu(z W3^T + b3)                                 16 rows / block
+//       h3 = relu(z W3^T + b3) ; cursor++                     (16 rows / block)
 //   F3  logits = h3 W4^T + b4 ; dlogits = sigmoid - x ; BCE partial (logit form)
 //   B1  dh3 = (dlogits W4) . [h3>0]    ||  dW4 = dlogits^T h3, db4
 //   B2  dz = dh3 W3 -> dmu, dlv (reparam + beta-KLD) ; dh1 = ([dmu|dlv] W2) . [h1>0]
-//                                      ||  dW3 = dh3^T z, db3
-//   B3  dW2 = [dmu|dlv]^T h1, db2      ||  dW1 = dh1^T X[rows], db1
-//   (+ bucketed all-reduce on the comm stream, then fused Adam: adam.hip)
+//                                      ||  dW3 = dh3^T z, db3  || loss reduction
+//   B3  dW2 = [dmu|dlv]^T h1, db2      ||  dW1 = dh1^T xb, db1
+//       with fuse_adam: Adam applied in those epilogues, + Adam streamed over
+//       the fc3/fc4 slice of the arena (gradients final since B1/B2). Without
+//       it (intra-group DDP), the bucketed all-reduce runs on the comm stream
+//       and adam.hip updates the whole arena afterwards.
 //
 // Gradients are written (not accumulated) straight into the flat gradient
-// arena, so there is no zero_grad and no bucket copy-back. The batch rows are
-// gathered by sampler index inside F1/F3/B3 (no host collate, no H2D copy).
-// The batch cursor and step counter are device-resident so one captured graph
-// replays over an entire epoch.
+// arena: no zero_grad, no bucket copy-back. The batch rows are gathered by
+// sampler index inside F1 (no host collate, no H2D copy). The batch cursor
+// and step counter are device-resident (see TrainState), so one captured
+// graph replays over an entire epoch.
 #include "common.h"
 #include "tile_gemm.h"
 #include "vae_mlp.h"
+#include "adam_common.h"
 
 namespace mdt {
 
-__device__ __forceinline__ const int* batch_rows(const VaeArgs& a) {
-  return a.idx + (size_t)a.st->cursor * a.B;
-}
+constexpr int kWaves = 8;
+constexpr int kThreads = kWaves * 64;
+
+__device__ __forceinline__ int cdiv_d(int a, int b) { return (a + b - 1) / b; }
+
+// Phase timestamps for the profiling tool (obs/stamps.py); a null pointer
+// (production) costs one uniform branch.
+#define STAMP(K, S)                                                                         \
+  do {                                                                                      \
+    if (a.stamps && lane_id() == 0 && blockIdx.x < kStampBlocks)                            \
+      a.stamps[(((size_t)(K) * kStampBlocks + blockIdx.x) * 8 + wave_id()) * 8 + (S)] =     \
+          __builtin_amdgcn_s_memrealtime();                                                 \
+  } while (0)
 
 // ------------------------------------------------------------------- F1 ----
+// Epilogues: `run<N>` receives one lane's N outputs of one column; every load
+// is issued before the first store (one round trip per fragment).
 struct EpiBiasRelu {
   float* out; const float* bias; int ld, M, N;
-  __device__ __forceinline__ float operator()(int i, int j, float v, bool) const {
-    if (i < M && j < N) out[(size_t)i * ld + j] = fmaxf(v + bias[j], 0.f);
+  template <int R>
+  __device__ __forceinline__ float run(const int (&rows)[R], int j, const float (&v)[R]) const {
+    if (j >= N) return 0.f;
+    const float b = bias[j];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (rows[r] < M) out[(size_t)rows[r] * ld + j] = fmaxf(v[r] + b, 0.f);
     return 0.f;
   }
 };
 
-__global__ void __launch_bounds__(256) vae_f1(VaeArgs a) {
-  __shared__ float lds[4 * 256];
-  const int* rows = batch_rows(a);
+// One block = one 16x16 tile of h1, its K = D split over the 8 waves.
+__global__ void __launch_bounds__(kThreads) vae_f1(VaeArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[kWaves * 256];
+  STAMP(0, 0);
+  const int* rows = a.idx + (size_t)a.st->cursor * a.B;
   ARowGather A{a.X, rows, a.D, a.M, a.D};
   BWeightNT Bw{a.W1, a.D, a.H, a.D};
   EpiBiasRelu epi{a.h1, a.b1, a.H, a.M, a.H};
-  gemm_tiles<1>(A, Bw, epi, a.D, (a.M + 15) / 16, (a.H + 15) / 16, -1, blockIdx.x, lds);
+  const int tiles_j = cdiv_d(a.H, 16);
+  gemm_tiles<kWaves, 1, 1, 7, false>(A, Bw, epi, a.D, cdiv_d(a.M, 16), tiles_j, blockIdx.x, lds);
+  STAMP(0, 1);
+  // blocks of tile column 0 materialise their 16 batch rows into xb for F3/B3
+  // (each wave re-reads the K slice it just loaded: L1/L2 hits, no barrier)
+  if ((int)blockIdx.x % tiles_j == 0) {
+    const int w = wave_id(), lane = lane_id();
+    const int i = ((int)blockIdx.x / tiles_j) * 16 + (lane & 15);
+    const int nch = cdiv_d(a.D, 16);
+    const int kc0 = (w * nch) / kWaves, kc1 = ((w + 1) * nch) / kWaves;
+    if (i < a.M) {
+      const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)rows[i] * a.D);
+      float4* dst = reinterpret_cast<float4*>(a.xb + (size_t)i * a.D);
+      for (int c = kc0; c < kc1; ++c) {
+        const int k4 = c * 4 + (lane >> 4);
+        if (k4 * 4 < a.D) dst[k4] = src[k4];
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    TrainState* st = a.st;
+    st->step = st->step + 1;
+    st->b1pow = st->b1pow * a.hp->beta1_d;
+    st->b2pow = st->b2pow * a.hp->beta2_d;
+  }
+  STAMP(0, 2);
 }
 
 // ------------------------------------------------------------------- F2 ----
-// One block = 16 batch rows. Stage A: [mu|lv](16 x 2Z) = h1 W2^T, split over 4
-// waves along k. Stage B: reparameterise + KLD. Stage C: h3 = relu(z W3^T + b3).
-// Requires Z <= 32 (2Z <= 64 -> <= 4 n-tiles).
-__global__ void __launch_bounds__(256) vae_f2(VaeArgs a) {
-  __shared__ float red[4][4][256];   // [wave][ntile][lane*4+r]
-  __shared__ float zt[16][36];       // z tile (row-major, k padded)
-  __shared__ float scratch[16];
-  const int w = wave_id(), lane = lane_id();
+// One block = 16 batch rows, 8 waves. Stage A: [mu|lv] (16 x 2Z) = h1 W2^T,
+// each wave one k-slice of all n-tiles. Stage B: reparameterise + KLD.
+// Stage C: h3 = relu(z W3^T + b3), n-tiles strided over the waves. All global
+// stores are issued after the last barrier. Requires Z <= 32, Z % 4 == 0.
+__global__ void __launch_bounds__(kThreads) vae_f2(VaeArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[kWaves][4][256];
+  __shared__ __attribute__((aligned(16))) float zt[16][36];
+  const int w = __builtin_amdgcn_readfirstlane(wave_id()), lane = lane_id();
   const int i0 = blockIdx.x * 16;
   const int Z2 = 2 * a.Z;
-  const int ntj = (Z2 + 15) / 16;
-  // Stage A
+  STAMP(1, 0);
   {
     ARowMajor A{a.h1, a.H, a.M, a.H};
     BWeightNT Bw{a.W2, a.H, Z2, a.H};
-    const int nch = (a.H + 15) / 16;
-    const int kc0 = (w * nch) / 4, kc1 = ((w + 1) * nch) / 4;
-    for (int tj = 0; tj < 4; ++tj) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      if (tj < ntj) acc = wave_tile(A, Bw, i0, tj * 16, kc0, kc1);
-      float* m = &red[w][tj][lane * 4];
-      m[0] = acc[0]; m[1] = acc[1]; m[2] = acc[2]; m[3] = acc[3];
-    }
+    const int nch = cdiv_d(a.H, 16);
+    const int kc0 = (w * nch) / kWaves, kc1 = ((w + 1) * nch) / kWaves;
+    f32x4 acc[4];
+    wave_tiles<4, 4>(A, Bw, i0, 0, 16, kc0, kc1, acc);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(&red[w][t][lane * 4]) = acc[t];
   }
+  STAMP(1, 1);
   __syncthreads();
-  // Stage B: thread t -> (row r = t / Z, latent c = t % Z), loop over 16*Z.
-  float kld = 0.f;
-  const uint32_t step_lo = (uint32_t)(a.st->step & 0xffffffffu);
-  const uint32_t step_hi = (uint32_t)((uint64_t)a.st->step >> 32);
-  for (int e = threadIdx.x; e < 16 * a.Z; e += blockDim.x) {
-    const int r = e / a.Z, c = e - r * a.Z;
-    const int i = i0 + r;
-    // fetch accumulated value of output column col for row r from red[][][]
+  // Stage B: one (row, latent) element per thread (16*Z <= 512)
+  const long long stp = a.st->step - 1;  // F1 of this step already incremented it
+  const uint32_t step_lo = (uint32_t)((unsigned long long)stp & 0xffffffffu);
+  const uint32_t step_hi = (uint32_t)((unsigned long long)stp >> 32);
+  const int e = threadIdx.x;
+  const int r = e / a.Z, c = e - r * a.Z;
+  const int i = i0 + r;
+  const bool mine = e < 16 * a.Z;
+  const bool valid = mine && i < a.M;
+  float mu = 0.f, lv = 0.f, ep = 0.f, zz = 0.f, kld = 0.f;
+  if (mine) {
     auto acc_at = [&](int col) {
       const int tj = col >> 4, cc = col & 15;
       const int l = ((r >> 2) << 4) + cc;  // lane holding (row r, col cc)
       const int rr = r & 3;
-      return red[0][tj][l * 4 + rr] + red[1][tj][l * 4 + rr] + red[2][tj][l * 4 + rr] +
-             red[3][tj][l * 4 + rr];
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) s += red[ww][tj][l * 4 + rr];
+      return s;
     };
-    float zz = 0.f;
-    if (i < a.M) {
-      const float mu = acc_at(c) + a.b2[c];
-      const float lv = acc_at(a.Z + c) + a.b2[a.Z + c];
-      const float sd = expf(0.5f * lv);
-      // counter: (row*Z + c, step) keyed by the trial seed; the sampler row id
-      // is deliberately NOT used so replicas of one group draw independent eps
-      // only through their seed (parity with per-process randn_like streams).
-      const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(i * a.Z + c), a.rng_stream, step_lo, step_hi},
-                                       a.hp->seed_lo, a.hp->seed_hi);
-      const float ep = normal_from_bits(bits.x, bits.y);
-      zz = mu + ep * sd;
-      const size_t o = (size_t)i * Z2;
-      a.mulv[o + c] = mu;
-      a.mulv[o + a.Z + c] = lv;
-      a.eps[(size_t)i * a.Z + c] = ep;
-      a.z[(size_t)i * a.Z + c] = zz;
-      kld += 1.f + lv - mu * mu - sd * sd;
-    }
+    mu = acc_at(c) + a.b2[c];
+    lv = acc_at(a.Z + c) + a.b2[a.Z + c];
+    const float sd = expf(0.5f * lv);
+    // counter (row*Z + c, stream, step): replicas of a group differ by
+    // `rng_stream` (like per-process randn_like streams in the reference)
+    const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(i * a.Z + c), a.rng_stream, step_lo, step_hi},
+                                     a.hp->seed_lo, a.hp->seed_hi);
+    ep = normal_from_bits(bits.x, bits.y);
+    zz = valid ? mu + ep * sd : 0.f;
+    kld = valid ? 1.f + lv - mu * mu - sd * sd : 0.f;
     zt[r][c] = zz;
   }
-  // pad k columns of z up to a multiple of 4 with zeros (ARowMajor over LDS)
-  for (int e = threadIdx.x; e < 16 * 36; e += blockDim.x) {
-    const int r = e / 36, c = e % 36;
-    if (c >= a.Z) zt[r][c] = 0.f;
-  }
-  const float ks = block_sum(kld, scratch);
-  if (threadIdx.x == 0) a.partials[kKldPartial + blockIdx.x] = -0.5f * ks;
+  kld = wave_sum(kld);
   __syncthreads();
-  // Stage C: h3 tiles; z from LDS (k = Z <= 32 -> two 16-chunks max)
+  STAMP(1, 2);
   {
-    const int ntiles = (a.H + 15) / 16;
-    const int r = lane & 15, q = lane >> 4;
-    for (int tj = w; tj < ntiles; tj += 4) {
-      const int j = tj * 16 + r;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* wrow = j < a.H ? a.W3 + (size_t)j * a.Z : nullptr;
-      for (int k0 = 0; k0 < a.Z; k0 += 16) {
+    ARowMajor Az{&zt[0][0], 36, 16, a.Z};
+    BWeightNT Bw{a.W3, a.Z, a.H, a.Z};
+    f32x4 acc[4];
+    wave_tiles<4, 2>(Az, Bw, 0, w * 16, kWaves * 16, 0, cdiv_d(a.Z, 16), acc);
+    const int q = lane >> 4;
+    float bj[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int k = k0 + 4 * q + t;
-          const float av = (k < a.Z) ? zt[r][k] : 0.f;
-          const float bv = (wrow && k < a.Z) ? wrow[k] : 0.f;
-          acc = mfma16x16x4(av, bv, acc);
-        }
-      }
-      const int row0 = i0 + 4 * q;
-      const int col = j;
-      if (col < a.H) {
+    for (int t = 0; t < 4; ++t) bj[t] = a.b3[min((w + t * kWaves) * 16 + (lane & 15), a.H - 1)];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = (w + t * kWaves) * 16 + (lane & 15);
+      if (j < a.H) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int i = row0 + rr;
-          if (i < a.M) a.h3[(size_t)i * a.H + col] = fmaxf(acc[rr] + a.b3[col], 0.f);
+          const int ii = i0 + 4 * q + rr;
+          if (ii < a.M) a.h3[(size_t)ii * a.H + j] = fmaxf(acc[t][rr] + bj[t], 0.f);
         }
       }
     }
   }
+  // deferred stores of stage B
+  if (valid) {
+    const size_t o = (size_t)i * Z2;
+    a.mulv[o + c] = mu;
+    a.mulv[o + a.Z + c] = lv;
+    a.eps[(size_t)i * a.Z + c] = ep;
+    a.z[(size_t)i * a.Z + c] = zz;
+  }
+  if (lane == 0) a.partials[kKldPartial + blockIdx.x * kWaves + w] = -0.5f * kld;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int cur = a.st->cursor + 1;
+    if (a.st->nbatches > 0 && cur >= a.st->nbatches) cur = 0;
+    a.st->cursor = cur;
+  }
+  STAMP(1, 3);
 }
 
 // ------------------------------------------------------------------- F3 ----
 struct EpiBce {
-  const float* X; const int* rows; const float* bias; float* dlog; float* recon;
+  const float* xb; const float* bias; float* dlog; float* recon;
   int D, M, train;
-  __device__ __forceinline__ float operator()(int i, int j, float v, bool) const {
-    if (i >= M || j >= D) return 0.f;
-    const float t = v + bias[j];
-    const float x = X[(size_t)rows[i] * D + j];
-    const float p = 1.f / (1.f + expf(-t));
-    if (train) dlog[(size_t)i * D + j] = p - x;
-    if (recon) recon[(size_t)i * D + j] = p;
-    // -[x log p + (1-x) log(1-p)] in the overflow-free logit form, with the
-    // reference's log clamp at -100 (torch binary_cross_entropy) preserved.
-    const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));  // -log(1-p)
-    const float sp_neg = sp_pos - t;                                 // -log p
-    return x * fminf(sp_neg, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
+  template <int R>
+  __device__ __forceinline__ float run(const int (&rows)[R], int j, const float (&v)[R]) const {
+    if (j >= D) return 0.f;
+    const float b = bias[j];
+    float x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = xb[(size_t)min(rows[r], M - 1) * D + j];
+    float loss = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (rows[r] >= M) continue;
+      const float t = v[r] + b;
+      const size_t o = (size_t)rows[r] * D + j;
+      const float p = 1.f / (1.f + expf(-t));
+      if (train) dlog[o] = p - x[r];
+      if (recon) recon[o] = p;
+      // -[x log p + (1-x) log(1-p)] in the overflow-free logit form, with the
+      // reference's log clamp at -100 (torch binary_cross_entropy) preserved.
+      const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));  // -log(1-p)
+      const float sp_neg = sp_pos - t;                                 // -log p
+      loss += x[r] * fminf(sp_neg, 100.f) + (1.f - x[r]) * fminf(sp_pos, 100.f);
+    }
+    return loss;
   }
 };
 
-__global__ void __launch_bounds__(256) vae_f3(VaeArgs a) {
-  __shared__ float lds[4 * 256];
-  __shared__ float scratch[16];
-  const int* rows = batch_rows(a);
+__global__ void __launch_bounds__(kThreads) vae_f3(VaeArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[kWaves * 256];
+  STAMP(2, 0);
   ARowMajor A{a.h3, a.H, a.M, a.H};
   BWeightNT Bw{a.W4, a.H, a.D, a.H};
-  EpiBce epi{a.X, rows, a.b4, a.dlog, a.recon, a.D, a.M, a.train};
-  const float c = gemm_tiles<2>(A, Bw, epi, a.H, (a.M + 15) / 16, (a.D + 15) / 16, -1, blockIdx.x, lds);
-  const float s = block_sum(c, scratch);
-  if (threadIdx.x == 0) a.partials[kBcePartial + blockIdx.x] = s;
+  EpiBce epi{a.xb, a.b4, a.dlog, a.recon, a.D, a.M, a.train};
+  const float c = gemm_tiles<kWaves, 2, 1, 7, false>(A, Bw, epi, a.H, cdiv_d(a.M, 16), cdiv_d(a.D, 16),
+                                                     blockIdx.x, lds);
+  const float s = wave_sum(c);
+  if (lane_id() == 0) a.partials[kBcePartial + blockIdx.x * kWaves + wave_id()] = s;
+  STAMP(2, 1);
 }
 
 // ------------------------------------------------------------------- B1 ----
 struct EpiMask {
   float* out; const float* mask; int ld, M, N;
-  __device__ __forceinline__ float operator()(int i, int j, float v, bool) const {
-    if (i < M && j < N) {
-      const size_t o = (size_t)i * ld + j;
-      out[o] = mask[o] > 0.f ? v : 0.f;
-    }
+  template <int R>
+  __device__ __forceinline__ float run(const int (&rows)[R], int j, const float (&v)[R]) const {
+    if (j >= N) return 0.f;
+    float mk[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) mk[r] = mask[(size_t)min(rows[r], M - 1) * ld + j];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (rows[r] < M) out[(size_t)rows[r] * ld + j] = mk[r] > 0.f ? v[r] : 0.f;
     return 0.f;
   }
 };
 
-struct EpiWGrad {  // weight grad [M=out, N=in] + bias grad [M]
+struct EpiWGrad {  // weight grad [M=out, N=in] (j >= 0) and bias grad [M] (j == -1)
   float* gw; float* gb; int ld, M, N;
-  __device__ __forceinline__ float operator()(int i, int j, float v, bool is_bias) const {
-    if (i >= M) return 0.f;
-    if (is_bias) {
-      if (j == 0) gb[i] = v;
-    } else if (j < N) {
-      gw[(size_t)i * ld + j] = v;
+  template <int R>
+  __device__ __forceinline__ float run(const int (&rows)[R], int j, const float (&v)[R]) const {
+    if (j >= N) return 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (rows[r] >= M) continue;
+      if (j < 0) gb[rows[r]] = v[r];
+      else gw[(size_t)rows[r] * ld + j] = v[r];
     }
     return 0.f;
   }
 };
 
-__global__ void __launch_bounds__(256) vae_b1(VaeArgs a, int nblk_dh3) {
-  __shared__ float lds[4 * 256];
+// Weight/bias grad + in-place Adam on (param, exp_avg, exp_avg_sq) of the same
+// elements: the gradient never round-trips through HBM before the update, and
+// the R parameter/moment loads of a fragment are issued together.
+struct EpiWGradAdam {
+  float* G; float* P; float* Mo; float* Vo; long long ow, ob; int ld, M, N; AdamC c;
+  template <int R>
+  __device__ __forceinline__ float run(const int (&rows)[R], int j, const float (&v)[R]) const {
+    if (j >= N) return 0.f;
+    long long o[R];
+    float p[R], m[R], vv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = min(rows[r], M - 1);
+      o[r] = (j < 0) ? ob + i : ow + (long long)i * ld + j;
+      p[r] = P[o[r]]; m[r] = Mo[o[r]]; vv[r] = Vo[o[r]];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) adam_update(p[r], m[r], vv[r], v[r], c);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (rows[r] >= M) continue;
+      G[o[r]] = v[r]; P[o[r]] = p[r]; Mo[o[r]] = m[r]; Vo[o[r]] = vv[r];
+    }
+    return 0.f;
+  }
+};
+
+// dW GEMMs (K = batch): 32x32x2 f32 MFMA tiles, 2 tiles per block, k split
+// over 4 waves each; bias from the A-operand row sums (gemm_tiles32).
+constexpr int kWgTPB = 2;
+constexpr int kWgNPW = 16;  // k pairs per wave per round: B = 128 -> 64 pairs / 4 waves
+constexpr int kWgLds = kWaves * 1024 + kWaves * 64;
+__host__ __device__ inline int wgrad_blocks(int out_rows, int in_cols) {
+  return ((out_rows + 31) / 32 * ((in_cols + 31) / 32) + kWgTPB - 1) / kWgTPB;
+}
+#define WGRAD(A, B, EPI, OUT, IN, BLK, LDS) \
+  gemm_tiles32<kWaves, kWgTPB, kWgNPW, true>(A, B, EPI, a.M, cdiv_d(OUT, 32), cdiv_d(IN, 32), BLK, LDS)
+
+__global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a, int nblk_dh3) {
+  __shared__ __attribute__((aligned(16))) float lds[kWgLds];
+  STAMP(3, 0);
   if ((int)blockIdx.x < nblk_dh3) {
     ARowMajor A{a.dlog, a.D, a.M, a.D};
     BRowMajor Bw{a.W4, a.H, a.H, a.D};
     EpiMask epi{a.dh3, a.h3, a.H, a.M, a.H};
-    gemm_tiles<1>(A, Bw, epi, a.D, (a.M + 15) / 16, (a.H + 15) / 16, -1, blockIdx.x, lds);
+    gemm_tiles<kWaves, 1, 1, 7, false>(A, Bw, epi, a.D, cdiv_d(a.M, 16), cdiv_d(a.H, 16), blockIdx.x, lds);
   } else {
-    // dW4[D, H] = dlog^T h3, k = batch
+    // dW4[D, H] = dlog^T h3 (k = batch), db4 = column sums of dlog
     ATrans A{a.dlog, a.D, a.D, a.M};
     BRowMajor Bh{a.h3, a.H, a.H, a.M};
     EpiWGrad epi{a.gW4, a.gb4, a.H, a.D, a.H};
-    const int tj = (a.H + 15) / 16;
-    gemm_tiles<4>(A, Bh, epi, a.M, (a.D + 15) / 16, tj + 1, tj, blockIdx.x - nblk_dh3, lds);
+    WGRAD(A, Bh, epi, a.D, a.H, blockIdx.x - nblk_dh3, lds);
   }
+  STAMP(3, 1);
 }
 
 // ------------------------------------------------------------------- B2 ----
 // Blocks [0, nrow): 16-row fused dz -> (dmu, dlv) -> dh1.
-// Blocks [nrow, ...): dW3 = dh3^T z, db3.
-__global__ void __launch_bounds__(256) vae_b2(VaeArgs a, int nrow) {
-  __shared__ float red[4][2][256];
-  __shared__ float dml[16][68];  // [row][dmu(Z) | dlv(Z)], padded
-  if ((int)blockIdx.x >= nrow) {
-    float* lds = &red[0][0][0];  // 2048 floats >= 4*256
+// Blocks [nrow, nrow + nw3): dW3 = dh3^T z, db3. Last block: loss reduction.
+__global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3) {
+  __shared__ __attribute__((aligned(16))) float red[kWgLds];
+  __shared__ __attribute__((aligned(16))) float dml[16][68];  // [row][dmu(Z) | dlv(Z)]
+  __shared__ float scratch[16];
+  const int bid = blockIdx.x;
+  STAMP(4, 0);
+  if (bid >= nrow + nw3) {
+    // loss = sum(BCE partials) + beta * sum(KLD partials) of this step's forward
+    const int nk = cdiv_d(a.M, 16) * kWaves;
+    const int nb = cdiv_d(cdiv_d(a.M, 16) * cdiv_d(a.D, 16), 2) * kWaves;
+    float sb = 0.f, sk = 0.f;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) sb += a.partials[kBcePartial + i];
+    for (int i = threadIdx.x; i < nk; i += blockDim.x) sk += a.partials[kKldPartial + i];
+    const float bce = block_sum(sb, scratch);
+    __syncthreads();
+    const float kld = block_sum(sk, scratch);
+    if (threadIdx.x == 0) {
+      const float loss = bce + a.hp->kl_beta * kld;
+      TrainState* st = a.st;
+      st->loss_hist[(st->step - 1) % kLossHist] = loss;
+      st->epoch_loss += (double)loss;
+      st->epoch_count += 1.0;
+    }
+    return;
+  }
+  if (bid >= nrow) {
     ATrans A{a.dh3, a.H, a.H, a.M};
     BRowMajor Bz{a.z, a.Z, a.Z, a.M};
     EpiWGrad epi{a.gW3, a.gb3, a.Z, a.H, a.Z};
-    const int tj = (a.Z + 15) / 16;
-    gemm_tiles<4>(A, Bz, epi, a.M, (a.H + 15) / 16, tj + 1, tj, blockIdx.x - nrow, lds);
+    WGRAD(A, Bz, epi, a.H, a.Z, bid - nrow, red);
     return;
   }
-  const int w = wave_id(), lane = lane_id();
-  const int i0 = blockIdx.x * 16;
+  const int w = __builtin_amdgcn_readfirstlane(wave_id()), lane = lane_id();
+  const int i0 = bid * 16;
   const int Z2 = 2 * a.Z;
-  // dz (16 x Z) = dh3 (16 x H) W3 (H x Z), split-K over 4 waves
-  {
+  {  // dz (16 x Z) = dh3 (16 x H) W3 (H x Z), split-K over the waves
     ARowMajor A{a.dh3, a.H, a.M, a.H};
     BRowMajor Bw{a.W3, a.Z, a.Z, a.H};
-    const int nch = (a.H + 15) / 16;
-    const int kc0 = (w * nch) / 4, kc1 = ((w + 1) * nch) / 4;
-    for (int tj = 0; tj < 2; ++tj) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      if (tj * 16 < a.Z) acc = wave_tile(A, Bw, i0, tj * 16, kc0, kc1);
-      float* m = &red[w][tj][lane * 4];
-      m[0] = acc[0]; m[1] = acc[1]; m[2] = acc[2]; m[3] = acc[3];
-    }
+    const int nch = cdiv_d(a.H, 16);
+    const int kc0 = (w * nch) / kWaves, kc1 = ((w + 1) * nch) / kWaves;
+    f32x4 acc[2];
+    wave_tiles<2, 4>(A, Bw, i0, 0, 16, kc0, kc1, acc);
+    *reinterpret_cast<f32x4*>(&red[(w * 2 + 0) * 256 + lane * 4]) = acc[0];
+    *reinterpret_cast<f32x4*>(&red[(w * 2 + 1) * 256 + lane * 4]) = acc[1];
   }
+  STAMP(4, 1);
   __syncthreads();
   const float beta = a.hp->kl_beta;
-  for (int e = threadIdx.x; e < 16 * a.Z; e += blockDim.x) {
-    const int r = e / a.Z, c = e - r * a.Z;
-    const int i = i0 + r;
+  const int e = threadIdx.x;
+  const int r = e / a.Z, c = e - r * a.Z;
+  const int i = i0 + r;
+  const bool mine = e < 16 * a.Z;
+  const bool valid = mine && i < a.M;
+  float dmu = 0.f, dlv = 0.f;
+  if (mine) {
     const int tj = c >> 4, cc = c & 15;
     const int l = ((r >> 2) << 4) + cc, rr = r & 3;
-    const float dz = red[0][tj][l * 4 + rr] + red[1][tj][l * 4 + rr] + red[2][tj][l * 4 + rr] +
-                     red[3][tj][l * 4 + rr];
-    float dmu = 0.f, dlv = 0.f;
-    if (i < a.M) {
+    float dz = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) dz += red[(ww * 2 + tj) * 256 + l * 4 + rr];
+    if (valid) {
       const float mu = a.mulv[(size_t)i * Z2 + c];
       const float lv = a.mulv[(size_t)i * Z2 + a.Z + c];
       const float ep = a.eps[(size_t)i * a.Z + c];
@@ -269,108 +393,134 @@ __global__ void __launch_bounds__(256) vae_b2(VaeArgs a, int nrow) {
       // L = BCE + beta * (-0.5 sum(1 + lv - mu^2 - e^lv)), z = mu + eps*sd
       dmu = dz + beta * mu;
       dlv = 0.5f * dz * ep * sd + 0.5f * beta * (sd * sd - 1.f);
-      a.dmulv[(size_t)i * Z2 + c] = dmu;
-      a.dmulv[(size_t)i * Z2 + a.Z + c] = dlv;
     }
     dml[r][c] = dmu;
     dml[r][a.Z + c] = dlv;
   }
-  for (int e = threadIdx.x; e < 16 * 68; e += blockDim.x) {
-    const int r = e / 68, c = e % 68;
-    if (c >= Z2) dml[r][c] = 0.f;
-  }
   __syncthreads();
-  // dh1 (16 x H) = dml (16 x 2Z) W2 (2Z x H), masked by h1 > 0
-  {
-    const int ntiles = (a.H + 15) / 16;
-    const int r = lane & 15, q = lane >> 4;
-    for (int tj = w; tj < ntiles; tj += 4) {
-      const int j = tj * 16 + r;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int k0 = 0; k0 < Z2; k0 += 16) {
+  STAMP(4, 2);
+  {  // dh1 (16 x H) = dml (16 x 2Z) W2 (2Z x H), masked by h1 > 0
+    ARowMajor Ad{&dml[0][0], 68, 16, Z2};
+    BRowMajor Bw{a.W2, a.H, a.H, Z2};
+    f32x4 acc[4];
+    wave_tiles<4, 3>(Ad, Bw, 0, w * 16, kWaves * 16, 0, cdiv_d(Z2, 16), acc);
+    const int q = lane >> 4;
+    float mk[4][4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int k = k0 + 4 * q + t;
-          const float av = (k < Z2) ? dml[r][k] : 0.f;
-          const float bv = (j < a.H && k < Z2) ? a.W2[(size_t)k * a.H + j] : 0.f;
-          acc = mfma16x16x4(av, bv, acc);
-        }
-      }
+    for (int t = 0; t < 4; ++t) {
+      const int j = min((w + t * kWaves) * 16 + (lane & 15), a.H - 1);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) mk[t][rr] = a.h1[(size_t)min(i0 + 4 * q + rr, a.M - 1) * a.H + j];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = (w + t * kWaves) * 16 + (lane & 15);
       if (j < a.H) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int i = i0 + 4 * q + rr;
-          if (i < a.M) {
-            const size_t o = (size_t)i * a.H + j;
-            a.dh1[o] = a.h1[o] > 0.f ? acc[rr] : 0.f;
-          }
+          const int ii = i0 + 4 * q + rr;
+          if (ii < a.M) a.dh1[(size_t)ii * a.H + j] = mk[t][rr] > 0.f ? acc[t][rr] : 0.f;
         }
       }
     }
   }
+  if (valid) {
+    a.dmulv[(size_t)i * Z2 + c] = dmu;
+    a.dmulv[(size_t)i * Z2 + a.Z + c] = dlv;
+  }
+  STAMP(4, 3);
 }
 
 // ------------------------------------------------------------------- B3 ----
-__global__ void __launch_bounds__(256) vae_b3(VaeArgs a, int nblk_w2) {
-  __shared__ float lds[4 * 256];
+__global__ void __launch_bounds__(kThreads) vae_b3(VaeArgs a, int nblk_w2, int nblk_w1) {
+  __shared__ __attribute__((aligned(16))) float lds[kWgLds];
+  __shared__ AdamC cs;
   const int Z2 = 2 * a.Z;
-  if ((int)blockIdx.x < nblk_w2) {
+  const int bid = blockIdx.x;
+  STAMP(5, 0);
+  if (!a.fuse_adam) {
+    if (bid < nblk_w2) {
+      ATrans A{a.dmulv, Z2, Z2, a.M};
+      BRowMajor Bh{a.h1, a.H, a.H, a.M};
+      EpiWGrad epi{a.gW2, a.gb2, a.H, Z2, a.H};
+      WGRAD(A, Bh, epi, Z2, a.H, bid, lds);
+    } else {
+      ATrans A{a.dh1, a.H, a.H, a.M};
+      BRowMajor Bx{a.xb, a.D, a.D, a.M};
+      EpiWGrad epi{a.gW1, a.gb1, a.D, a.H, a.D};
+      WGRAD(A, Bx, epi, a.H, a.D, bid - nblk_w2, lds);
+    }
+    STAMP(5, 1);
+    return;
+  }
+  const AdamC c = adam_consts_block(a.st, a.hp, &cs);
+  if (bid < nblk_w2) {
     ATrans A{a.dmulv, Z2, Z2, a.M};
     BRowMajor Bh{a.h1, a.H, a.H, a.M};
-    EpiWGrad epi{a.gW2, a.gb2, a.H, Z2, a.H};
-    const int tj = (a.H + 15) / 16;
-    gemm_tiles<4>(A, Bh, epi, a.M, (Z2 + 15) / 16, tj + 1, tj, blockIdx.x, lds);
-  } else {
-    const int* rows = batch_rows(a);
+    EpiWGradAdam epi{a.G, a.P, a.Mo, a.Vo, a.oW2, a.ob2, a.H, Z2, a.H, c};
+    WGRAD(A, Bh, epi, Z2, a.H, bid, lds);
+  } else if (bid < nblk_w2 + nblk_w1) {
     ATrans A{a.dh1, a.H, a.H, a.M};
-    BRowGather Bx{a.X, rows, a.D, a.D, a.M};
-    EpiWGrad epi{a.gW1, a.gb1, a.D, a.H, a.D};
-    const int tj = (a.D + 15) / 16;
-    gemm_tiles<4>(A, Bx, epi, a.M, (a.H + 15) / 16, tj + 1, tj, blockIdx.x - nblk_w2, lds);
+    BRowMajor Bx{a.xb, a.D, a.D, a.M};
+    EpiWGradAdam epi{a.G, a.P, a.Mo, a.Vo, a.oW1, a.ob1, a.D, a.H, a.D, c};
+    WGRAD(A, Bx, epi, a.H, a.D, bid - nblk_w2, lds);
+  } else {
+    const int nb = gridDim.x - nblk_w2 - nblk_w1;
+    adam_stream(a.P, a.G, a.Mo, a.Vo, a.s_beg, a.s_end, bid - nblk_w2 - nblk_w1, nb, c);
   }
+  STAMP(5, 1);
 }
 
 // --------------------------------------------------------------- decode ----
 // Sampling path (/root/reference/vae-hpo.py:163-170): x = sigmoid(fc4(relu(fc3(z)))).
 struct EpiSigmoid {
   float* out; const float* bias; int ld, M, N;
-  __device__ __forceinline__ float operator()(int i, int j, float v, bool) const {
-    if (i < M && j < N) out[(size_t)i * ld + j] = 1.f / (1.f + expf(-(v + bias[j])));
+  template <int R>
+  __device__ __forceinline__ float run(const int (&rows)[R], int j, const float (&v)[R]) const {
+    if (j >= N) return 0.f;
+    const float b = bias[j];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (rows[r] < M) out[(size_t)rows[r] * ld + j] = 1.f / (1.f + expf(-(v[r] + b)));
     return 0.f;
   }
 };
 
-__global__ void __launch_bounds__(256) vae_dec1(VaeArgs a, const float* zin) {
-  __shared__ float lds[4 * 256];
+__global__ void __launch_bounds__(kThreads) vae_dec1(VaeArgs a, const float* zin) {
+  __shared__ __attribute__((aligned(16))) float lds[kWaves * 256];
   ARowMajor A{zin, a.Z, a.M, a.Z};
   BWeightNT Bw{a.W3, a.Z, a.H, a.Z};
   EpiBiasRelu epi{a.h3, a.b3, a.H, a.M, a.H};
-  gemm_tiles<4>(A, Bw, epi, a.Z, (a.M + 15) / 16, (a.H + 15) / 16, -1, blockIdx.x, lds);
+  gemm_tiles<kWaves, kWaves, 1, 2, false>(A, Bw, epi, a.Z, cdiv_d(a.M, 16), cdiv_d(a.H, 16), blockIdx.x, lds);
 }
 
-__global__ void __launch_bounds__(256) vae_dec2(VaeArgs a) {
-  __shared__ float lds[4 * 256];
+__global__ void __launch_bounds__(kThreads) vae_dec2(VaeArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[kWaves * 256];
   ARowMajor A{a.h3, a.H, a.M, a.H};
   BWeightNT Bw{a.W4, a.H, a.D, a.H};
   EpiSigmoid epi{a.recon, a.b4, a.D, a.M, a.D};
-  gemm_tiles<2>(A, Bw, epi, a.H, (a.M + 15) / 16, (a.D + 15) / 16, -1, blockIdx.x, lds);
+  gemm_tiles<kWaves, 2, 1, 7, false>(A, Bw, epi, a.H, cdiv_d(a.M, 16), cdiv_d(a.D, 16), blockIdx.x, lds);
 }
 
 // -------------------------------------------------------------- host side ----
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-VaeGrid vae_grid(int M, int D, int H, int Z) {
+VaeGrid vae_grid(const VaeArgs& a) {
   VaeGrid g;
-  const int ti = cdiv(M, 16);
-  g.f1 = ti * cdiv(H, 16);
+  const int ti = cdiv(a.M, 16);
+  g.f1 = ti * cdiv(a.H, 16);
   g.f2 = ti;
-  g.f3 = cdiv(ti * cdiv(D, 16), 2);
-  g.b1_dh3 = ti * cdiv(H, 16);
-  g.b1 = g.b1_dh3 + cdiv(cdiv(D, 16) * (cdiv(H, 16) + 1), 4);
+  g.f3 = cdiv(ti * cdiv(a.D, 16), 2);
+  g.b1_dh3 = ti * cdiv(a.H, 16);
+  g.b1 = g.b1_dh3 + wgrad_blocks(a.D, a.H);
   g.b2_rows = ti;
-  g.b2 = g.b2_rows + cdiv(cdiv(H, 16) * (cdiv(Z, 16) + 1), 4);
-  g.b3_w2 = cdiv(cdiv(2 * Z, 16) * (cdiv(H, 16) + 1), 4);
-  g.b3 = g.b3_w2 + cdiv(cdiv(H, 16) * (cdiv(D, 16) + 1), 4);
+  g.b2 = g.b2_rows + wgrad_blocks(a.H, a.Z) + 1;
+  g.b3_w2 = wgrad_blocks(2 * a.Z, a.H);
+  g.b3_w1 = wgrad_blocks(a.H, a.D);
+  const long long n4 = (a.s_end - a.s_beg) / 4;
+  // Adam streaming blocks: ~2 float4 per thread keeps B3 within one CU round
+  g.b3_stream = a.fuse_adam ? (int)((n4 + 2 * kThreads - 1) / (2 * kThreads)) : 0;
+  g.b3 = g.b3_w2 + g.b3_w1 + g.b3_stream;
   return g;
 }
 
@@ -380,38 +530,43 @@ using namespace mdt;
 
 extern "C" int mdt_vae_check(const VaeArgs* a) {
   if (a->M <= 0 || a->M > a->B || a->B > kMaxBatch) return 1;
-  if (a->Z > 32 || a->Z <= 0) return 2;
-  if ((a->D & 3) || (a->H & 3)) return 3;  // float4 alignment of row-major operands
-  const VaeGrid g = vae_grid(a->M, a->D, a->H, a->Z);
-  if (g.f2 > kBcePartial - kKldPartial) return 4;
-  if (g.f3 > kPartials - kBcePartial) return 5;
+  if (a->Z > 32 || a->Z <= 0 || (a->Z & 3)) return 2;
+  if ((a->D & 3) || (a->H & 3)) return 3;      // float4 alignment of row-major operands
+  if (a->H > kWaves * 16 * 4) return 6;        // F2/B2 stage C: <= 4 n-tiles per wave
+  const VaeGrid g = vae_grid(*a);
+  if (g.f2 * kWaves > kBcePartial - kKldPartial) return 4;
+  if (g.f3 * kWaves > kPartials - kBcePartial) return 5;
+  if (16 * a->Z > kThreads) return 2;
+  if (a->fuse_adam && (!a->P || !a->G || !a->Mo || !a->Vo || (a->s_beg & 3) || (a->s_end & 3))) return 7;
   return 0;
 }
 
 extern "C" int mdt_vae_forward(const VaeArgs* a, hipStream_t s) {
   const int rc = mdt_vae_check(a);
   if (rc) return rc;
-  const VaeGrid g = vae_grid(a->M, a->D, a->H, a->Z);
-  hipLaunchKernelGGL(vae_f1, dim3(g.f1), dim3(256), 0, s, *a);
-  hipLaunchKernelGGL(vae_f2, dim3(g.f2), dim3(256), 0, s, *a);
-  hipLaunchKernelGGL(vae_f3, dim3(g.f3), dim3(256), 0, s, *a);
+  const VaeGrid g = vae_grid(*a);
+  hipLaunchKernelGGL(vae_f1, dim3(g.f1), dim3(kThreads), 0, s, *a);
+  hipLaunchKernelGGL(vae_f2, dim3(g.f2), dim3(kThreads), 0, s, *a);
+  hipLaunchKernelGGL(vae_f3, dim3(g.f3), dim3(kThreads), 0, s, *a);
   return (int)hipGetLastError();
 }
 
 extern "C" int mdt_vae_backward(const VaeArgs* a, hipStream_t s, int part) {
   const int rc = mdt_vae_check(a);
   if (rc) return rc;
-  const VaeGrid g = vae_grid(a->M, a->D, a->H, a->Z);
-  if (part == 0 || part == 1) hipLaunchKernelGGL(vae_b1, dim3(g.b1), dim3(256), 0, s, *a, g.b1_dh3);
-  if (part == 0 || part == 2) hipLaunchKernelGGL(vae_b2, dim3(g.b2), dim3(256), 0, s, *a, g.b2_rows);
-  if (part == 0 || part == 3) hipLaunchKernelGGL(vae_b3, dim3(g.b3), dim3(256), 0, s, *a, g.b3_w2);
+  const VaeGrid g = vae_grid(*a);
+  if (part == 0 || part == 1) hipLaunchKernelGGL(vae_b1, dim3(g.b1), dim3(kThreads), 0, s, *a, g.b1_dh3);
+  if (part == 0 || part == 2)
+    hipLaunchKernelGGL(vae_b2, dim3(g.b2), dim3(kThreads), 0, s, *a, g.b2_rows, g.b2 - g.b2_rows - 1);
+  if (part == 0 || part == 3)
+    hipLaunchKernelGGL(vae_b3, dim3(g.b3), dim3(kThreads), 0, s, *a, g.b3_w2, g.b3_w1);
   return (int)hipGetLastError();
 }
 
 extern "C" int mdt_vae_decode(const VaeArgs* a, const float* zin, hipStream_t s) {
-  if (a->M <= 0 || a->M > a->B || !a->recon) return 1;
-  const int ti = (a->M + 15) / 16;
-  hipLaunchKernelGGL(vae_dec1, dim3((ti * ((a->H + 15) / 16) + 3) / 4), dim3(256), 0, s, *a, zin);
-  hipLaunchKernelGGL(vae_dec2, dim3((ti * ((a->D + 15) / 16) + 1) / 2), dim3(256), 0, s, *a);
+  if (a->M <= 0 || a->M > a->B || !a->recon || (a->Z & 3)) return 1;
+  const int ti = cdiv(a->M, 16);
+  hipLaunchKernelGGL(vae_dec1, dim3(cdiv(ti * cdiv(a->H, 16), kWaves)), dim3(kThreads), 0, s, *a, zin);
+  hipLaunchKernelGGL(vae_dec2, dim3(cdiv(ti * cdiv(a->D, 16), 2)), dim3(kThreads), 0, s, *a);
   return (int)hipGetLastError();
 }

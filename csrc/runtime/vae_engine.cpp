@@ -3,18 +3,16 @@
 #include <c10/hip/HIPStream.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
+#include <cmath>
 #include <cstring>
 #include <stdexcept>
 
 #include "../kernels/vae_mlp.h"
 
 extern "C" int mdt_adam_step(float* p, const float* g, float* m, float* v, long long n,
-                             const mdt::HParams* hp, mdt::TrainState* st, const float* partials,
-                             int nkld, int nbce, int advance, int decoupled_wd, int max_blocks,
-                             hipStream_t s);
+                             const mdt::HParams* hp, mdt::TrainState* st, hipStream_t s);
 extern "C" int mdt_loss_finalize(const mdt::HParams* hp, mdt::TrainState* st,
-                                 const float* partials, int nkld, int nbce, int advance,
-                                 hipStream_t s);
+                                 const float* partials, int nkld, int nbce, hipStream_t s);
 
 namespace mdt {
 
@@ -68,7 +66,7 @@ MlpVaeEngine::MlpVaeEngine(int64_t batch, int64_t D, int64_t H, int64_t Z, int64
   };
   act_add("h1", H); act_add("mulv", 2 * Z); act_add("eps", Z); act_add("z", Z);
   act_add("h3", H); act_add("dlog", D); act_add("dh3", H); act_add("dmulv", 2 * Z);
-  act_add("dh1", H); act_add("recon", D);
+  act_add("dh1", H); act_add("recon", D); act_add("xb", D);
   acts = torch::zeros({a}, fopt);
   partials = torch::zeros({kPartials}, fopt);
   auto bopt = torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device_index);
@@ -76,7 +74,7 @@ MlpVaeEngine::MlpVaeEngine(int64_t batch, int64_t D, int64_t H, int64_t Z, int64
   train_state = torch::zeros({st_bytes}, bopt);
   eval_state = torch::zeros({st_bytes}, bopt);
   hparams = torch::zeros({align64((int64_t)sizeof(HParams))}, bopt);
-  set_hparams(1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0, 1.0, 0);
+  set_hparams(1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0, 1.0, 0, false);
 }
 
 std::vector<std::tuple<std::string, int64_t, std::vector<int64_t>>> MlpVaeEngine::layout() const {
@@ -97,7 +95,7 @@ at::Tensor MlpVaeEngine::act(const std::string& name, int64_t M) {
       int64_t per = 0;
       if (name == "h1" || name == "h3" || name == "dh3" || name == "dh1") per = H_;
       else if (name == "mulv" || name == "dmulv") per = 2 * Z_;
-      else if (name == "eps" || name == "z") per = Z_;
+      else if (name == "eps" || name == "z") per = Z_;  // recon, xb, dlog: D
       else per = D_;
       return acts.narrow(0, p.second, M * per).view({M, per});
     }
@@ -107,17 +105,32 @@ at::Tensor MlpVaeEngine::act(const std::string& name, int64_t M) {
 
 void MlpVaeEngine::set_hparams(double lr, double beta1, double beta2, double eps,
                                double weight_decay, double kl_beta, double grad_scale,
-                               int64_t seed) {
+                               int64_t seed, bool decoupled_wd) {
   HParams h;
   std::memset(&h, 0, sizeof(h));
   h.lr = (float)lr; h.beta1 = (float)beta1; h.beta2 = (float)beta2; h.eps = (float)eps;
   h.weight_decay = (float)weight_decay; h.kl_beta = (float)kl_beta;
   h.grad_scale = (float)grad_scale;
+  h.decoupled_wd = decoupled_wd ? 1 : 0;
+  h.lr_d = lr; h.beta1_d = beta1; h.beta2_d = beta2;
+  const bool betas_changed = (beta1 != beta1_) || (beta2 != beta2_);
+  beta1_ = beta1; beta2_ = beta2;
   h.seed_lo = (uint32_t)((uint64_t)seed & 0xffffffffu);
   h.seed_hi = (uint32_t)((uint64_t)seed >> 32);
   auto cpu = torch::empty({(int64_t)sizeof(HParams)}, torch::kUInt8);
   std::memcpy(cpu.data_ptr(), &h, sizeof(h));
   hparams.narrow(0, 0, sizeof(HParams)).copy_(cpu);
+  if (betas_changed) {  // keep the device beta^t products consistent with the new betas
+    set_step((int64_t)read_state(false)[0]);
+    write_pows(eval_state, (int64_t)read_state(true)[0]);
+  }
+}
+
+void MlpVaeEngine::write_pows(at::Tensor& s, int64_t step) {
+  double v[2] = {std::pow(beta1_, (double)step), std::pow(beta2_, (double)step)};
+  auto cpu = torch::empty({16}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), v, 16);
+  s.narrow(0, offsetof(TrainState, b1pow), 16).copy_(cpu);
 }
 
 void MlpVaeEngine::set_cursor(bool eval, int64_t cursor, int64_t nbatches) {
@@ -132,6 +145,7 @@ void MlpVaeEngine::set_step(int64_t step) {
   auto cpu = torch::empty({8}, torch::kUInt8);
   std::memcpy(cpu.data_ptr(), &step, 8);
   train_state.narrow(0, offsetof(TrainState, step), 8).copy_(cpu);
+  write_pows(train_state, step);
 }
 
 void MlpVaeEngine::reset_loss(bool eval) {
@@ -188,6 +202,14 @@ void MlpVaeEngine::fill_args(void* out, const at::Tensor& X, const at::Tensor& i
   a.h1 = ap("h1"); a.mulv = ap("mulv"); a.eps = ap("eps"); a.z = ap("z"); a.h3 = ap("h3");
   a.dlog = ap("dlog"); a.dh3 = ap("dh3"); a.dmulv = ap("dmulv"); a.dh1 = ap("dh1");
   a.recon = want_recon ? ap("recon") : nullptr;
+  a.xb = ap("xb");
+  a.P = P; a.G = G;
+  a.Mo = exp_avg.data_ptr<float>(); a.Vo = exp_avg_sq.data_ptr<float>();
+  a.oW1 = oW1; a.ob1 = ob1; a.oW2 = oW2; a.ob2 = ob2;
+  a.s_beg = oW3; a.s_end = total_;
+  a.stamps = stamps_.defined() && stamps_.numel() > 0
+                 ? reinterpret_cast<unsigned long long*>(stamps_.data_ptr<int64_t>())
+                 : nullptr;
   a.partials = partials.data_ptr<float>();
   a.st = reinterpret_cast<TrainState*>((eval ? eval_state : train_state).data_ptr<uint8_t>());
   a.hp = reinterpret_cast<const HParams*>(hparams.data_ptr<uint8_t>());
@@ -198,28 +220,29 @@ void MlpVaeEngine::forward(const at::Tensor& X, const at::Tensor& idx, int64_t M
   c10::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
   VaeArgs a;
   fill_args(&a, X, idx, M, train, eval, rng_stream, want_recon);
-  const VaeGrid g = vae_grid(a.M, a.D, a.H, a.Z);
-  last_f2_blocks_ = g.f2;
-  last_f3_blocks_ = g.f3;
+  const VaeGrid g = vae_grid(a);
+  last_f2_blocks_ = g.f2 * 8;  // per-wave partial slots
+  last_f3_blocks_ = g.f3 * 8;
   check_rc(mdt_vae_forward(&a, c10::hip::getCurrentHIPStream().stream()), "vae forward");
 }
 
-void MlpVaeEngine::backward(const at::Tensor& X, const at::Tensor& idx, int64_t M, int64_t part) {
+void MlpVaeEngine::backward(const at::Tensor& X, const at::Tensor& idx, int64_t M, int64_t part,
+                            bool fuse_adam) {
   c10::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
   VaeArgs a;
   fill_args(&a, X, idx, M, true, false, 0, false);
+  a.fuse_adam = fuse_adam ? 1 : 0;
   check_rc(mdt_vae_backward(&a, c10::hip::getCurrentHIPStream().stream(), (int)part),
            "vae backward");
 }
 
-void MlpVaeEngine::adam(bool decoupled_wd) {
+void MlpVaeEngine::adam() {
   c10::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
   check_rc(mdt_adam_step(params.data_ptr<float>(), grads.data_ptr<float>(),
                          exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(), total_,
                          reinterpret_cast<const HParams*>(hparams.data_ptr<uint8_t>()),
                          reinterpret_cast<TrainState*>(train_state.data_ptr<uint8_t>()),
-                         partials.data_ptr<float>(), last_f2_blocks_, last_f3_blocks_, 3,
-                         decoupled_wd ? 1 : 0, 0, c10::hip::getCurrentHIPStream().stream()),
+                         c10::hip::getCurrentHIPStream().stream()),
            "adam");
 }
 
@@ -229,7 +252,7 @@ void MlpVaeEngine::loss_finalize(bool eval) {
                              reinterpret_cast<TrainState*>(
                                  (eval ? eval_state : train_state).data_ptr<uint8_t>()),
                              partials.data_ptr<float>(), last_f2_blocks_, last_f3_blocks_,
-                             eval ? 3 : 0, c10::hip::getCurrentHIPStream().stream()),
+                             c10::hip::getCurrentHIPStream().stream()),
            "loss finalize");
 }
 

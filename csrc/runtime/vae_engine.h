@@ -33,7 +33,7 @@ class MlpVaeEngine {
   int64_t bucket_split() const { return split_; }  // arena offset where fc4 starts
 
   void set_hparams(double lr, double beta1, double beta2, double eps, double weight_decay,
-                   double kl_beta, double grad_scale, int64_t seed);
+                   double kl_beta, double grad_scale, int64_t seed, bool decoupled_wd);
   void set_cursor(bool eval, int64_t cursor, int64_t nbatches);
   void set_step(int64_t step);
   void reset_loss(bool eval);
@@ -42,20 +42,24 @@ class MlpVaeEngine {
 
   void forward(const at::Tensor& X, const at::Tensor& idx, int64_t M, bool train, bool eval,
                int64_t rng_stream, bool want_recon);
-  void backward(const at::Tensor& X, const at::Tensor& idx, int64_t M, int64_t part);
-  void adam(bool decoupled_wd);
+  void backward(const at::Tensor& X, const at::Tensor& idx, int64_t M, int64_t part, bool fuse_adam);
+  void adam();
   void loss_finalize(bool eval);
   at::Tensor decode(const at::Tensor& z);  // sigmoid(fc4(relu(fc3 z))) -> [M, D]
   at::Tensor act(const std::string& name, int64_t M);
+  void set_stamps(at::Tensor t) { stamps_ = t; }  // int64 [6*512*8*8] or undefined
 
   at::Tensor params, grads, exp_avg, exp_avg_sq, acts, partials, train_state, eval_state, hparams;
 
  private:
   void fill_args(void* args, const at::Tensor& X, const at::Tensor& idx, int64_t M, bool train,
                  bool eval, int64_t rng_stream, bool want_recon);
+  void write_pows(at::Tensor& state, int64_t step);
   int64_t B_, D_, H_, Z_, total_, split_;
+  double beta1_ = -1.0, beta2_ = -1.0;
   int last_f2_blocks_ = 0, last_f3_blocks_ = 0;
   std::vector<LayoutEntry> layout_;
+  at::Tensor stamps_;
   std::vector<std::pair<std::string, int64_t>> act_off_;
 };
 

@@ -123,7 +123,7 @@ class MlpVaeTrainer:
         if self.engine is not None:
             h = self.hp
             self.engine.set_hparams(h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"],
-                                    h["kl_beta"], h["grad_scale"], self.seed)
+                                    h["kl_beta"], h["grad_scale"], self.seed, self.decoupled_wd)
 
     # ------------------------------------------------------------------ state
     @property
@@ -188,15 +188,16 @@ class MlpVaeTrainer:
         e = self.engine
         e.forward(X, idx, M, True, False, self.rng_stream, False)
         if self.reducer is not None:
-            e.backward(X, idx, M, 1)
+            e.backward(X, idx, M, 1, False)
             self.reducer.launch(1)          # fc4 bucket: overlaps B2/B3
-            e.backward(X, idx, M, 2)
-            e.backward(X, idx, M, 3)
+            e.backward(X, idx, M, 2, False)
+            e.backward(X, idx, M, 3, False)
             self.reducer.launch(0)
             self.reducer.wait_all()
+            e.adam()
         else:
-            e.backward(X, idx, M, 0)
-        e.adam(self.decoupled_wd)
+            # Adam fused into the weight-gradient epilogues of B3
+            e.backward(X, idx, M, 0, True)
 
     @torch.no_grad()
     def _step_torch(self, M: int):

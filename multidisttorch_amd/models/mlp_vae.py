@@ -114,16 +114,25 @@ def _bce_terms(t, x):
     return x * torch.clamp(sp_neg, max=100.0) + (1 - x) * torch.clamp(sp_pos, max=100.0)
 
 
-def reference_forward(v, x, eps, beta: float = 1.0):
-    """Forward + loss pieces exactly as kernels F1-F3 compute them."""
+def _relu(pre, mask):
+    return torch.relu(pre) if mask is None else pre * mask.to(pre.dtype)
+
+
+def reference_forward(v, x, eps, beta: float = 1.0, masks=None):
+    """Forward + loss pieces exactly as kernels F1-F3 compute them.
+
+    ``masks=(m1, m3)`` optionally pins the ReLU masks (tests: a pre-activation
+    within rounding of 0 may legitimately flip between summation orders).
+    """
     W1, b1, W2, b2, W3, b3, W4, b4 = _w(v)
     Z = W3.shape[1]
-    h1 = torch.relu(x @ W1.t() + b1)
+    m1, m3 = masks if masks is not None else (None, None)
+    h1 = _relu(x @ W1.t() + b1, m1)
     mulv = h1 @ W2.t() + b2
     mu, lv = mulv[:, :Z], mulv[:, Z:]
     sd = torch.exp(0.5 * lv)
     z = mu + eps * sd
-    h3 = torch.relu(z @ W3.t() + b3)
+    h3 = _relu(z @ W3.t() + b3, m3)
     t = h3 @ W4.t() + b4
     p = torch.sigmoid(t)
     bce = _bce_terms(t, x).sum()
@@ -132,9 +141,9 @@ def reference_forward(v, x, eps, beta: float = 1.0):
                 bce=bce, kld=kld, loss=bce + beta * kld)
 
 
-def reference_step(v, g, x, eps, beta: float = 1.0):
+def reference_step(v, g, x, eps, beta: float = 1.0, masks=None):
     """Explicit backward (kernels B1-B3) writing into grad views ``g``. Returns fwd dict."""
-    f = reference_forward(v, x, eps, beta)
+    f = reference_forward(v, x, eps, beta, masks)
     W1, b1, W2, b2, W3, b3, W4, b4 = _w(v)
     Z = W3.shape[1]
     dlog = f["p"] - x

@@ -48,7 +48,8 @@ def test_forward_backward_matches_reference(M, native_ext):
     eps = e.act("eps", M).double()
     x = X[idx[:M].long()].double()
     p, g, pv, gv = _ref_views(tr)
-    f = reference_step(pv, gv, x, eps, 1.0)
+    masks = (e.act("h1", M) > 0, e.act("h3", M) > 0)  # pin ReLU decisions at exact zeros
+    f = reference_step(pv, gv, x, eps, 1.0, masks)
     # eps is a standard normal draw
     assert abs(float(eps.mean())) < 0.5 and 0.5 < float(eps.std()) < 1.5 if M > 16 else True
     tol = dict(rtol=2e-4, atol=2e-5)
@@ -66,9 +67,7 @@ def test_forward_backward_matches_reference(M, native_ext):
         scale = float(ref.abs().max()) + 1e-6
         err = float((got - ref).abs().max()) / scale
         assert err < 2e-4, (name, err)
-    # loss partials -> loss
-    e.adam(False)
-    torch.cuda.synchronize()
+    # loss partials -> loss (reduced by B2's last block)
     loss = float(tr.loss_history()[0])
     assert math.isclose(loss, float(f["loss"]), rel_tol=1e-4), (loss, float(f["loss"]))
 
@@ -83,15 +82,24 @@ def test_matches_autograd_on_reference_module(native_ext):
     e.forward(X, idx, M, True, False, 0, False)
     e.backward(X, idx, M, 0)
     torch.cuda.synchronize()
-    eps = e.act("eps", M).clone()
-    m = VAE().cuda()
-    m.load_state_dict(tr.state_dict())
-    x = X[idx[:M].long()]
-    recon, mu, lv = m(x, eps=eps)
+    eps = e.act("eps", M).clone().double()
+    # float64 autograd oracle: torch's own fp32 GEMMs on ROCm are not an
+    # exact-f32 reference (see test_torch_fp32_gemm_precision below)
+    m = VAE().cuda().double()
+    m.load_state_dict({k: v.double() for k, v in tr.state_dict().items()})
+    x = X[idx[:M].long()].double()
+    # same layers/loss as the reference module, with the kernel's ReLU masks
+    # pinned (pre-activations within rounding of 0 flip with summation order)
+    m1 = (e.act("h1", M) > 0).double()
+    m3 = (e.act("h3", M) > 0).double()
+    h1 = m.fc1(x) * m1
+    mu, lv = m.fc21(h1), m.fc22(h1)
+    z = m.reparameterize(mu, lv, eps)
+    recon = torch.sigmoid(m.fc4(m.fc3(z) * m3))
     loss = loss_function(recon, x, mu, lv)
     loss.backward()
     for n, p in m.named_parameters():
-        got = tr.named_grads()[n]
+        got = tr.named_grads()[n].double()
         scale = float(p.grad.abs().max()) + 1e-6
         err = float((got - p.grad).abs().max()) / scale
         assert err < 5e-4, (n, err)
@@ -115,7 +123,7 @@ def test_adam_matches_torch(native_ext):
         for n, p in m.named_parameters():
             p.grad = tr.named_grads()[n].clone()
         opt.step()
-        e.adam(False)
+        e.adam()
         torch.cuda.synchronize()
         for n, p in m.named_parameters():
             torch.testing.assert_close(tr.named_parameters()[n], p.detach(), rtol=1e-5, atol=1e-6)
@@ -189,3 +197,15 @@ def test_philox_host_matches_device(native_ext):
     dev_eps = tr.engine.act("eps", 128).cpu().numpy()
     host = reparam_eps(128, 20, 123456789012, 5, 0)
     np.testing.assert_allclose(dev_eps, host, rtol=1e-5, atol=1e-5)
+
+
+def test_torch_fp32_gemm_precision():
+    """Diagnostic: how exact is torch's fp32 GEMM on this GPU (vs float64)?"""
+    g = torch.Generator().manual_seed(0)
+    a = torch.rand(400, 128, generator=g).cuda() - 0.5
+    b = torch.rand(128, 784, generator=g).cuda()
+    ref = a.double() @ b.double()
+    err = float(((a @ b).double() - ref).abs().max() / ref.abs().max())
+    print("torch fp32 GEMM rel err vs f64:", err, "allow_tf32:", torch.backends.cuda.matmul.allow_tf32,
+          "precision:", torch.get_float32_matmul_precision())
+    assert err < 1e-2
