@@ -49,6 +49,9 @@ struct VaeArgs {
   const float *W1, *b1, *W2, *b2, *W3, *b3, *W4, *b4;
   float *gW1, *gb1, *gW2, *gb2, *gW3, *gb3, *gW4, *gb4;
   float *h1, *mulv, *eps, *z, *h3, *dlog, *dh3, *dmulv, *dh1, *xb;
+  // split-K partial slabs handed from F1 -> F2 ([mu|lv] over 16-wide h1 slices)
+  // and B1 -> B2 (dz over 16-wide dh3 slices): [row tile][H/16][16][width]
+  float *slab_mv, *slab_dz;
   float* recon;          // optional sigmoid output [M, D] (eval / images)
   float* partials;       // [kPartials]
   TrainState* st;
@@ -66,6 +69,7 @@ constexpr int kStampKernels = 6;
 
 struct VaeGrid {
   int f1, f2, f3, b1, b1_dh3, b2, b2_rows, b3, b3_w2, b3_w1, b3_stream;
+  int th, ntm, sw, ntz, swz, groups;  // slab geometry (see vae_mlp.hip)
 };
 
 VaeGrid vae_grid(const VaeArgs& a);

@@ -59,29 +59,100 @@ struct EpiBiasRelu {
   }
 };
 
-// One block = one 16x16 tile of h1, its K = D split over the 8 waves.
+// Slab geometry: TH = H/16 slices; [mu|lv] slabs are NTM = ceil(2Z/16) tiles
+// wide (SW floats), dz slabs NTZ = ceil(Z/16) tiles (SWZ floats). F2/B2 run
+// GROUPS = ceil(TH/8) blocks per row tile, one 16-column output tile per wave.
+struct SlabGeo {
+  int th, ntm, sw, ntz, swz, groups;
+  __device__ __host__ SlabGeo(int H, int Z)
+      : th((H + 15) / 16), ntm((2 * Z + 15) / 16), sw(((2 * Z + 15) / 16) * 16), ntz((Z + 15) / 16),
+        swz(((Z + 15) / 16) * 16), groups(((H + 15) / 16 + kWaves - 1) / kWaves) {}
+};
+
+// Transposes a 16x16 C-layout tile (wave 0's registers: col = lane&15,
+// rows 4q..4q+3) into an LDS [row][k] image readable as A fragments.
+__device__ __forceinline__ void tile_to_lds(float (*t)[20], const float (&v)[4]) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) t[4 * (lane >> 4) + rr][lane & 15] = v[rr];
+}
+
+// 16x16 MFMA with A from the LDS tile (k = 16) and a prefetched B fragment.
+__device__ __forceinline__ f32x4 lds_tile_mma(float (*t)[20], const float (&b)[4]) {
+  const int lane = lane_id();
+  const float4 av = *reinterpret_cast<const float4*>(&t[lane & 15][4 * (lane >> 4)]);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = mfma16x16x4(av.x, b[0], acc);
+  acc = mfma16x16x4(av.y, b[1], acc);
+  acc = mfma16x16x4(av.z, b[2], acc);
+  acc = mfma16x16x4(av.w, b[3], acc);
+  return acc;
+}
+
+// One block = one 16x16 tile (ti, tj) of h1, its K = D split over the 8
+// waves. The relu'd tile then feeds the encoder head as a split-K slice:
+// waves 0..NTM-1 compute slab[ti][tj] = h1[:, tj*16:+16] W2[:, tj*16:+16]^T
+// (one 16-deep MFMA chunk each), so F2 only sums TH slabs instead of running
+// a 400-deep GEMM on 8 CUs.
 __global__ void __launch_bounds__(kThreads) vae_f1(VaeArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[kWaves * 256];
+  __shared__ __attribute__((aligned(16))) float ht[16][20];
   STAMP(0, 0);
+  const SlabGeo geo(a.H, a.Z);
+  const int w = __builtin_amdgcn_readfirstlane(wave_id()), lane = lane_id();
+  const int tiles_j = geo.th;
+  const int ti = blockIdx.x / tiles_j, tj = blockIdx.x - ti * tiles_j;
+  const int i0 = ti * 16, j = tj * 16 + (lane & 15);
+  const int q = lane >> 4;
+  const int Z2 = 2 * a.Z;
+  // prefetch: bias, and the W2 slice this wave multiplies in the slab step
+  const float bj = a.b1[min(j, a.H - 1)];
+  float wb[4] = {0.f, 0.f, 0.f, 0.f};
+  if (w < geo.ntm) {
+    const int n = w * 16 + (lane & 15);
+    const int k0 = tj * 16 + 4 * q;
+    const float4 v = *reinterpret_cast<const float4*>(a.W2 + (size_t)min(n, Z2 - 1) * a.H + min(k0, a.H - 4));
+    const float m = (n < Z2 && k0 < a.H) ? 1.f : 0.f;
+    wb[0] = v.x * m; wb[1] = v.y * m; wb[2] = v.z * m; wb[3] = v.w * m;
+  }
   const int* rows = a.idx + (size_t)a.st->cursor * a.B;
   ARowGather A{a.X, rows, a.D, a.M, a.D};
   BWeightNT Bw{a.W1, a.D, a.H, a.D};
-  EpiBiasRelu epi{a.h1, a.b1, a.H, a.M, a.H};
-  const int tiles_j = cdiv_d(a.H, 16);
-  gemm_tiles<kWaves, 1, 1, 7, false>(A, Bw, epi, a.D, cdiv_d(a.M, 16), tiles_j, blockIdx.x, lds);
+  const int nch = cdiv_d(a.D, 16);
+  const int kc0 = (w * nch) / kWaves, kc1 = ((w + 1) * nch) / kWaves;
+  f32x4 acc = wave_tile<7>(A, Bw, i0, tj * 16, kc0, kc1);
+  *reinterpret_cast<f32x4*>(lds + w * 256 + lane * 4) = acc;
+  __syncthreads();
+  float h[4];
+  if (w == 0) {
+#pragma unroll
+    for (int s = 1; s < kWaves; ++s) acc += *reinterpret_cast<const f32x4*>(lds + s * 256 + lane * 4);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) h[rr] = (i0 + 4 * q + rr < a.M && j < a.H) ? fmaxf(acc[rr] + bj, 0.f) : 0.f;
+    tile_to_lds(ht, h);
+  }
+  __syncthreads();
   STAMP(0, 1);
+  if (w < geo.ntm) {
+    const f32x4 sl = lds_tile_mma(ht, wb);
+    float* dst = a.slab_mv + ((size_t)(ti * geo.th + tj) * 16) * geo.sw + w * 16 + (lane & 15);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) dst[(size_t)(4 * q + rr) * geo.sw] = sl[rr];
+  }
+  if (w == 0 && j < a.H) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+      if (i0 + 4 * q + rr < a.M) a.h1[(size_t)(i0 + 4 * q + rr) * a.H + j] = h[rr];
+  }
   // blocks of tile column 0 materialise their 16 batch rows into xb for F3/B3
   // (each wave re-reads the K slice it just loaded: L1/L2 hits, no barrier)
-  if ((int)blockIdx.x % tiles_j == 0) {
-    const int w = wave_id(), lane = lane_id();
-    const int i = ((int)blockIdx.x / tiles_j) * 16 + (lane & 15);
-    const int nch = cdiv_d(a.D, 16);
-    const int kc0 = (w * nch) / kWaves, kc1 = ((w + 1) * nch) / kWaves;
+  if (tj == 0) {
+    const int i = i0 + (lane & 15);
     if (i < a.M) {
       const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)rows[i] * a.D);
       float4* dst = reinterpret_cast<float4*>(a.xb + (size_t)i * a.D);
       for (int c = kc0; c < kc1; ++c) {
-        const int k4 = c * 4 + (lane >> 4);
+        const int k4 = c * 4 + q;
         if (k4 * 4 < a.D) dst[k4] = src[k4];
       }
     }
@@ -96,30 +167,59 @@ __global__ void __launch_bounds__(kThreads) vae_f1(VaeArgs a) {
 }
 
 // ------------------------------------------------------------------- F2 ----
-// One block = 16 batch rows, 8 waves. Stage A: [mu|lv] (16 x 2Z) = h1 W2^T,
-// each wave one k-slice of all n-tiles. Stage B: reparameterise + KLD.
-// Stage C: h3 = relu(z W3^T + b3), n-tiles strided over the waves. All global
-// stores are issued after the last barrier. Requires Z <= 32, Z % 4 == 0.
+// Block (row tile ti, group g), 8 waves. Sums the TH [mu|lv] slabs of the row
+// tile (two half-sums in LDS), reparameterises (Philox eps, KLD), then wave w
+// computes h3 tile g*8+w = relu(z W3^T + b3) with K = Z from LDS. Group 0
+// stores mu/lv/eps/z and the KLD partials. All global stores follow the last
+// barrier. Requires Z <= 32, Z % 4 == 0, H <= 512.
 __global__ void __launch_bounds__(kThreads) vae_f2(VaeArgs a) {
-  __shared__ __attribute__((aligned(16))) float red[kWaves][4][256];
+  __shared__ __attribute__((aligned(16))) float part[2][16][64];
   __shared__ __attribute__((aligned(16))) float zt[16][36];
+  const SlabGeo geo(a.H, a.Z);
   const int w = __builtin_amdgcn_readfirstlane(wave_id()), lane = lane_id();
-  const int i0 = blockIdx.x * 16;
+  const int ti = blockIdx.x / geo.groups, g = blockIdx.x - ti * geo.groups;
+  const int i0 = ti * 16;
   const int Z2 = 2 * a.Z;
+  const int q = lane >> 4;
   STAMP(1, 0);
+  // prefetch: W3 fragments (K = Z <= 32 -> 2 chunks) and b3 for this wave's tile
+  const int jt = g * kWaves + w;
+  const int j = jt * 16 + (lane & 15);
+  float wb[2][4];
   {
-    ARowMajor A{a.h1, a.H, a.M, a.H};
-    BWeightNT Bw{a.W2, a.H, Z2, a.H};
-    const int nch = cdiv_d(a.H, 16);
-    const int kc0 = (w * nch) / kWaves, kc1 = ((w + 1) * nch) / kWaves;
-    f32x4 acc[4];
-    wave_tiles<4, 4>(A, Bw, i0, 0, 16, kc0, kc1, acc);
+    const float* wr = a.W3 + (size_t)min(j, a.H - 1) * a.Z;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(&red[w][t][lane * 4]) = acc[t];
+    for (int c = 0; c < 2; ++c) {
+      const int k0 = c * 16 + 4 * q;
+      const float4 v = *reinterpret_cast<const float4*>(wr + min(k0, a.Z - 4));
+      const float m = (j < a.H && k0 < a.Z) ? 1.f : 0.f;
+      wb[c][0] = v.x * m; wb[c][1] = v.y * m; wb[c][2] = v.z * m; wb[c][3] = v.w * m;
+    }
   }
-  STAMP(1, 1);
+  const float bj = a.b3[min(j, a.H - 1)];
+  // phase 1: two half-sums over the slabs, float4 per (row, quad)
+  {
+    const int quads = geo.sw / 4;
+    const int pairs = 16 * quads;
+    const int t = threadIdx.x;
+    if (t < 2 * pairs) {
+      const int half = t / pairs, pr = t - half * pairs;
+      const int r = pr / quads, cq = pr - r * quads;
+      const float4* base = reinterpret_cast<const float4*>(a.slab_mv + ((size_t)(ti * geo.th) * 16 + r) * geo.sw) + cq;
+      const size_t sstride = (size_t)16 * geo.sw / 4;
+      float4 acc4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int sidx = half * 16 + u;
+        const float4 v = base[min(sidx, geo.th - 1) * sstride];
+        const float m = sidx < geo.th ? 1.f : 0.f;
+        acc4.x += v.x * m; acc4.y += v.y * m; acc4.z += v.z * m; acc4.w += v.w * m;
+      }
+      *reinterpret_cast<float4*>(&part[half][r][cq * 4]) = acc4;
+    }
+  }
   __syncthreads();
-  // Stage B: one (row, latent) element per thread (16*Z <= 512)
+  // phase 2: one (row, latent) element per thread (16*Z <= 512)
   const long long stp = a.st->step - 1;  // F1 of this step already incremented it
   const uint32_t step_lo = (uint32_t)((unsigned long long)stp & 0xffffffffu);
   const uint32_t step_hi = (uint32_t)((unsigned long long)stp >> 32);
@@ -130,17 +230,8 @@ __global__ void __launch_bounds__(kThreads) vae_f2(VaeArgs a) {
   const bool valid = mine && i < a.M;
   float mu = 0.f, lv = 0.f, ep = 0.f, zz = 0.f, kld = 0.f;
   if (mine) {
-    auto acc_at = [&](int col) {
-      const int tj = col >> 4, cc = col & 15;
-      const int l = ((r >> 2) << 4) + cc;  // lane holding (row r, col cc)
-      const int rr = r & 3;
-      float s = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < kWaves; ++ww) s += red[ww][tj][l * 4 + rr];
-      return s;
-    };
-    mu = acc_at(c) + a.b2[c];
-    lv = acc_at(a.Z + c) + a.b2[a.Z + c];
+    mu = part[0][r][c] + part[1][r][c] + a.b2[c];
+    lv = part[0][r][a.Z + c] + part[1][r][a.Z + c] + a.b2[a.Z + c];
     const float sd = expf(0.5f * lv);
     // counter (row*Z + c, stream, step): replicas of a group differ by
     // `rng_stream` (like per-process randn_like streams in the reference)
@@ -153,43 +244,44 @@ __global__ void __launch_bounds__(kThreads) vae_f2(VaeArgs a) {
   }
   kld = wave_sum(kld);
   __syncthreads();
-  STAMP(1, 2);
+  STAMP(1, 1);
   {
-    ARowMajor Az{&zt[0][0], 36, 16, a.Z};
-    BWeightNT Bw{a.W3, a.Z, a.H, a.Z};
-    f32x4 acc[4];
-    wave_tiles<4, 2>(Az, Bw, 0, w * 16, kWaves * 16, 0, cdiv_d(a.Z, 16), acc);
-    const int q = lane >> 4;
-    float bj[4];
+    const int rr0 = lane & 15;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) bj[t] = a.b3[min((w + t * kWaves) * 16 + (lane & 15), a.H - 1)];
+    for (int cc = 0; cc < 2; ++cc) {
+      const int k0 = cc * 16 + 4 * q;
+      const float4 av = *reinterpret_cast<const float4*>(&zt[rr0][min(k0, 32)]);
+      const bool in = k0 < a.Z;  // select, not multiply: unwritten LDS may hold NaN bits
+      acc = mfma16x16x4(in ? av.x : 0.f, wb[cc][0], acc);
+      acc = mfma16x16x4(in ? av.y : 0.f, wb[cc][1], acc);
+      acc = mfma16x16x4(in ? av.z : 0.f, wb[cc][2], acc);
+      acc = mfma16x16x4(in ? av.w : 0.f, wb[cc][3], acc);
+    }
+    if (j < a.H) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int j = (w + t * kWaves) * 16 + (lane & 15);
-      if (j < a.H) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int ii = i0 + 4 * q + rr;
-          if (ii < a.M) a.h3[(size_t)ii * a.H + j] = fmaxf(acc[t][rr] + bj[t], 0.f);
-        }
+      for (int rr = 0; rr < 4; ++rr) {
+        const int ii = i0 + 4 * q + rr;
+        if (ii < a.M) a.h3[(size_t)ii * a.H + j] = fmaxf(acc[rr] + bj, 0.f);
       }
     }
   }
-  // deferred stores of stage B
-  if (valid) {
-    const size_t o = (size_t)i * Z2;
-    a.mulv[o + c] = mu;
-    a.mulv[o + a.Z + c] = lv;
-    a.eps[(size_t)i * a.Z + c] = ep;
-    a.z[(size_t)i * a.Z + c] = zz;
+  if (g == 0) {
+    if (valid) {
+      const size_t o = (size_t)i * Z2;
+      a.mulv[o + c] = mu;
+      a.mulv[o + a.Z + c] = lv;
+      a.eps[(size_t)i * a.Z + c] = ep;
+      a.z[(size_t)i * a.Z + c] = zz;
+    }
+    if (lane == 0) a.partials[kKldPartial + ti * kWaves + w] = -0.5f * kld;
   }
-  if (lane == 0) a.partials[kKldPartial + blockIdx.x * kWaves + w] = -0.5f * kld;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     int cur = a.st->cursor + 1;
     if (a.st->nbatches > 0 && cur >= a.st->nbatches) cur = 0;
     a.st->cursor = cur;
   }
-  STAMP(1, 3);
+  STAMP(1, 2);
 }
 
 // ------------------------------------------------------------------- F3 ----
@@ -306,12 +398,55 @@ __host__ __device__ inline int wgrad_blocks(int out_rows, int in_cols) {
 
 __global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a, int nblk_dh3) {
   __shared__ __attribute__((aligned(16))) float lds[kWgLds];
+  __shared__ __attribute__((aligned(16))) float ht[16][20];
   STAMP(3, 0);
   if ((int)blockIdx.x < nblk_dh3) {
+    // one 16x16 tile (ti, tj) of dh3 = (dlog W4) . [h3 > 0], K = D over 8 waves;
+    // then waves 0..NTZ-1 emit the dz split-K slab dh3[:, tj] W3[tj, :].
+    const SlabGeo geo(a.H, a.Z);
+    const int w = __builtin_amdgcn_readfirstlane(wave_id()), lane = lane_id();
+    const int ti = blockIdx.x / geo.th, tj = blockIdx.x - ti * geo.th;
+    const int i0 = ti * 16, j = tj * 16 + (lane & 15);
+    const int q = lane >> 4;
+    float mk[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) mk[rr] = a.h3[(size_t)min(i0 + 4 * q + rr, a.M - 1) * a.H + min(j, a.H - 1)];
+    float wb[4] = {0.f, 0.f, 0.f, 0.f};
+    if (w < geo.ntz) {  // B(k, n) = W3[(tj*16 + k) * Z + w*16 + n]
+      const int n = w * 16 + (lane & 15);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int k = tj * 16 + 4 * q + t;
+        wb[t] = a.W3[(size_t)min(k, a.H - 1) * a.Z + min(n, a.Z - 1)] * ((k < a.H && n < a.Z) ? 1.f : 0.f);
+      }
+    }
     ARowMajor A{a.dlog, a.D, a.M, a.D};
     BRowMajor Bw{a.W4, a.H, a.H, a.D};
-    EpiMask epi{a.dh3, a.h3, a.H, a.M, a.H};
-    gemm_tiles<kWaves, 1, 1, 7, false>(A, Bw, epi, a.D, cdiv_d(a.M, 16), cdiv_d(a.H, 16), blockIdx.x, lds);
+    const int nch = cdiv_d(a.D, 16);
+    const int kc0 = (w * nch) / kWaves, kc1 = ((w + 1) * nch) / kWaves;
+    f32x4 acc = wave_tile<7>(A, Bw, i0, tj * 16, kc0, kc1);
+    *reinterpret_cast<f32x4*>(lds + w * 256 + lane * 4) = acc;
+    __syncthreads();
+    float d[4];
+    if (w == 0) {
+#pragma unroll
+      for (int s = 1; s < kWaves; ++s) acc += *reinterpret_cast<const f32x4*>(lds + s * 256 + lane * 4);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) d[rr] = (mk[rr] > 0.f && i0 + 4 * q + rr < a.M && j < a.H) ? acc[rr] : 0.f;
+      tile_to_lds(ht, d);
+    }
+    __syncthreads();
+    if (w < geo.ntz) {
+      const f32x4 sl = lds_tile_mma(ht, wb);
+      float* dst = a.slab_dz + ((size_t)(ti * geo.th + tj) * 16) * geo.swz + w * 16 + (lane & 15);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) dst[(size_t)(4 * q + rr) * geo.swz] = sl[rr];
+    }
+    if (w == 0 && j < a.H) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        if (i0 + 4 * q + rr < a.M) a.dh3[(size_t)(i0 + 4 * q + rr) * a.H + j] = d[rr];
+    }
   } else {
     // dW4[D, H] = dlog^T h3 (k = batch), db4 = column sums of dlog
     ATrans A{a.dlog, a.D, a.D, a.M};
@@ -323,8 +458,10 @@ __global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a, int nblk_dh3) {
 }
 
 // ------------------------------------------------------------------- B2 ----
-// Blocks [0, nrow): 16-row fused dz -> (dmu, dlv) -> dh1.
-// Blocks [nrow, nrow + nw3): dW3 = dh3^T z, db3. Last block: loss reduction.
+// Blocks [0, nrow): (row tile ti, group g): sum the TH dz slabs (4 quarter
+// sums in LDS), dmu/dlv (reparam + beta-KLD grads), then wave w computes dh1
+// tile g*8+w = ([dmu|dlv] W2) . [h1 > 0] with K = 2Z from LDS; group 0 stores
+// dmulv. Blocks [nrow, nrow + nw3): dW3 = dh3^T z, db3. Last block: loss.
 __global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3) {
   __shared__ __attribute__((aligned(16))) float red[kWgLds];
   __shared__ __attribute__((aligned(16))) float dml[16][68];  // [row][dmu(Z) | dlv(Z)]
@@ -357,38 +494,70 @@ __global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3)
     WGRAD(A, Bz, epi, a.H, a.Z, bid - nrow, red);
     return;
   }
+  const SlabGeo geo(a.H, a.Z);
   const int w = __builtin_amdgcn_readfirstlane(wave_id()), lane = lane_id();
-  const int i0 = bid * 16;
+  const int ti = bid / geo.groups, g = bid - ti * geo.groups;
+  const int i0 = ti * 16;
   const int Z2 = 2 * a.Z;
-  {  // dz (16 x Z) = dh3 (16 x H) W3 (H x Z), split-K over the waves
-    ARowMajor A{a.dh3, a.H, a.M, a.H};
-    BRowMajor Bw{a.W3, a.Z, a.Z, a.H};
-    const int nch = cdiv_d(a.H, 16);
-    const int kc0 = (w * nch) / kWaves, kc1 = ((w + 1) * nch) / kWaves;
-    f32x4 acc[2];
-    wave_tiles<2, 4>(A, Bw, i0, 0, 16, kc0, kc1, acc);
-    *reinterpret_cast<f32x4*>(&red[(w * 2 + 0) * 256 + lane * 4]) = acc[0];
-    *reinterpret_cast<f32x4*>(&red[(w * 2 + 1) * 256 + lane * 4]) = acc[1];
-  }
-  STAMP(4, 1);
-  __syncthreads();
-  const float beta = a.hp->kl_beta;
+  const int q = lane >> 4;
+  const int jt = g * kWaves + w;
+  const int j = jt * 16 + (lane & 15);
+  // prefetch: W2 fragments (K = 2Z <= 64 -> up to 4 chunks), h1 mask, and
+  // this thread's mu / lv / eps
+  float wb[4][4];
+#pragma unroll
+  for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = cc * 16 + 4 * q + t;
+      wb[cc][t] = a.W2[(size_t)min(k, Z2 - 1) * a.H + min(j, a.H - 1)] * ((k < Z2 && j < a.H) ? 1.f : 0.f);
+    }
+  float mk[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) mk[rr] = a.h1[(size_t)min(i0 + 4 * q + rr, a.M - 1) * a.H + min(j, a.H - 1)];
   const int e = threadIdx.x;
   const int r = e / a.Z, c = e - r * a.Z;
   const int i = i0 + r;
   const bool mine = e < 16 * a.Z;
   const bool valid = mine && i < a.M;
+  float mu = 0.f, lv = 0.f, ep = 0.f;
+  if (mine) {
+    const int ic = min(i, a.M - 1);
+    mu = a.mulv[(size_t)ic * Z2 + c];
+    lv = a.mulv[(size_t)ic * Z2 + a.Z + c];
+    ep = a.eps[(size_t)ic * a.Z + c];
+  }
+  // phase 1: quarter sums of the dz slabs, float4 per (row, quad)
+  float* part = red;  // [4][16][SWZ]
+  {
+    const int quads = geo.swz / 4;
+    const int pairs = 16 * quads;
+    const int t = threadIdx.x;
+    if (t < 4 * pairs) {
+      const int qq = t / pairs, pr = t - qq * pairs;
+      const int rr = pr / quads, cq = pr - rr * quads;
+      const float4* base = reinterpret_cast<const float4*>(a.slab_dz + ((size_t)(ti * geo.th) * 16 + rr) * geo.swz) + cq;
+      const size_t sstride = (size_t)16 * geo.swz / 4;
+      float4 acc4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int sidx = qq * 8 + u;
+        const float4 v = base[min(sidx, geo.th - 1) * sstride];
+        const float m = sidx < geo.th ? 1.f : 0.f;
+        acc4.x += v.x * m; acc4.y += v.y * m; acc4.z += v.z * m; acc4.w += v.w * m;
+      }
+      *reinterpret_cast<float4*>(&part[(qq * 16 + rr) * geo.swz + cq * 4]) = acc4;
+    }
+  }
+  __syncthreads();
+  STAMP(4, 1);
+  const float beta = a.hp->kl_beta;
   float dmu = 0.f, dlv = 0.f;
   if (mine) {
-    const int tj = c >> 4, cc = c & 15;
-    const int l = ((r >> 2) << 4) + cc, rr = r & 3;
     float dz = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) dz += red[(ww * 2 + tj) * 256 + l * 4 + rr];
+    for (int qq = 0; qq < 4; ++qq) dz += part[(qq * 16 + r) * geo.swz + c];
     if (valid) {
-      const float mu = a.mulv[(size_t)i * Z2 + c];
-      const float lv = a.mulv[(size_t)i * Z2 + a.Z + c];
-      const float ep = a.eps[(size_t)i * a.Z + c];
       const float sd = expf(0.5f * lv);
       // L = BCE + beta * (-0.5 sum(1 + lv - mu^2 - e^lv)), z = mu + eps*sd
       dmu = dz + beta * mu;
@@ -399,32 +568,28 @@ __global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3)
   }
   __syncthreads();
   STAMP(4, 2);
-  {  // dh1 (16 x H) = dml (16 x 2Z) W2 (2Z x H), masked by h1 > 0
-    ARowMajor Ad{&dml[0][0], 68, 16, Z2};
-    BRowMajor Bw{a.W2, a.H, a.H, Z2};
-    f32x4 acc[4];
-    wave_tiles<4, 3>(Ad, Bw, 0, w * 16, kWaves * 16, 0, cdiv_d(Z2, 16), acc);
-    const int q = lane >> 4;
-    float mk[4][4];
+  {
+    const int rr0 = lane & 15;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int j = min((w + t * kWaves) * 16 + (lane & 15), a.H - 1);
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) mk[t][rr] = a.h1[(size_t)min(i0 + 4 * q + rr, a.M - 1) * a.H + j];
+    for (int cc = 0; cc < 4; ++cc) {
+      const int k0 = cc * 16 + 4 * q;
+      const float4 av = *reinterpret_cast<const float4*>(&dml[rr0][min(k0, 64)]);
+      const bool in = k0 < Z2;  // select, not multiply: unwritten LDS may hold NaN bits
+      acc = mfma16x16x4(in ? av.x : 0.f, wb[cc][0], acc);
+      acc = mfma16x16x4(in ? av.y : 0.f, wb[cc][1], acc);
+      acc = mfma16x16x4(in ? av.z : 0.f, wb[cc][2], acc);
+      acc = mfma16x16x4(in ? av.w : 0.f, wb[cc][3], acc);
     }
+    if (j < a.H) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int j = (w + t * kWaves) * 16 + (lane & 15);
-      if (j < a.H) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int ii = i0 + 4 * q + rr;
-          if (ii < a.M) a.dh1[(size_t)ii * a.H + j] = mk[t][rr] > 0.f ? acc[t][rr] : 0.f;
-        }
+      for (int rr = 0; rr < 4; ++rr) {
+        const int ii = i0 + 4 * q + rr;
+        if (ii < a.M) a.dh1[(size_t)ii * a.H + j] = mk[rr] > 0.f ? acc[rr] : 0.f;
       }
     }
   }
-  if (valid) {
+  if (g == 0 && valid) {
     a.dmulv[(size_t)i * Z2 + c] = dmu;
     a.dmulv[(size_t)i * Z2 + a.Z + c] = dlv;
   }
@@ -507,13 +672,15 @@ static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 VaeGrid vae_grid(const VaeArgs& a) {
   VaeGrid g;
+  const SlabGeo geo(a.H, a.Z);
+  g.th = geo.th; g.ntm = geo.ntm; g.sw = geo.sw; g.ntz = geo.ntz; g.swz = geo.swz; g.groups = geo.groups;
   const int ti = cdiv(a.M, 16);
   g.f1 = ti * cdiv(a.H, 16);
-  g.f2 = ti;
+  g.f2 = ti * geo.groups;
   g.f3 = cdiv(ti * cdiv(a.D, 16), 2);
   g.b1_dh3 = ti * cdiv(a.H, 16);
   g.b1 = g.b1_dh3 + wgrad_blocks(a.D, a.H);
-  g.b2_rows = ti;
+  g.b2_rows = ti * geo.groups;
   g.b2 = g.b2_rows + wgrad_blocks(a.H, a.Z) + 1;
   g.b3_w2 = wgrad_blocks(2 * a.Z, a.H);
   g.b3_w1 = wgrad_blocks(a.H, a.D);
@@ -534,7 +701,8 @@ extern "C" int mdt_vae_check(const VaeArgs* a) {
   if ((a->D & 3) || (a->H & 3)) return 3;      // float4 alignment of row-major operands
   if (a->H > kWaves * 16 * 4) return 6;        // F2/B2 stage C: <= 4 n-tiles per wave
   const VaeGrid g = vae_grid(*a);
-  if (g.f2 * kWaves > kBcePartial - kKldPartial) return 4;
+  if (cdiv(a->M, 16) * kWaves > kBcePartial - kKldPartial) return 4;
+  if (a->H > 16 * 32 || !a->slab_mv || !a->slab_dz) return 8;  // slab half-sums cover <= 32 slices
   if (g.f3 * kWaves > kPartials - kBcePartial) return 5;
   if (16 * a->Z > kThreads) return 2;
   if (a->fuse_adam && (!a->P || !a->G || !a->Mo || !a->Vo || (a->s_beg & 3) || (a->s_end & 3))) return 7;

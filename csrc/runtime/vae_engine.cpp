@@ -67,6 +67,12 @@ MlpVaeEngine::MlpVaeEngine(int64_t batch, int64_t D, int64_t H, int64_t Z, int64
   act_add("h1", H); act_add("mulv", 2 * Z); act_add("eps", Z); act_add("z", Z);
   act_add("h3", H); act_add("dlog", D); act_add("dh3", H); act_add("dmulv", 2 * Z);
   act_add("dh1", H); act_add("recon", D); act_add("xb", D);
+  const int64_t th = (H + 15) / 16, sw = (2 * Z + 15) / 16 * 16, swz = (Z + 15) / 16 * 16;
+  const int64_t Bpad = (B_ + 15) / 16 * 16;
+  act_off_.push_back({"slab_mv", a});
+  a = align64(a + Bpad * th * sw);
+  act_off_.push_back({"slab_dz", a});
+  a = align64(a + Bpad * th * swz);
   acts = torch::zeros({a}, fopt);
   partials = torch::zeros({kPartials}, fopt);
   auto bopt = torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device_index);
@@ -203,6 +209,8 @@ void MlpVaeEngine::fill_args(void* out, const at::Tensor& X, const at::Tensor& i
   a.dlog = ap("dlog"); a.dh3 = ap("dh3"); a.dmulv = ap("dmulv"); a.dh1 = ap("dh1");
   a.recon = want_recon ? ap("recon") : nullptr;
   a.xb = ap("xb");
+  a.slab_mv = ap("slab_mv");
+  a.slab_dz = ap("slab_dz");
   a.P = P; a.G = G;
   a.Mo = exp_avg.data_ptr<float>(); a.Vo = exp_avg_sq.data_ptr<float>();
   a.oW1 = oW1; a.ob1 = ob1; a.oW2 = oW2; a.ob2 = ob2;

@@ -46,7 +46,7 @@ def _ranges(M=128, D=784, H=400, Z=20, fuse=True):
     ti = cd(M, 16)
     wg = lambda o, i: cd(cd(o, 32) * cd(i, 32), 2)
     b1 = ti * cd(H, 16)
-    b2r = ti
+    b2r = ti * cd(cd(H, 16), 8)
     b2w = wg(H, Z)
     b3w2, b3w1 = wg(2 * Z, H), wg(H, D)
     return {"B1": [("dh3", 0, b1), ("dW4", b1, b1 + wg(D, H))],
