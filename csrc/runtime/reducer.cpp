@@ -7,6 +7,7 @@ namespace mdt {
 BucketReducer::BucketReducer(c10::intrusive_ptr<c10d::ProcessGroup> pg, at::Tensor flat,
                              std::vector<int64_t> bounds, bool average)
     : pg_(std::move(pg)), flat_(std::move(flat)), bounds_(std::move(bounds)), average_(average) {
+  TORCH_CHECK(pg_, "BucketReducer needs a process group (got None)");
   TORCH_CHECK(flat_.dim() == 1 && flat_.is_contiguous(), "flat gradient arena must be 1-D contiguous");
   TORCH_CHECK(bounds_.size() >= 2 && bounds_.front() == 0 && bounds_.back() == flat_.numel(),
               "bucket bounds must start at 0 and end at numel");

@@ -1,0 +1,216 @@
+"""Per-trial driver: one HPO trial trained by one group of ranks.
+
+Parity map (/root/reference/vae-hpo.py):
+  * ``run(group_id, batch_size, epochs, group)`` :122-174  -> ``run_trial``
+  * ``train`` :61-92 / ``test`` :95-119                     -> ``_train_epoch`` / ``_test_epoch``
+  * stdout formats (``[W:G] Train Epoch: ...``, ``====> Epoch: ...``,
+    ``====> Test set loss: ...``, ``"{rank} Done. time: ..."``) are byte
+    compatible; ``results-{group_rank}/reconstruction_{e}.png`` and
+    ``sample_{e}.png`` keep the reference's layout (SURVEY.md Q7 collision
+    included unless ``per_group_results``).
+  * the DistributedSampler shard (``rank=group_id, num_replicas=W//group_size``)
+    and its fixed epoch order (no ``set_epoch``) are reproduced exactly.
+
+MI355X-first differences: the whole epoch runs as replays of a captured
+hipGraph over device-resident data (no DataLoader, no per-step ``.item()``);
+the loss history is read once per epoch to print the same log lines; global
+barriers run on the gloo control plane so uneven trials never trip the RCCL
+watchdog; replicas of a group (size > 1) all-reduce gradients through the
+native bucket reducer, overlapped with the tail of the backward pass.
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ckpt import checkpoint as ckpt
+from ..data.sampler import shard_indices
+from ..obs.metrics import TrialMetrics
+from ..obs import trace
+from ..parallel.ddp import broadcast_params, make_arena_reducer
+from ..parallel.groups import print0
+from ..runtime.bootstrap import bound_device, global_barrier
+from ..utils.images import save_image
+from .trial import TrialSpec
+
+__all__ = ["RunOptions", "TrialResult", "run_trial", "idle_rank"]
+
+
+@dataclass
+class RunOptions:
+    batch_size: int = 128
+    log_interval: int = 10
+    model: str = "mlp"
+    backend: Optional[str] = None          # hip | torch (default: hip on GPU)
+    use_graphs: bool = True
+    graph_steps: int = 10
+    ckpt_dir: Optional[str] = None
+    resume: bool = False
+    metrics_dir: Optional[str] = None
+    results: bool = True                   # write PNGs like the reference
+    per_group_results: bool = False        # opt-in fix for the results-0 collision (Q7)
+    eval_each_epoch: bool = True
+    quiet_train_log: bool = False
+    train_samples: Optional[int] = None    # synthetic dataset size (default 60000)
+    test_samples: Optional[int] = None     # (default 10000)
+    image_size: int = 28
+    data_dir: str = "data"
+    synthetic: Optional[bool] = True
+
+
+@dataclass
+class TrialResult:
+    group_id: int
+    epochs: int
+    shard: int
+    samples: int
+    wall_s: float
+    final_train_loss: float = float("nan")
+    final_test_loss: float = float("nan")
+    extra: dict = field(default_factory=dict)
+
+
+def _results_dir(opts: RunOptions, group_id: int, group_rank: int) -> str:
+    if opts.per_group_results:
+        return f"results-g{group_id}-{group_rank}"
+    return f"results-{group_rank}"
+
+
+def _make_trainer(spec: TrialSpec, opts: RunOptions, device, group_rank: int, D: int):
+    if opts.model != "mlp":
+        raise ValueError(f"model {opts.model!r} is handled by run_conv_trial")
+    from ..models.mlp_trainer import MlpVaeTrainer
+
+    return MlpVaeTrainer(batch_size=opts.batch_size, D=D, device=device, backend=opts.backend,
+                         seed=spec.seed, lr=spec.lr, kl_beta=spec.beta, rng_stream=group_rank,
+                         use_graphs=opts.use_graphs, graph_steps=opts.graph_steps)
+
+
+def _load_data(opts: RunOptions, device):
+    from ..data.datasets import mnist_like
+
+    train = mnist_like(True, data_dir=opts.data_dir, device=device, size=opts.image_size,
+                       synthetic=opts.synthetic, n=opts.train_samples)
+    test = mnist_like(False, data_dir=opts.data_dir, device=device, size=opts.image_size,
+                      synthetic=opts.synthetic, n=opts.test_samples)
+    return train, test
+
+
+def _train_epoch(trainer, epoch: int, n_shard: int, n_dataset: int, opts: RunOptions, group) -> float:
+    B = opts.batch_size
+    full, tail = n_shard // B, n_shard % B
+    nb = full + (1 if tail else 0)
+    trainer.set_cursor(0, nb)
+    trainer.reset_loss()
+    step0 = trainer.step_count
+    with trace.range(f"train_epoch_{epoch}"):
+        trainer.train_steps(full, B)
+        if tail:
+            trainer.train_steps(1, tail)
+    hist = trainer.loss_history()
+    st = trainer.read_state()
+    if not opts.quiet_train_log:
+        for batch_idx in range(0, nb, opts.log_interval):
+            bsz = B if batch_idx < full else tail
+            loss_b = float(hist[(step0 + batch_idx) % len(hist)])
+            print0("Train Epoch: {} [{}/{} ({:.0f}%)]\tLoss: {:.6f}".format(
+                epoch, batch_idx * bsz, n_dataset, 100.0 * batch_idx / nb, loss_b / bsz), process_group=group)
+    # The reference divides by the FULL dataset size, not the shard (Q6).
+    print0("====> Epoch: {} Average loss: {:.4f}".format(epoch, st["epoch_loss"] / n_dataset), process_group=group)
+    return st["epoch_loss"]
+
+
+def _test_epoch(trainer, epoch: int, test, opts: RunOptions, group, rdir: Optional[str], shape) -> float:
+    idx = torch.arange(len(test), dtype=torch.int32, device=test.data.device)
+    with trace.range(f"test_epoch_{epoch}"):
+        total, first = trainer.evaluate(test.data, idx, want_first_recon=rdir is not None)
+    if rdir is not None and first is not None:
+        m = first.shape[0]
+        n = min(m, 8)
+        data = test.data[:n].view(n, *shape).float().cpu()
+        comparison = torch.cat([data, first[:n].view(n, *shape).float().cpu()])
+        os.makedirs(rdir, exist_ok=True)
+        save_image(comparison, f"{rdir}/reconstruction_" + str(epoch) + ".png", nrow=n)
+    test_loss = total / len(test)
+    print0("====> Test set loss: {:.4f}".format(test_loss), process_group=group)
+    return test_loss
+
+
+def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: Optional[int] = None) -> TrialResult:
+    """Train one trial on the ranks of ``group`` (this rank is a member)."""
+    world_rank = dist.get_rank() if dist.is_initialized() else 0
+    world_size = dist.get_world_size() if dist.is_initialized() else 1
+    grank = dist.get_rank(group) if dist.is_initialized() else 0
+    gsize = dist.get_world_size(group) if dist.is_initialized() else 1
+    K = num_trials if num_trials is not None else world_size // gsize
+    device = bound_device()
+
+    train, test = data if data is not None else _load_data(opts, device)
+    D = int(train.data.shape[1])
+    trainer = _make_trainer(spec, opts, device, grank, D)
+    if gsize > 1:
+        # DDP's _sync_module_states: replicas start from group rank 0's weights
+        broadcast_params([trainer.params], group)
+        trainer.attach_reducer(make_arena_reducer(group, trainer.grads, [0, trainer.split, trainer.numel]))
+    start_epoch = 1
+    if opts.ckpt_dir and opts.resume:
+        prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer)
+        if prog is not None:
+            start_epoch = prog["epoch"] + 1
+            print0(f"resumed trial {spec.group_id} from {prog['path']} (epoch {prog['epoch']})", process_group=group)
+        if gsize > 1:
+            broadcast_params([trainer.params, trainer.exp_avg, trainer.exp_avg_sq], group)
+    metrics = TrialMetrics(opts.metrics_dir, spec.group_id, enabled=(grank == 0))
+
+    # Parity with the reference's download barrier (vae-hpo.py:133-144).
+    global_barrier()
+
+    idx = shard_indices(len(train), K, spec.group_id)
+    trainer.bind_train_data(train.data, idx)
+    n_shard = idx.numel()
+    rdir = _results_dir(opts, spec.group_id, grank) if opts.results else None
+    shape = (1, opts.image_size, opts.image_size)
+    gen = torch.Generator(device="cpu").manual_seed(spec.seed * 7919 + 17)
+
+    t0 = time.time()
+    train_loss = test_loss = float("nan")
+    for epoch in range(start_epoch, spec.epochs + 1):
+        te = time.perf_counter()
+        train_loss = _train_epoch(trainer, epoch, n_shard, len(train), opts, group)
+        t_train = time.perf_counter() - te
+        if opts.eval_each_epoch:
+            test_loss = _test_epoch(trainer, epoch, test, opts, group, rdir, shape)
+        if rdir is not None:
+            with torch.no_grad():
+                sample = torch.randn(64, trainer.Z, generator=gen).to(device)
+                sample = trainer.decode(sample).cpu()
+                os.makedirs(rdir, exist_ok=True)
+                save_image(sample.view(64, *shape), f"{rdir}/sample_" + str(epoch) + ".png")
+        if opts.ckpt_dir and grank == 0:
+            ckpt.save_trial(opts.ckpt_dir, trainer, spec, epoch)
+        metrics.log(epoch=epoch, train_loss_sum=train_loss, train_loss=train_loss / len(train),
+                    test_loss=test_loss, epoch_train_s=t_train, samples=n_shard,
+                    train_samples_per_s=n_shard / max(t_train, 1e-9), lr=spec.lr, beta=spec.beta)
+
+    global_barrier()  # parity: vae-hpo.py:172 (waits for the slowest trial)
+    t1 = time.time()
+    print(world_rank, "Done. time: %f" % (t1 - t0), flush=True)
+    epochs_run = max(0, spec.epochs - start_epoch + 1)
+    return TrialResult(spec.group_id, epochs_run, n_shard, epochs_run * n_shard, t1 - t0,
+                       train_loss / len(train), test_loss)
+
+
+def idle_rank():
+    """Leftover ranks (W % K) own no trial but join both global barriers, so the
+    members never block on them (fixes the reference's crash)."""
+    global_barrier()
+    t0 = time.time()
+    global_barrier()
+    return time.time() - t0

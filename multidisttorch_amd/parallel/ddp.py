@@ -150,6 +150,8 @@ class PyBucketReducer:
 
 def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: bool = True,
                        prefer_native: bool = True):
+    if pg is None:
+        pg = dist.distributed_c10d._get_default_group()
     if prefer_native and native.available():
         return native.require().BucketReducer(pg, flat, [int(b) for b in bounds], average)
     if flat.is_cuda:

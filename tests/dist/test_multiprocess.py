@@ -1,0 +1,139 @@
+"""Multi-process CPU/gloo tests (BASELINE config #1 plumbing), launched with the
+framework's own launcher under emulated SLURM / Open MPI / torchrun env."""
+import json
+import os
+import re
+import sys
+
+import pytest
+import torch
+
+from multidisttorch_amd.launch import launch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+WORKER = os.path.join(HERE, "worker.py")
+ENV = {"DDP_BACKEND": "gloo", "OMP_NUM_THREADS": "1", "PYTHONPATH": ROOT}
+
+
+def _results(outs):
+    res = []
+    for o in outs:
+        for line in (o or "").splitlines():
+            if line.startswith("RESULT "):
+                res.append(json.loads(line[7:]))
+    return res
+
+
+def _run(args, n, emulate="torchrun", timeout=180, cwd=None):
+    cmd = [sys.executable] + args
+    old = os.getcwd()
+    if cwd:
+        os.chdir(cwd)
+    try:
+        rc, outs = launch(cmd, n, emulate=emulate, timeout=timeout, extra_env=ENV, capture=True)
+    finally:
+        os.chdir(old)
+    return rc, outs
+
+
+@pytest.mark.parametrize("w,k,emulate", [(2, 2, "slurm"), (4, 2, "ompi"), (5, 2, "torchrun"), (3, 1, "slurm")])
+def test_group_carving(w, k, emulate):
+    rc, outs = _run([WORKER, "groups", str(k)], w, emulate)
+    assert rc == 0, "\n".join(outs)
+    res = sorted(_results(outs), key=lambda r: r["rank"])
+    assert len(res) == w
+    n = w // k
+    for r in res:
+        g = r["rank"] // n
+        if g < k:
+            assert r["member"] == [g]
+            assert r["gathered"] == list(range(g * n, g * n + n))
+            assert r["grank"][g] == r["rank"] - g * n
+        else:  # leftover rank: idle but joins the control-plane barrier (no crash, Q3)
+            assert r["member"] == [] and r["gathered"] is None
+    text = "\n".join(outs)
+    # reference print formats (utils.py:149, :161, :174)
+    assert f"world_size, world_rank: {w} 0" in text
+    assert "Rank 0 is in group 0" in text
+    assert re.search(r"^\[0:0\] hello from group 0$", text, re.M)
+
+
+def test_native_and_python_reducer():
+    rc, outs = _run([WORKER, "reducer"], 2)
+    assert rc == 0, "\n".join(outs)
+    for r in _results(outs):
+        assert r["native"] == 0.0 and r["py"] == 0.0
+        assert r["type_native"] == "BucketReducer"
+        assert r["ready_native"] == [3.0, 3.0] and r["ready_py"] == [3.0, 3.0]
+
+
+def test_arena_ddp_matches_torch_ddp():
+    rc, outs = _run([WORKER, "arena_ddp"], 2)
+    assert rc == 0, "\n".join(outs)
+    res = _results(outs)
+    assert len(res) == 2
+    for r in res:
+        assert r["err"] < 1e-5 and r["buckets"] >= 2
+
+
+def test_trainer_replicas_stay_in_sync():
+    rc, outs = _run([WORKER, "trainer_ddp"], 2)
+    assert rc == 0, "\n".join(outs)
+    for r in _results(outs):
+        assert r["maxdiff"] == 0.0 and r["step"] == 5
+
+
+def test_example_subgroup_world4(tmp_path):
+    old = dict(ENV)
+    ENV["MDT_EXAMPLE_WORLD"] = "4"
+    try:
+        rc, outs = _run([os.path.join(ROOT, "example-subgroup.py")], 4, "slurm", cwd=str(tmp_path))
+    finally:
+        ENV.clear()
+        ENV.update(old)
+    text = "\n".join(outs)
+    assert rc == 0, text
+    assert "0 gather_list: [tensor([0]), tensor([1])]" in text
+    assert "2 gather_list: [tensor([2]), tensor([3])]" in text
+
+
+def _vae_hpo(tmp_path, n, *args, emulate="slurm"):
+    return _run([os.path.join(ROOT, "vae-hpo.py"), "--train-samples", "1024", "--test-samples", "256",
+                 "--batch-size", "64"] + list(args), n, emulate, timeout=300, cwd=str(tmp_path))
+
+
+def test_vae_hpo_two_trials_config1(tmp_path):
+    rc, outs = _vae_hpo(tmp_path, 2, "--epochs", "1", "--ngroups", "2", "--metrics-dir", "m")
+    text = "\n".join(outs)
+    assert rc == 0, text
+    # trial g trains epochs+g epochs (vae-hpo.py:202): trial 1 logs epoch 2
+    assert re.search(r"^\[1:0\] ====> Epoch: 2 Average loss: \d+\.\d{4}$", text, re.M)
+    assert not re.search(r"^\[0:0\] ====> Epoch: 2", text, re.M)
+    assert re.search(r"^\[0:0\] Train Epoch: 1 \[0/1024 \(0%\)\]\tLoss: \d+\.\d{6}$", text, re.M)
+    assert re.search(r"^\[0:0\] ====> Test set loss: \d+\.\d{4}$", text, re.M)
+    assert re.search(r"^0 Done\. time: \d+\.\d{6}$", text, re.M)
+    agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
+    assert agg["trials"] == 2 and agg["samples"] == 512 * 1 + 512 * 2
+    assert (tmp_path / "results-0" / "sample_1.png").exists()
+    assert (tmp_path / "m" / "trial-1.jsonl").exists()
+
+
+def test_vae_hpo_intra_group_ddp_and_resume(tmp_path):
+    rc, outs = _vae_hpo(tmp_path, 2, "--epochs", "1", "--ngroups", "1", "--ckpt-dir", "ck", "--no-results")
+    assert rc == 0, "\n".join(outs)
+    assert (tmp_path / "ck" / "trial-0" / "epoch-1.pt").exists()
+    rc, outs = _vae_hpo(tmp_path, 2, "--epochs", "2", "--ngroups", "1", "--ckpt-dir", "ck", "--resume",
+                        "--no-results")
+    text = "\n".join(outs)
+    assert rc == 0, text
+    assert "resumed trial 0" in text and "Epoch: 2 Average" in text and "Epoch: 1 Average" not in text
+    ck = torch.load(str(tmp_path / "ck" / "trial-0" / "epoch-2.pt"), weights_only=True)
+    assert ck["progress"]["epoch"] == 2
+
+
+def test_vae_hpo_idle_leftover_rank(tmp_path):
+    rc, outs = _vae_hpo(tmp_path, 3, "--epochs", "1", "--ngroups", "2", "--no-results", emulate="torchrun")
+    text = "\n".join(outs)
+    assert rc == 0, text  # the reference crashes here
+    assert "Rank 2 is in group" not in text

@@ -1,0 +1,60 @@
+"""Launcher discovery parity (reference utils.py:9-26, :40-56, :59-90, :108-119)."""
+import pytest
+
+from multidisttorch_amd.runtime import env as E
+
+
+def test_precedence_ompi_over_slurm_over_torchrun():
+    e = {"OMPI_COMM_WORLD_SIZE": "6", "OMPI_COMM_WORLD_RANK": "5", "SLURM_NPROCS": "4",
+         "SLURM_PROCID": "3", "WORLD_SIZE": "2", "RANK": "1"}
+    assert E.init_comm_size_and_rank(e) == (6, 5)
+    e.pop("OMPI_COMM_WORLD_SIZE")
+    assert E.init_comm_size_and_rank(e) == (4, 3)
+    e.pop("SLURM_NPROCS")
+    assert E.init_comm_size_and_rank(e) == (2, 1)  # extension: torchrun honoured (Q1)
+    assert E.init_comm_size_and_rank({}) == (1, 0)
+
+
+def test_partial_env_falls_through():
+    # reference requires BOTH size and rank of a launcher
+    assert E.init_comm_size_and_rank({"OMPI_COMM_WORLD_SIZE": "4"}) == (1, 0)
+    assert E.init_comm_size_and_rank({"SLURM_PROCID": "2"}) == (1, 0)
+
+
+def test_local_rank():
+    assert E.local_rank_from_env({"OMPI_COMM_WORLD_LOCAL_RANK": "3"}) == 3
+    assert E.local_rank_from_env({"SLURM_LOCALID": "2"}) == 2
+    assert E.local_rank_from_env({"LOCAL_RANK": "1"}) == 1
+    assert E.local_rank_from_env({}, world_rank=13, ndev=8) == 5
+
+
+@pytest.mark.parametrize("s,expect", [
+    ("or-condo-g04", ["or-condo-g04"]),
+    ("or-condo-g[05,07-08,13]", ["or-condo-g05", "or-condo-g07", "or-condo-g08", "or-condo-g13"]),
+    ("or-condo-g[05,07-08,13],or-condo-h[01,12]",
+     ["or-condo-g05", "or-condo-g07", "or-condo-g08", "or-condo-g13", "or-condo-h01", "or-condo-h12"]),
+    ("frontier[00001-00003]", ["frontier00001", "frontier00002", "frontier00003"]),
+    ("a1,b2", ["a1", "b2"]),
+    ("node[8-11]", ["node8", "node9", "node10", "node11"]),
+    ("localhost", ["localhost"]),
+])
+def test_parse_slurm_nodelist(s, expect):
+    assert E.parse_slurm_nodelist(s) == expect
+
+
+def test_find_ifname_loopback():
+    assert E.find_ifname("127.0.0.1") in ("lo", "lo0")
+    assert E.find_ifname("203.0.113.77") is None
+
+
+def test_master_discovery():
+    assert E.discover_master({}) == ("127.0.0.1", "8889")
+    assert E.discover_master({"MASTER_ADDR": "h", "MASTER_PORT": "1"}) == ("h", "1")
+    assert E.discover_master({"LSB_HOSTS": "batch1 h1 h1 h2"})[0] == "h1"
+    assert E.discover_master({"LSB_MCPU_HOSTS": "batch1 1 h7 42"})[0] == "h7"
+    assert E.discover_master({"SLURM_NODELIST": "or-condo-g[05,07]"})[0] == "or-condo-g05"
+
+
+def test_discover_launcher_name():
+    assert E.discover({"SLURM_NPROCS": "2", "SLURM_PROCID": "1"}).launcher == "slurm"
+    assert E.discover({}).launcher == "single"
