@@ -1,0 +1,44 @@
+"""End-to-end on one MI355X: vae-hpo.py with the fused HIP path (single trial,
+world of 1), output formats, images, metrics; plus the native reducer on a
+size-1 RCCL group (no-op path) and graph capture through the trainer."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def test_vae_hpo_single_gpu(tmp_path):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29611")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "vae-hpo.py"), "--ngroups", "1", "--epochs", "2",
+                        "--metrics-dir", "m", "--ckpt-dir", "ck"],
+                       capture_output=True, text=True, timeout=600, cwd=str(tmp_path), env=env)
+    text = r.stdout + r.stderr
+    assert r.returncode == 0, text[-4000:]
+    assert "Distributed data parallel: nccl master at 127.0.0.1:29611" in text
+    assert re.search(r"^\[0:0\] Train Epoch: 1 \[0/60000 \(0%\)\]\tLoss: \d+\.\d{6}$", text, re.M)
+    assert re.search(r"^\[0:0\] ====> Epoch: 2 Average loss: \d+\.\d{4}$", text, re.M)
+    assert re.search(r"^\[0:0\] ====> Test set loss: \d+\.\d{4}$", text, re.M)
+    assert re.search(r"^0 Done\. time: \d+\.\d{6}$", text, re.M)
+    agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
+    assert agg["samples"] == 120000 and agg["value"] > 1e5
+    # the loss actually decreases over training
+    losses = [float(x) for x in re.findall(r"Average loss: (\d+\.\d+)", text)]
+    assert losses[-1] < losses[0]
+    assert (tmp_path / "results-0" / "reconstruction_2.png").exists()
+    assert (tmp_path / "ck" / "trial-0" / "epoch-2.pt").exists()
+
+
+def test_bench_gpu_contract():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "50", "--warmup", "10"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29612"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["config"]["backend"] == "hip" and out["config"]["valid"] and out["value"] > 1e5
