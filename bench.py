@@ -31,11 +31,11 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-# Reference hot training step measured on the survey box (BASELINE.md row
-# "Reference hot step (fwd+bwd+DDP+Adam), B=128, 1 rank": 32.9k samples/s per
-# trial). Used per trial: baseline(K) = K x 32.9k (generous to the reference,
-# which measured sub-linear on 2 trials).
-REF_SAMPLES_PER_S_PER_TRIAL = 32900.0
+# Reference-equivalent step on the SAME MI355X (BASELINE.md, row 2:
+# bench/ref_torch_baseline.py = the reference's DDP + DataLoader + .item() +
+# Adam hot loop in stock PyTorch-ROCm): 93.5k samples/s per trial. Used per
+# trial: baseline(K) = K x 93.5k (generous to the reference: perfect scaling).
+REF_SAMPLES_PER_S_PER_TRIAL = 93465.0
 
 
 def main(argv=None):
