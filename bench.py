@@ -45,7 +45,8 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch-size", type=int, default=128)
     ap.add_argument("--ngroups", type=int, default=None, help="trials K (default: world size)")
-    ap.add_argument("--model", default="mlp", choices=["mlp"])
+    ap.add_argument("--model", default="mlp", choices=["mlp", "conv28", "conv128"],
+                    help="mlp = reference MLP-VAE fp32 (headline); conv28/conv128 = bf16 conv-VAE extension")
     ap.add_argument("--graph-steps", type=int, default=10)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--backend", default=None, help="hip|torch (default: hip on GPU)")
@@ -74,14 +75,24 @@ def main(argv=None):
         pg = handles[gid]
         grank = dist.get_rank(pg)
         spec = specs[gid]
-        trainer = MlpVaeTrainer(batch_size=a.batch_size, device=dev, backend=a.backend,
-                                seed=spec.seed, lr=spec.lr, kl_beta=spec.beta, rng_stream=grank,
-                                use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
+        if a.model == "mlp":
+            trainer = MlpVaeTrainer(batch_size=a.batch_size, device=dev, backend=a.backend,
+                                    seed=spec.seed, lr=spec.lr, kl_beta=spec.beta, rng_stream=grank,
+                                    use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
+        else:
+            from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+            img = 28 if a.model == "conv28" else 128
+            trainer = ConvVaeTrainer(batch_size=a.batch_size, image=img, z=32 if img == 28 else 64, device=dev,
+                                     backend=a.backend, seed=spec.seed, lr=spec.lr, kl_beta=spec.beta,
+                                     rng_stream=grank, use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
         # replicas of a group start from group rank 0's weights (DDP broadcast)
         if n_per > 1:
             dist.broadcast(trainer.params, src=dist.get_global_rank(pg, 0), group=pg)
             trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, [0, trainer.split, trainer.numel]))
-        train = mnist_like(True, synthetic=True, device=dev)
+        img = 28 if a.model in ("mlp", "conv28") else 128
+        train = mnist_like(True, synthetic=True, device=dev, size=img,
+                           n=None if img == 28 else 4096 * max(1, a.batch_size // 32))
         idx = shard_indices(len(train), K, gid)
         trainer.bind_train_data(train.data, idx)
         trainer.set_cursor(0, idx.numel() // a.batch_size)  # full batches only
@@ -128,13 +139,17 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / (REF_SAMPLES_PER_S_PER_TRIAL * K), 2),
-            "dtype": "fp32",
-            "data": "synthetic (MNIST-shaped 60000x1x28x28, random-init weights)",
+            "dtype": "fp32" if a.model == "mlp" else "bf16",
+            "data": ("synthetic (MNIST-shaped 60000x1x28x28, random-init weights)" if a.model != "conv128"
+                     else "synthetic (1x128x128 images, random-init weights)"),
             "config": {
-                "model": "MLP-VAE 784-400-20 (reference vae-hpo.py topology)",
+                "model": {"mlp": "MLP-VAE 784-400-20 (reference vae-hpo.py topology)",
+                          "conv28": "conv-VAE 28x28 (2 conv + 2 deconv, z=32)",
+                          "conv128": "conv-VAE 128x128 (4 conv + 4 deconv, z=64)"}[a.model],
                 "global_batch": a.batch_size * K,
                 "per_trial_batch": a.batch_size,
                 "seq_len": None,
+                "image": img,
                 "parallelism": f"groups{K}x{n_per}",
                 "trials": K,
                 "backend": trainer.backend if trainer is not None else None,

@@ -9,7 +9,6 @@ namespace mdt {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kWave = 64;
 

@@ -84,13 +84,20 @@ def _results_dir(opts: RunOptions, group_id: int, group_rank: int) -> str:
 
 
 def _make_trainer(spec: TrialSpec, opts: RunOptions, device, group_rank: int, D: int):
-    if opts.model != "mlp":
-        raise ValueError(f"model {opts.model!r} is handled by run_conv_trial")
-    from ..models.mlp_trainer import MlpVaeTrainer
+    if opts.model == "mlp":
+        from ..models.mlp_trainer import MlpVaeTrainer
 
-    return MlpVaeTrainer(batch_size=opts.batch_size, D=D, device=device, backend=opts.backend,
-                         seed=spec.seed, lr=spec.lr, kl_beta=spec.beta, rng_stream=group_rank,
-                         use_graphs=opts.use_graphs, graph_steps=opts.graph_steps)
+        return MlpVaeTrainer(batch_size=opts.batch_size, D=D, device=device, backend=opts.backend,
+                             seed=spec.seed, lr=spec.lr, kl_beta=spec.beta, rng_stream=group_rank,
+                             use_graphs=opts.use_graphs, graph_steps=opts.graph_steps)
+    if opts.model == "conv":
+        from ..models.conv_vae import ConvVaeTrainer
+
+        return ConvVaeTrainer(batch_size=opts.batch_size, image=opts.image_size,
+                              z=32 if opts.image_size == 28 else 64, device=device, backend=opts.backend,
+                              seed=spec.seed, lr=spec.lr, kl_beta=spec.beta, rng_stream=group_rank,
+                              use_graphs=opts.use_graphs, graph_steps=opts.graph_steps)
+    raise ValueError(f"unknown model {opts.model!r}")
 
 
 def _load_data(opts: RunOptions, device):

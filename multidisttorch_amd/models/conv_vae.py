@@ -1,0 +1,630 @@
+"""Convolutional VAE (28x28 and 128x128) on hand-written bf16 MFMA kernels.
+
+North-star extension (BASELINE.json configs #2 and #5; absent from the
+reference, whose model is the MLP of /root/reference/vae-hpo.py:19-45):
+a conv/deconv encoder-decoder with the same ELBO (BCE(sum) + beta*KLD) and
+reparameterisation as the reference.
+
+Layout and precision: NHWC activations in bf16, fp32 master weights + fp32
+gradients + fp32 Adam moments in flat arenas (one ``adam_cast`` launch per step
+updates the masters and re-emits the bf16 weights AND their [Cin][KH][KW][Cout]
+transposes), f32 accumulation everywhere, f32 mu/logvar/logits and loss.
+
+Every layer is one of three implicit-GEMM kernels (csrc/kernels/conv_bf16.hip):
+  conv    fwd = conv_fwd,   d_in = conv_dgrad,  dW = conv_wgrad(G=d_out, X=in)
+  linear  = conv 1x1 on a 1x1 "image"
+  convT   fwd = conv_dgrad, d_in = conv_fwd,    dW = conv_wgrad(G=in, X=d_out), db = chan_sum
+ReLU backward is fused into the epilogue that produces each gradient (output
+mask), so no separate elementwise pass exists in the backward.
+``TorchConvVAE`` is the same network in stock torch ops (fp32, NCHW): the CPU
+backend and the numerical oracle of the GPU tests.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..ops import native
+from ..ops.philox import reparam_eps
+from .mlp_vae import reference_adam_
+
+__all__ = ["Layer", "conv_vae_spec", "TorchConvVAE", "ConvVaeTrainer", "conv_layout"]
+
+EVAL_STREAM = 1 << 30
+
+
+@dataclass(frozen=True)
+class Layer:
+    name: str
+    kind: str          # conv | convT | linear
+    cin: int
+    cout: int
+    k: int
+    s: int
+    p: int
+    relu: bool
+    in_hw: int         # input spatial size (1 for linear)
+    out_hw: int
+
+
+def conv_vae_spec(image: int = 28, channels: int = 1, z: int = 32) -> List[Layer]:
+    if image == 28:
+        enc = [(channels, 32), (32, 64)]
+    elif image == 128:
+        enc = [(channels, 32), (32, 64), (64, 128), (128, 256)]
+    else:
+        raise ValueError("image must be 28 or 128")
+    L, hw = [], image
+    for i, (ci, co) in enumerate(enc):
+        L.append(Layer(f"enc{i + 1}", "conv", ci, co, 4, 2, 1, True, hw, hw // 2))
+        hw //= 2
+    flat = enc[-1][1] * hw * hw
+    L.append(Layer("enc_head", "linear", flat, 2 * z, 1, 1, 0, False, 1, 1))
+    L.append(Layer("dec_fc", "linear", z, flat, 1, 1, 0, True, 1, 1))
+    dec = [(co, ci) for (ci, co) in reversed(enc)]
+    for i, (ci, co) in enumerate(dec):
+        last = i == len(dec) - 1
+        L.append(Layer(f"dec{i + 1}", "convT", ci, co, 4, 2, 1, not last, hw, hw * 2))
+        hw *= 2
+    return L
+
+
+def _w_shape(l: Layer):
+    """Our weight layout: conv/linear [Cout][K][K][Cin]; convT [Cin_t][K][K][Cout_t]."""
+    if l.kind == "convT":
+        return (l.cin, l.k, l.k, l.cout)
+    return (l.cout, l.k, l.k, l.cin)
+
+
+def conv_layout(spec: List[Layer]):
+    """[(name, offset, shape)], total; weights then bias per layer, 64-aligned."""
+    a = lambda v: (v + 63) // 64 * 64
+    out, off = [], 0
+    for l in spec:
+        ws = _w_shape(l)
+        out.append((l.name + ".weight", off, ws))
+        off = a(off + math.prod(ws))
+        out.append((l.name + ".bias", off, (l.cout,)))
+        off = a(off + l.cout)
+    return out, off
+
+
+# --------------------------------------------------------------------------
+class TorchConvVAE(nn.Module):
+    """Reference network in stock torch ops (fp32, NCHW; Linear inputs flattened
+    in NHWC order so weights map 1:1 onto the kernel layout)."""
+
+    def __init__(self, spec: List[Layer], image: int, channels: int, z: int):
+        super().__init__()
+        self.spec, self.image, self.channels, self.z = spec, image, channels, z
+        mods = {}
+        for l in spec:
+            if l.kind == "conv":
+                mods[l.name] = nn.Conv2d(l.cin, l.cout, l.k, l.s, l.p)
+            elif l.kind == "convT":
+                mods[l.name] = nn.ConvTranspose2d(l.cin, l.cout, l.k, l.s, l.p)
+            else:
+                mods[l.name] = nn.Linear(l.cin, l.cout)
+        self.layers = nn.ModuleDict(mods)
+
+    def _run(self, layers, h):
+        for l in layers:
+            m = self.layers[l.name]
+            if l.kind == "linear":
+                if h.dim() == 4:  # NCHW -> NHWC flatten
+                    h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)
+                h = m(h)
+            else:
+                if h.dim() == 2:  # NHWC flat -> NCHW
+                    c = l.cin
+                    hw = int(round(math.sqrt(h.shape[1] // c)))
+                    h = h.view(h.shape[0], hw, hw, c).permute(0, 3, 1, 2)
+                h = m(h)
+            if l.relu:
+                h = F.relu(h)
+        return h
+
+    def encode(self, x):
+        enc = [l for l in self.spec if l.name.startswith("enc")]
+        h = self._run(enc, x.view(-1, self.channels, self.image, self.image))
+        return h[:, : self.z], h[:, self.z:]
+
+    def decode_logits(self, zz):
+        dec = [l for l in self.spec if l.name.startswith("dec")]
+        return self._run(dec, zz)
+
+    def forward(self, x, eps):
+        mu, lv = self.encode(x)
+        zz = mu + eps * torch.exp(0.5 * lv)
+        t = self.decode_logits(zz)
+        return t, mu, lv
+
+    def loss(self, x, eps, beta: float = 1.0):
+        t, mu, lv = self.forward(x, eps)
+        xt = x.view(x.shape[0], self.image, self.image, self.channels).permute(0, 3, 1, 2)
+        sp_pos = torch.clamp(t, min=0) + torch.log1p(torch.exp(-t.abs()))
+        bce = (xt * torch.clamp(sp_pos - t, max=100.0) + (1 - xt) * torch.clamp(sp_pos, max=100.0)).sum()
+        kld = -0.5 * torch.sum(1 + lv - mu.pow(2) - lv.exp())
+        return bce + beta * kld, t, mu, lv
+
+    # weight mapping between torch modules and the kernel arena layout
+    def to_arena(self) -> Dict[str, torch.Tensor]:
+        out = {}
+        for l in self.spec:
+            m = self.layers[l.name]
+            w = m.weight.detach()
+            if l.kind in ("conv", "convT"):
+                w = w.permute(0, 2, 3, 1).contiguous()
+            else:
+                w = w.reshape(l.cout, 1, 1, l.cin)
+            out[l.name + ".weight"] = w
+            out[l.name + ".bias"] = m.bias.detach()
+        return out
+
+    @torch.no_grad()
+    def from_arena(self, d: Dict[str, torch.Tensor]):
+        for l in self.spec:
+            m = self.layers[l.name]
+            w = d[l.name + ".weight"].to(m.weight.device, m.weight.dtype)
+            if l.kind in ("conv", "convT"):
+                m.weight.copy_(w.permute(0, 3, 1, 2))
+            else:
+                m.weight.copy_(w.reshape(l.cout, l.cin))
+            m.bias.copy_(d[l.name + ".bias"])
+
+    def grads_to_arena(self) -> Dict[str, torch.Tensor]:
+        out = {}
+        for l in self.spec:
+            m = self.layers[l.name]
+            g = m.weight.grad
+            if l.kind in ("conv", "convT"):
+                g = g.permute(0, 2, 3, 1).contiguous()
+            else:
+                g = g.reshape(l.cout, 1, 1, l.cin)
+            out[l.name + ".weight"] = g
+            out[l.name + ".bias"] = m.bias.grad
+        return out
+
+
+# --------------------------------------------------------------------------
+class ConvVaeTrainer:
+    """One trial of the conv VAE. Same driver-facing API as MlpVaeTrainer."""
+
+    def __init__(self, batch_size: int = 128, image: int = 28, channels: int = 1, z: int = 32, device=None,
+                 backend: Optional[str] = None, seed: int = 0, lr: float = 1e-3, kl_beta: float = 1.0,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, decoupled_wd: bool = False,
+                 rng_stream: int = 0, use_graphs: bool = True, graph_steps: int = 10, init_seed: Optional[int] = None):
+        self.B, self.image, self.channels, self.Z = batch_size, image, channels, z
+        self.D = image * image * channels
+        self.H = None
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        backend = backend or ("hip" if self.device.type == "cuda" else "torch")
+        self.backend = backend
+        self.seed, self.rng_stream = int(seed), int(rng_stream)
+        self.hp = dict(lr=lr, beta1=betas[0], beta2=betas[1], eps=eps, weight_decay=weight_decay,
+                       kl_beta=kl_beta, grad_scale=1.0)
+        self.decoupled_wd = decoupled_wd
+        self.spec = conv_vae_spec(image, channels, z)
+        self.layout, self.numel = conv_layout(self.spec)
+        self.split = self.layout[-2][1] if len(self.layout) >= 2 else 0
+        self.use_graphs = use_graphs and backend == "hip"
+        self.graph_steps = max(1, graph_steps)
+        self._graphs = {}
+        self.reducer = None
+        self._data = None
+        torch.manual_seed(self.seed if init_seed is None else init_seed)
+        ref = TorchConvVAE(self.spec, image, channels, z)
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.params = torch.zeros(self.numel, **f32)
+        self.grads = torch.zeros(self.numel, **f32)
+        self.exp_avg = torch.zeros(self.numel, **f32)
+        self.exp_avg_sq = torch.zeros(self.numel, **f32)
+        for name, t in ref.to_arena().items():
+            self.named_parameters()[name].copy_(t)
+        if backend == "torch":
+            self.model = ref.to(self.device)
+            self._st = dict(step=0, cursor=0, nbatches=0, epoch_loss=0.0, epoch_count=0.0)
+            self._st_eval = dict(step=0, cursor=0, nbatches=0, epoch_loss=0.0, epoch_count=0.0)
+            self._hist = np.zeros(4096, np.float32)
+            self._hist_eval = np.zeros(4096, np.float32)
+        else:
+            self.C = native.require()
+            self.state = self.C.TrialState(self.device.index or 0)
+            self._alloc_hip()
+        self._push_hparams()
+
+    # ----------------------------------------------------------- arenas
+    def named_parameters(self):
+        return {n: self.params.narrow(0, o, math.prod(s)).view(s) for n, o, s in self.layout}
+
+    def named_grads(self):
+        return {n: self.grads.narrow(0, o, math.prod(s)).view(s) for n, o, s in self.layout}
+
+    def state_dict(self):
+        return {k: v.detach().cpu().clone() for k, v in self.named_parameters().items()}
+
+    @torch.no_grad()
+    def load_state_dict(self, sd):
+        for k, t in self.named_parameters().items():
+            t.copy_(sd[k].to(t.device, torch.float32))
+        if self.backend == "hip":
+            self._cast_weights()
+        else:
+            self.model.from_arena(self.named_parameters())
+
+    def optimizer_state(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg.cpu().clone(), "exp_avg_sq": self.exp_avg_sq.cpu().clone()}
+
+    @torch.no_grad()
+    def load_optimizer_state(self, st):
+        self.exp_avg.copy_(st["exp_avg"])
+        self.exp_avg_sq.copy_(st["exp_avg_sq"])
+        self.set_step(int(st["step"]))
+
+    def set_hparams(self, **kw):
+        for k, v in kw.items():
+            self.hp[k] = float(v)
+        self._push_hparams()
+
+    def _push_hparams(self):
+        if self.backend == "hip":
+            h = self.hp
+            self.state.set_hparams(h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"], h["kl_beta"],
+                                   h["grad_scale"], self.seed, self.decoupled_wd)
+
+    # ----------------------------------------------------------- state
+    @property
+    def step_count(self):
+        return int(self.read_state()["step"])
+
+    def set_step(self, step):
+        if self.backend == "hip":
+            self.state.set_step(False, int(step))
+        else:
+            self._st["step"] = int(step)
+
+    def set_cursor(self, cursor, nbatches, eval=False):
+        if self.backend == "hip":
+            self.state.set_cursor(eval, int(cursor), int(nbatches))
+        else:
+            st = self._st_eval if eval else self._st
+            st["cursor"], st["nbatches"] = int(cursor), int(nbatches)
+
+    def reset_loss(self, eval=False):
+        if self.backend == "hip":
+            self.state.reset_loss(eval)
+        else:
+            st = self._st_eval if eval else self._st
+            st["epoch_loss"], st["epoch_count"] = 0.0, 0.0
+
+    def read_state(self, eval=False):
+        if self.backend == "hip":
+            s = self.state.read_state(eval)
+            return dict(step=int(s[0]), cursor=int(s[1]), nbatches=int(s[2]), epoch_loss=s[3], epoch_count=s[4])
+        return dict(self._st_eval if eval else self._st)
+
+    def loss_history(self, eval=False):
+        if self.backend == "hip":
+            return self.state.loss_history(eval).numpy()
+        return (self._hist_eval if eval else self._hist).copy()
+
+    def bind_train_data(self, X, idx):
+        assert X.dim() == 2 and X.shape[1] == self.D and X.dtype == torch.float32
+        n = idx.numel()
+        nb = -(-n // self.B)
+        idx = idx.to(device=self.device, dtype=torch.int32)
+        pad = nb * self.B - n
+        if pad:
+            idx = torch.cat([idx, idx[:1].expand(pad)])
+        self._data = (X.contiguous(), idx.contiguous(), n, nb)
+        self._graphs.clear()
+
+    def attach_reducer(self, reducer):
+        self.reducer = reducer
+        self._graphs.clear()
+
+    # ----------------------------------------------------------- HIP path
+    def _alloc_hip(self):
+        dev = self.device
+        B = self.B
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.w16 = torch.zeros(self.numel, **bf)
+        tl, toff = [], 0
+        segs = []
+        lay = {n: (o, s) for n, o, s in self.layout}
+        for l in self.spec:
+            o, s = lay[l.name + ".weight"]
+            tl.append(toff)
+            segs.append([o, math.prod(s), s[0], s[1] * s[2], s[3], toff])
+            toff = (toff + math.prod(s) + 63) // 64 * 64
+            ob, sb = lay[l.name + ".bias"]
+            segs.append([ob, sb[0], 0, 0, 0, -1])
+        self.w16t = torch.zeros(max(toff, 64), **bf)
+        self._toff = dict(zip([l.name for l in self.spec], tl))
+        self.segs = self.C.make_adam_segs(segs, dev.index or 0)
+        self.nseg = len(segs)
+        self.xb = torch.zeros(B, self.D, **f32)
+        self.acts, self.gacts = {}, {}
+        for l in self.spec:
+            n_out = B * l.out_hw * l.out_hw * l.cout
+            self.acts[l.name] = torch.zeros(n_out, **bf)
+            self.gacts[l.name] = torch.zeros(n_out, **bf)
+        zf = self.Z
+        self.mulv = torch.zeros(B, 2 * zf, **f32)
+        self.eps = torch.zeros(B, zf, **f32)
+        self.z16 = torch.zeros(B, zf, **bf)
+        self.dz = torch.zeros(B, zf, **f32)
+        self.dmulv = torch.zeros(B, 2 * zf, **f32)
+        self.dmulv16 = torch.zeros(B, 2 * zf, **bf)
+        self.logits = torch.zeros(B * self.D, **f32)
+        self.recon = torch.zeros(B * self.D, **f32)
+        self.dlog16 = torch.zeros(B * self.D, **bf)
+        self.bce_part = torch.zeros(-(-B * self.D // 256), **f32)
+        self.kld_part = torch.zeros(-(-B * zf // 256), **f32)
+        self._cast_weights()
+
+    def _cast_weights(self):
+        h = self.state
+        self.C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.w16t, self.segs,
+                         self.nseg, h.train_state, h.hparams, False)
+
+    def _w(self, l):
+        o, s = next((o, s) for n, o, s in self.layout if n == l.name + ".weight")
+        return self.w16.narrow(0, o, math.prod(s))
+
+    def _wt(self, l):
+        s = _w_shape(l)
+        return self.w16t.narrow(0, self._toff[l.name], math.prod(s))
+
+    def _b(self, l):
+        return self.named_parameters()[l.name + ".bias"]
+
+    def _gw(self, l):
+        o, s = next((o, s) for n, o, s in self.layout if n == l.name + ".weight")
+        return self.grads.narrow(0, o, math.prod(s))
+
+    def _gb(self, l):
+        return self.named_grads()[l.name + ".bias"]
+
+    @staticmethod
+    def _desc(l: Layer, M: int):
+        if l.kind == "convT":  # conv geometry: conv input = convT output
+            return [M, l.out_hw, l.out_hw, l.cout, l.in_hw, l.in_hw, l.cin, l.k, l.k, l.s, l.p]
+        return [M, l.in_hw, l.in_hw, l.cin, l.out_hw, l.out_hw, l.cout, l.k, l.k, l.s, l.p]
+
+    def _forward_hip(self, M, state, stream, want_recon=False, train=True):
+        C = self.C
+        spec = self.spec
+        enc = [l for l in spec if l.name.startswith("enc")]
+        dec = [l for l in spec if l.name.startswith("dec")]
+        h = self.xb
+        for l in enc:
+            d = self._desc(l, M)
+            last = l is enc[-1]
+            out16 = None if last else self.acts[l.name]
+            out32 = self.mulv if last else None
+            C.conv_fwd(h, None, self._w(l), d, self._b(l), l.relu, out16, out32)
+            h = self.acts[l.name]
+        C.reparam(self.mulv, self.eps, self.z16, None, M, self.Z, state, self.state.hparams, stream, self.kld_part)
+        h = self.z16
+        for l in dec:
+            d = self._desc(l, M)
+            last = l is dec[-1]
+            out16 = None if last else self.acts[l.name]
+            out32 = self.logits if last else None
+            if l.kind == "convT":
+                C.conv_dgrad(h, None, self._wt(l), d, self._b(l), l.relu, out16, out32)
+            else:
+                C.conv_fwd(h, None, self._w(l), d, self._b(l), l.relu, out16, out32)
+            h = self.acts[l.name]
+        C.bce_logits(self.logits, self.xb, None, M, self.D, self.dlog16 if train else None,
+                     self.recon if want_recon else None, self.bce_part)
+
+    def _backward_hip(self, M):
+        C = self.C
+        spec = self.spec
+        self.grads.zero_()
+        idx_of = {l.name: i for i, l in enumerate(spec)}
+        g = self.dlog16
+        for l in reversed(spec):
+            i = idx_of[l.name]
+            prev = spec[i - 1] if i > 0 else None
+            d = self._desc(l, M)
+            if l.name == "dec_fc":
+                a_in = self.z16
+            elif prev is None:
+                a_in = self.xb
+            elif l.name == "enc_head":
+                a_in = self.acts[prev.name]
+            else:
+                a_in = self.acts[prev.name]
+            if prev is not None and prev.name == "enc_head":
+                a_in = self.z16
+            omask = a_in if (prev is not None and prev.relu and l.name != "dec_fc") else None
+            if l.kind == "convT":
+                C.conv_wgrad(a_in, None, g, None, d, self._gw(l), None)
+                C.chan_sum(g, M * l.out_hw * l.out_hw, l.cout, self._gb(l))
+                gin = self.gacts[prev.name]
+                C.conv_fwd(g, None, self._w(l), d, None, False, gin, None, omask)
+            else:
+                C.conv_wgrad(g, None, a_in, None, d, self._gw(l), self._gb(l))
+                if prev is None:
+                    break
+                if l.name == "dec_fc":
+                    C.conv_dgrad(g, None, self._wt(l), d, None, False, None, self.dz)
+                    C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M, self.Z, self.state.hparams)
+                    gin = self.dmulv16
+                else:
+                    gin = self.gacts[prev.name]
+                    C.conv_dgrad(g, None, self._wt(l), d, None, False, gin, None, omask)
+            g = gin
+
+    def _step_hip(self, M):
+        C = self.C
+        X, idx = self._data[0], self._data[1]
+        st = self.state
+        C.step_begin(st.train_state, st.hparams)
+        C.gather_rows(X, idx, st.train_state, self.B, M, self.xb)
+        self._forward_hip(M, st.train_state, self.rng_stream)
+        C.loss_finalize2(self.bce_part, -(-M * self.D // 256), self.kld_part, -(-M * self.Z // 256),
+                         st.train_state, st.hparams, True)
+        self._backward_hip(M)
+        if self.reducer is not None:
+            self.reducer.launch_all()
+            self.reducer.wait_all()
+        C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.w16t, self.segs,
+                    self.nseg, st.train_state, st.hparams, True)
+
+    # ----------------------------------------------------------- torch path
+    def _step_torch(self, M):
+        X, idx = self._data[0], self._data[1]
+        st = self._st
+        rows = idx[st["cursor"] * self.B: st["cursor"] * self.B + M].long()
+        x = X[rows]
+        eps = torch.from_numpy(reparam_eps(M, self.Z, self.seed, self.rng_stream, st["step"])).to(self.device)
+        self.model.zero_grad(set_to_none=True)
+        loss, *_ = self.model.loss(x, eps, self.hp["kl_beta"])
+        loss.backward()
+        with torch.no_grad():
+            gv = self.named_grads()
+            for k, v in self.model.grads_to_arena().items():
+                gv[k].copy_(v)
+            if self.reducer is not None:
+                self.reducer.launch_all()
+                self.reducer.wait_all()
+            h = self.hp
+            reference_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, st["step"] + 1, h["lr"],
+                            h["beta1"], h["beta2"], h["eps"], h["weight_decay"], h["grad_scale"], self.decoupled_wd)
+            self.model.from_arena(self.named_parameters())
+        lv = float(loss)
+        self._hist[st["step"] % 4096] = lv
+        st["epoch_loss"] += lv
+        st["epoch_count"] += 1
+        st["step"] += 1
+        st["cursor"] += 1
+        if st["nbatches"] and st["cursor"] >= st["nbatches"]:
+            st["cursor"] = 0
+
+    # ----------------------------------------------------------- driver API
+    def train_steps(self, n, M=None):
+        M = self.B if M is None else M
+        if n <= 0:
+            return
+        if self.backend == "torch":
+            for _ in range(n):
+                self._step_torch(M)
+            return
+        if not self.use_graphs:
+            for _ in range(n):
+                self._step_hip(M)
+            return
+        S = self.graph_steps
+        while n >= S:
+            self._replay(S, M)
+            n -= S
+        for _ in range(n):
+            self._replay(1, M)
+
+    def _replay(self, S, M):
+        g = self._graphs.get((S, M))
+        if g is None:
+            g = self._capture(S, M)
+            self._graphs[(S, M)] = g
+        g.replay()
+
+    def _capture(self, S, M):
+        snap = [t.clone() for t in (self.params, self.exp_avg, self.exp_avg_sq, self.state.train_state)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._step_hip(M)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(S):
+                self._step_hip(M)
+        for t, v in zip((self.params, self.exp_avg, self.exp_avg_sq, self.state.train_state), snap):
+            t.copy_(v)
+        self._cast_weights()
+        return g
+
+    @torch.no_grad()
+    def evaluate(self, X, idx, want_first_recon=True):
+        idx = idx.to(device=self.device, dtype=torch.int32).contiguous()
+        n = idx.numel()
+        nb = -(-n // self.B)
+        pad = nb * self.B - n
+        if pad:
+            idx = torch.cat([idx, idx[:1].expand(pad)])
+        self.set_cursor(0, nb, eval=True)
+        self.reset_loss(eval=True)
+        first = None
+        for b in range(nb):
+            M = min(self.B, n - b * self.B)
+            if self.backend == "hip":
+                st = self.state
+                self.C.step_begin(st.eval_state, st.hparams)
+                self.C.gather_rows(X.contiguous(), idx, st.eval_state, self.B, M, self.xb)
+                want = want_first_recon and b == 0
+                self._forward_hip(M, st.eval_state, EVAL_STREAM + self.rng_stream, want_recon=want, train=False)
+                self.C.loss_finalize2(self.bce_part, -(-M * self.D // 256), self.kld_part, -(-M * self.Z // 256),
+                                      st.eval_state, st.hparams, True)
+                if want:
+                    first = self.recon[: M * self.D].view(M, self.D).clone()
+            else:
+                st = self._st_eval
+                rows = idx[b * self.B: b * self.B + M].long()
+                x = X[rows]
+                eps = torch.from_numpy(reparam_eps(M, self.Z, self.seed, EVAL_STREAM + self.rng_stream,
+                                                   st["step"])).to(self.device)
+                loss, t, _, _ = self.model.loss(x, eps, self.hp["kl_beta"])
+                if want_first_recon and b == 0:
+                    first = torch.sigmoid(t).permute(0, 2, 3, 1).reshape(M, self.D).clone()
+                lv = float(loss)
+                self._hist_eval[st["step"] % 4096] = lv
+                st["epoch_loss"] += lv
+                st["epoch_count"] += 1
+                st["step"] += 1
+        return self.read_state(eval=True)["epoch_loss"], first
+
+    @torch.no_grad()
+    def decode(self, zz):
+        zz = zz.to(self.device, torch.float32)
+        if self.backend == "torch":
+            t = self.model.decode_logits(zz)
+            return torch.sigmoid(t).permute(0, 2, 3, 1).reshape(zz.shape[0], self.D)
+        outs = []
+        dec = [l for l in self.spec if l.name.startswith("dec")]
+        for i in range(0, zz.shape[0], self.B):
+            zc = zz[i:i + self.B]
+            M = zc.shape[0]
+            self.z16[:M].copy_(zc.to(torch.bfloat16))
+            h = self.z16
+            for l in dec:
+                d = self._desc(l, M)
+                last = l is dec[-1]
+                o16 = None if last else self.acts[l.name]
+                o32 = self.logits if last else None
+                if l.kind == "convT":
+                    self.C.conv_dgrad(h, None, self._wt(l), d, self._b(l), l.relu, o16, o32)
+                else:
+                    self.C.conv_fwd(h, None, self._w(l), d, self._b(l), l.relu, o16, o32)
+                h = self.acts[l.name]
+            outs.append(torch.sigmoid(self.logits[: M * self.D].view(M, self.D)).clone())
+        return torch.cat(outs)
+
+    def flops_per_sample(self):
+        f = 0
+        for l in self.spec:
+            f += 2 * l.out_hw * l.out_hw * l.cout * l.k * l.k * l.cin if l.kind != "convT" else \
+                2 * l.in_hw * l.in_hw * l.cin * l.k * l.k * l.cout
+        return 3 * f

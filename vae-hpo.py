@@ -53,6 +53,9 @@ def parse_args(argv=None):
     parser.add_argument("--data-dir", type=str, default="data")
     parser.add_argument("--train-samples", type=int, default=None)
     parser.add_argument("--test-samples", type=int, default=None)
+    parser.add_argument("--model", type=str, default="mlp", choices=["mlp", "conv"],
+                        help="mlp = reference MLP-VAE (fp32); conv = bf16 conv/deconv VAE")
+    parser.add_argument("--image-size", type=int, default=28, choices=[28, 128])
     return parser.parse_args(argv)
 
 
@@ -70,7 +73,8 @@ def main(argv=None):
                       ckpt_dir=args.ckpt_dir, resume=args.resume, metrics_dir=args.metrics_dir,
                       results=not args.no_results, per_group_results=args.per_group_results,
                       train_samples=args.train_samples, test_samples=args.test_samples,
-                      data_dir=args.data_dir, synthetic=False if args.real_data else True)
+                      data_dir=args.data_dir, synthetic=False if args.real_data else True,
+                      model=args.model, image_size=args.image_size)
     results = []
     member = False
     for group_id, group in enumerate(processes_groups):
