@@ -37,6 +37,7 @@ from ..obs import trace
 from ..parallel.ddp import broadcast_params, make_arena_reducer
 from ..parallel.groups import print0
 from ..runtime.bootstrap import bound_device, global_barrier
+from ..runtime.faults import guarded, maybe_inject
 from ..utils.images import save_image
 from .trial import TrialSpec
 
@@ -74,6 +75,8 @@ class TrialResult:
     wall_s: float
     final_train_loss: float = float("nan")
     final_test_loss: float = float("nan")
+    failed: bool = False
+    error: str = ""
     extra: dict = field(default_factory=dict)
 
 
@@ -188,30 +191,46 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
 
     t0 = time.time()
     train_loss = test_loss = float("nan")
-    for epoch in range(start_epoch, spec.epochs + 1):
-        te = time.perf_counter()
-        train_loss = _train_epoch(trainer, epoch, n_shard, len(train), opts, group)
-        t_train = time.perf_counter() - te
-        if opts.eval_each_epoch:
-            test_loss = _test_epoch(trainer, epoch, test, opts, group, rdir, shape)
-        if rdir is not None:
-            with torch.no_grad():
-                sample = torch.randn(64, trainer.Z, generator=gen).to(device)
-                sample = trainer.decode(sample).cpu()
-                os.makedirs(rdir, exist_ok=True)
-                save_image(sample.view(64, *shape), f"{rdir}/sample_" + str(epoch) + ".png")
-        if opts.ckpt_dir and grank == 0:
-            ckpt.save_trial(opts.ckpt_dir, trainer, spec, epoch)
-        metrics.log(epoch=epoch, train_loss_sum=train_loss, train_loss=train_loss / len(train),
-                    test_loss=test_loss, epoch_train_s=t_train, samples=n_shard,
-                    train_samples_per_s=n_shard / max(t_train, 1e-9), lr=spec.lr, beta=spec.beta)
+    failure = {}
+    epochs_done = 0
+
+    def _fail(e):
+        failure["error"] = f"{type(e).__name__}: {e}"
+        metrics.log(event="trial_failed", error=failure["error"])
+
+    with guarded(f"trial {spec.group_id} (world rank {world_rank})", group, _fail):
+        for epoch in range(start_epoch, spec.epochs + 1):
+            maybe_inject(trial=spec.group_id, epoch=epoch, rank=world_rank)
+            train_loss, test_loss = _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape,
+                                               gen, device, spec, grank, metrics)
+            epochs_done += 1
 
     global_barrier()  # parity: vae-hpo.py:172 (waits for the slowest trial)
     t1 = time.time()
     print(world_rank, "Done. time: %f" % (t1 - t0), flush=True)
-    epochs_run = max(0, spec.epochs - start_epoch + 1)
-    return TrialResult(spec.group_id, epochs_run, n_shard, epochs_run * n_shard, t1 - t0,
-                       train_loss / len(train), test_loss)
+    return TrialResult(spec.group_id, epochs_done, n_shard, epochs_done * n_shard, t1 - t0,
+                       train_loss / len(train), test_loss, failed=bool(failure), error=failure.get("error", ""))
+
+
+def _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape, gen, device, spec, grank, metrics):
+    te = time.perf_counter()
+    train_loss = _train_epoch(trainer, epoch, n_shard, len(train), opts, group)
+    t_train = time.perf_counter() - te
+    test_loss = float("nan")
+    if opts.eval_each_epoch:
+        test_loss = _test_epoch(trainer, epoch, test, opts, group, rdir, shape)
+    if rdir is not None:
+        with torch.no_grad():
+            sample = torch.randn(64, trainer.Z, generator=gen).to(device)
+            sample = trainer.decode(sample).cpu()
+            os.makedirs(rdir, exist_ok=True)
+            save_image(sample.view(64, *shape), f"{rdir}/sample_" + str(epoch) + ".png")
+    if opts.ckpt_dir and grank == 0:
+        ckpt.save_trial(opts.ckpt_dir, trainer, spec, epoch)
+    metrics.log(epoch=epoch, train_loss_sum=train_loss, train_loss=train_loss / len(train),
+                test_loss=test_loss, epoch_train_s=t_train, samples=n_shard,
+                train_samples_per_s=n_shard / max(t_train, 1e-9), lr=spec.lr, beta=spec.beta)
+    return train_loss, test_loss
 
 
 def idle_rank():

@@ -99,8 +99,13 @@ def setup_ddp_groups(num_groups: int, verbose: bool = True, backend: Optional[st
         print("world_size, world_rank:", world_size, world_rank)
     plan = GroupPlan(world_size, num_groups)
     handles = []
+    import datetime as _dt
+
+    from ..runtime.faults import group_timeout_s
+
     for g in range(num_groups):
-        kw = {"ranks": plan.ranks(g)}
+        # bounded collective timeout: a dead replica fails its group fast
+        kw = {"ranks": plan.ranks(g), "timeout": _dt.timedelta(seconds=group_timeout_s())}
         if backend is not None:
             kw["backend"] = backend
         handles.append(dist.new_group(**kw))

@@ -137,3 +137,20 @@ def test_vae_hpo_idle_leftover_rank(tmp_path):
     text = "\n".join(outs)
     assert rc == 0, text  # the reference crashes here
     assert "Rank 2 is in group" not in text
+
+
+def test_failed_trial_is_isolated(tmp_path):
+    """An injected failure in trial 1 does not stop trial 0 (reference: crash/hang)."""
+    old = dict(ENV)
+    ENV["MDT_FAULT"] = "trial=1,epoch=1"
+    try:
+        rc, outs = _vae_hpo(tmp_path, 2, "--epochs", "1", "--ngroups", "2", "--no-results")
+    finally:
+        ENV.clear()
+        ENV.update(old)
+    text = "\n".join(outs)
+    assert rc == 0, text
+    assert "trial 1 (world rank 1) FAILED: InjectedFault" in text
+    assert re.search(r"^\[0:0\] ====> Test set loss", text, re.M)
+    agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
+    assert agg["failed_trials"] == [1] and agg["samples"] == 512

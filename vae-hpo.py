@@ -85,19 +85,22 @@ def main(argv=None):
         idle_rank()
 
     # aggregate samples/s: samples once per trial, max wall over ranks
-    mine = [(r.group_id, r.samples, r.wall_s) for r in results]
+    mine = [(r.group_id, r.samples, r.wall_s, r.failed) for r in results]
     gathered = [None] * dist.get_world_size()
     dist.all_gather_object(gathered, mine, group=control_group())
     if dist.get_rank() == 0:
-        per_trial, wall = {}, 0.0
+        per_trial, wall, failed = {}, 0.0, set()
         for lst in gathered:
-            for gid, samples, w in lst or []:
-                per_trial[gid] = samples
+            for gid, samples, w, bad in lst or []:
+                per_trial[gid] = min(per_trial.get(gid, samples), samples)
                 wall = max(wall, w)
+                if bad:
+                    failed.add(gid)
         summary = {"metric": "aggregate VAE samples/sec across K concurrent HPO trials",
                    "trials": len(per_trial), "samples": int(sum(per_trial.values())),
                    "wall_s": round(wall, 4),
-                   "value": round(sum(per_trial.values()) / max(wall, 1e-9), 1), "unit": "samples/s"}
+                   "value": round(sum(per_trial.values()) / max(wall, 1e-9), 1), "unit": "samples/s",
+                   "failed_trials": sorted(failed)}
         if args.metrics_dir:
             os.makedirs(args.metrics_dir, exist_ok=True)
             with open(os.path.join(args.metrics_dir, "aggregate.json"), "w") as f:
