@@ -1,0 +1,854 @@
+// LDS-tiled implicit-GEMM convolution kernels for the conv-VAE on CDNA4
+// (gfx950): bf16 operands, v_mfma_f32_16x16x32_bf16, f32 accumulation.
+//
+// Design (docs/KERNELS.md, "Conv/deconv VAE"):
+//  * igemm_fwd_k — forward-type GEMM  Y[rows][cols] = sum_k A(row, k) * Bw[col][k]
+//      kModeConv : rows = conv output pixels, k = (ky, kx, ci)   (conv fwd, convT bwd-data)
+//      kModeTconv: rows = conv INPUT pixels of one stride-parity class (blockIdx.z),
+//                  k = (ty, tx, co) over the taps that actually hit the class
+//                  (conv bwd-data, convT fwd). No zero-insertion work: for the
+//                  k4/s2 layers each class sees exactly 2x2 of the 16 taps.
+//  * wgrad_k     — dW[co][k'] = sum_m G[m][co] * im2col(X)[m][k'] with the m
+//                  reduction on the MFMA k axis: both operands are staged m-major
+//                  (coalesced 16-B rows) and read with ds_read_b64_tr_b16, the
+//                  CDNA4 transposing LDS read. Split over m into f32 partial
+//                  slabs reduced deterministically by grad_finalize_k.
+//  * grad_finalize_k — partial-slab reduction (+ fused Adam, bf16 cast and
+//                  parity-ordered weight transpose when no DDP reducer runs).
+// Tiles are 64-deep in k, double-buffered in LDS (register staging: loads for
+// tile k+1 are in flight while the MFMAs of tile k run), XOR-swizzled images,
+// blockIdx remapped so neighbouring tiles share an XCD's L2.
+// Epilogues fuse bias, ReLU, the ReLU-backward mask of the produced gradient
+// and the per-block column sums that become the next layer's bias gradient.
+#include "common.h"
+#include "conv_igemm.h"
+
+namespace mdt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.mul) + n) >> f.shr; }
+
+// Bijective XCD-aware remap: blocks dispatched to the same XCD (orig % 8)
+// receive consecutive tile ids, so a tile row's A panel stays in one L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+  return z;
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ bf16x8 load_chunk(const T* p);
+template <>
+__device__ __forceinline__ bf16x8 load_chunk<__bf16>(const __bf16* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+template <>
+__device__ __forceinline__ bf16x8 load_chunk<float>(const float* p) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  bf16x8 r;
+  r[0] = (__bf16)a.x; r[1] = (__bf16)a.y; r[2] = (__bf16)a.z; r[3] = (__bf16)a.w;
+  r[4] = (__bf16)b.x; r[5] = (__bf16)b.y; r[6] = (__bf16)b.z; r[7] = (__bf16)b.w;
+  return r;
+}
+
+// Row-major [rows][64] bf16 image (128-B rows) read by rows: 16-B chunk ch of
+// row r lives at chunk slot ch ^ (r & 7).
+__device__ __forceinline__ int rimg(int r, int ch) { return (r << 7) + (((ch ^ r) & 7) << 4); }
+
+// m-major [64][WD] bf16 image read with ds_read_b64_tr_b16: the XOR keeps the
+// eight 32-B row segments a 32-lane half reads (rows 8g+q and 8g+8+q) on
+// disjoint banks for every row width used here.
+template <int WD>
+__device__ __forceinline__ int trsw(int r) {
+  if constexpr (WD == 128) return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+  else if constexpr (WD == 64) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+  else if constexpr (WD == 32) return 2 * ((r >> 3) & 1);
+  else return 0;
+}
+template <int WD>
+__device__ __forceinline__ int timg(int r, int ch) { return r * (WD * 2) + ((ch ^ trsw<WD>(r)) << 4); }
+
+// 16x16x32 MFMA operand whose 16 "rows" are image columns c0..c0+15 and whose
+// 32 k values are image rows kb..kb+31: lane l gets column l&15, rows
+// kb + 8(l>>4) + 0..7, via two transposing reads of 4 rows each.
+template <int WD>
+__device__ __forceinline__ bf16x8 tr_frag(const uint8_t* img, int c0, int kb, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int r0 = kb + 8 * g + q, r1 = r0 + 4;
+  const int ch = (c0 >> 3) + (p >> 1);
+  const int sub = (p & 1) << 3;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + timg<WD>(r0, ch) + sub));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + timg<WD>(r1, ch) + sub));
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int BM_, int BN_, int WM_, int WN_>
+struct TileCfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int KWS = 4 / (WM * WN);  // waves splitting the 64-deep k tile
+  static constexpr int FM = BM / (16 * WM), FN = BN / (16 * WN);
+  static_assert(WM * WN * KWS == 4 && KWS <= 2 && FM >= 1 && FN >= 1, "bad tile config");
+  static constexpr int RED_BYTES = KWS == 2 ? WM * WN * FM * FN * 64 * 16 : 0;
+};
+
+// ================================================================ forward ====
+struct IgArgs {
+  ConvDesc d;
+  const void* A;
+  const __bf16* B;  // [classes][Ncols][K]
+  __bf16* y16;
+  float* y32;
+  const float* bias;
+  const __bf16* omask;
+  float* colsum;    // [classes*mtiles][Ncols] or null
+  float* slab;      // split-K partials [ksplit][M][Ncols] (then no epilogue) or null
+  int relu;
+  int M, Ncols, K, mtiles, ntiles, ktiles, kt_per_split;
+  FastDiv f_pix, f_w, f_ch, f_tw;
+};
+
+template <int MODE, typename AT, bool VEC, class TC>
+__global__ void __launch_bounds__(256) igemm_fwd_k(IgArgs a) {
+  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
+  constexpr int A_CH = BM / 32;                // 16-B chunks per thread of the BM x 64 A tile
+  constexpr int B_CH = (BN * 8 + 255) / 256;   // ... of the BN x 64 B tile
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  static_assert(TC::RED_BYTES + WM * BN * 4 <= 2 * STAGE, "epilogue scratch exceeds LDS");
+  static_assert(VEC || MODE == kModeConv, "thin gathers exist for conv mode only");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
+
+  const ConvDesc& d = a.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / a.ntiles, nt = tile - mt * a.ntiles;
+  const int kz = blockIdx.y, cls = blockIdx.z;
+  const int kt0 = kz * a.kt_per_split;
+  const int kt1 = min(a.ktiles, kt0 + a.kt_per_split);
+
+  int ea = 0, eb = 0, oa = 0, ob = 0;
+  if constexpr (MODE == kModeTconv) {
+    const int ca = cls / d.S, cb = cls - ca * d.S;
+    oa = ((ca - d.P) % d.S + d.S) % d.S;
+    ob = ((cb - d.P) % d.S + d.S) % d.S;
+    ea = (oa + d.P - ca) / d.S;
+    eb = (ob + d.P - cb) / d.S;
+  }
+
+  // ---- per-thread staging coordinates (fixed for the whole k loop)
+  const int ach = tid & 7;
+  int abase[A_CH], ay[A_CH], ax[A_CH];
+  bool aok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int m = mt * BM + (tid >> 3) + 32 * i;
+    aok[i] = m < a.M;
+    const uint32_t mm = aok[i] ? (uint32_t)m : 0u;
+    const uint32_t n = fdiv(mm, a.f_pix);
+    const uint32_t rem = mm - n * a.f_pix.d;
+    const uint32_t yy = fdiv(rem, a.f_w);
+    const uint32_t xx = rem - yy * a.f_w.d;
+    if constexpr (MODE == kModeConv) {
+      abase[i] = (int)n * d.H * d.W * d.C;
+      ay[i] = (int)yy * d.S - d.P;
+      ax[i] = (int)xx * d.S - d.P;
+    } else {
+      abase[i] = (int)n * d.OH * d.OW * d.CO;
+      ay[i] = (int)yy + ea;
+      ax[i] = (int)xx + eb;
+    }
+  }
+  const AT* Ap = reinterpret_cast<const AT*>(a.A);
+  const __bf16* Bc = a.B + (size_t)cls * a.Ncols * a.K;
+
+  bf16x8 ra[A_CH], rb[B_CH];
+  auto gload = [&](int kt) {
+    const int kk = kt * 64 + 8 * ach;
+    if constexpr (VEC) {
+      const uint32_t tap = fdiv((uint32_t)kk, a.f_ch);
+      const int ch = kk - (int)(tap * a.f_ch.d);
+      const uint32_t t0 = fdiv(tap, a.f_tw);
+      const int t1 = (int)(tap - t0 * a.f_tw.d);
+      const bool kok = kk < a.K;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        int off;
+        bool ok;
+        if constexpr (MODE == kModeConv) {
+          const int iy = ay[i] + (int)t0, ix = ax[i] + t1;
+          ok = aok[i] && kok && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+          off = abase[i] + (iy * d.W + ix) * d.C + ch;
+        } else {
+          const int oy = ay[i] - (int)t0, ox = ax[i] - t1;
+          ok = aok[i] && kok && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
+          off = abase[i] + (oy * d.OW + ox) * d.CO + ch;
+        }
+        const bf16x8 v = load_chunk<AT>(Ap + (ok ? off : 0));
+        ra[i] = ok ? v : zero8();
+      }
+    } else {
+      float v[A_CH][8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = kk + j;
+        const uint32_t tap = fdiv((uint32_t)k, a.f_ch);
+        const int ch = k - (int)(tap * a.f_ch.d);
+        const uint32_t ky = fdiv(tap, a.f_tw);
+        const int kx = (int)(tap - ky * a.f_tw.d);
+        const bool kok = k < a.K;
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) {
+          const int iy = ay[i] + (int)ky, ix = ax[i] + kx;
+          const bool ok = aok[i] && kok && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+          const float x = (float)Ap[ok ? abase[i] + (iy * d.W + ix) * d.C + ch : 0];
+          v[i][j] = ok ? x : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ra[i][j] = (__bf16)v[i][j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      const int col = nt * BN + r;
+      const bool ok = r < BN && col < a.Ncols && kk < a.K;
+      const bf16x8 v = load_chunk<__bf16>(Bc + (ok ? (size_t)col * a.K + kk : 0));
+      rb[i] = ok ? v : zero8();
+    }
+  };
+  auto sstore = [&](int buf) {
+    uint8_t* As = lds + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *reinterpret_cast<bf16x8*>(As + rimg(r, ach)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      if (r < BN) *reinterpret_cast<bf16x8*>(Bs + rimg(r, ach)) = rb[i];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const uint8_t* As = lds + buf * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int s = (KWS == 2 ? 0 : 0); s < 2 / KWS; ++s) {
+      const int ks = KWS == 2 ? wk : s;
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+        af[fm] = *reinterpret_cast<const bf16x8*>(As + rimg(wm * (BM / WM) + fm * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
+        bfr[fn] = *reinterpret_cast<const bf16x8*>(Bs + rimg(wn * (BN / WN) + fn * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
+    }
+  };
+
+  if (kt0 < kt1) {
+    gload(kt0);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int buf = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) gload(kt + 1);
+    compute(buf);
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  if constexpr (KWS == 2) {  // combine the two k-halves
+    float* red = reinterpret_cast<float*>(lds);
+    const int slot = w % (WM * WN);
+    if (wk == 1) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          *reinterpret_cast<f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4) = acc[fm][fn];
+    }
+    __syncthreads();
+    if (wk == 0) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] += *reinterpret_cast<const f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4);
+    }
+  }
+
+  const bool epi = (KWS == 1) || wk == 0;
+  const int rbase = mt * BM + wm * (BM / WM) + 4 * (lane >> 4);
+  const int cbase = nt * BN + wn * (BN / WN) + (lane & 15);
+  if (a.slab) {
+    if (epi) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = rbase + fm * 16 + r;
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) {
+            const int col = cbase + fn * 16;
+            if (m < a.M && col < a.Ncols) a.slab[((size_t)kz * a.M + m) * a.Ncols + col] = acc[fm][fn][r];
+          }
+        }
+    }
+    return;
+  }
+  float cs[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) cs[fn] = 0.f;
+  if (epi) {
+    float bv[FN];
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int col = cbase + fn * 16;
+      bv[fn] = (a.bias && col < a.Ncols) ? a.bias[col] : 0.f;
+    }
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      int grow[4];
+      bool rok[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = rbase + fm * 16 + r;
+        rok[r] = m < a.M;
+        if constexpr (MODE == kModeConv) {
+          grow[r] = m;
+        } else {
+          const uint32_t mm = rok[r] ? (uint32_t)m : 0u;
+          const uint32_t n = fdiv(mm, a.f_pix);
+          const uint32_t rem = mm - n * a.f_pix.d;
+          const uint32_t yy = fdiv(rem, a.f_w);
+          const uint32_t xx = rem - yy * a.f_w.d;
+          grow[r] = ((int)n * d.H + (int)yy * d.S + oa) * d.W + (int)xx * d.S + ob;
+        }
+      }
+      float mk[4][FN];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int col = cbase + fn * 16;
+          const bool ok = rok[r] && col < a.Ncols;
+          mk[r][fn] = (a.omask && ok) ? (float)a.omask[(size_t)grow[r] * a.Ncols + col] : 1.f;
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int col = cbase + fn * 16;
+          const bool ok = rok[r] && col < a.Ncols;
+          float v = acc[fm][fn][r] + bv[fn];
+          if (a.relu) v = fmaxf(v, 0.f);
+          v = mk[r][fn] > 0.f ? v : 0.f;
+          if (ok) {
+            const size_t o = (size_t)grow[r] * a.Ncols + col;
+            if (a.y16) a.y16[o] = (__bf16)v;
+            if (a.y32) a.y32[o] = v;
+          }
+          cs[fn] += ok ? v : 0.f;
+        }
+    }
+  }
+  if (a.colsum) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      cs[fn] += __shfl_xor(cs[fn], 16, 64);
+      cs[fn] += __shfl_xor(cs[fn], 32, 64);
+    }
+    float* sc = reinterpret_cast<float*>(lds + TC::RED_BYTES);
+    if (epi && lane < 16) {
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) sc[wm * BN + wn * (BN / WN) + fn * 16 + lane] = cs[fn];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < WM; ++q) t += sc[q * BN + tid];
+      const int col = nt * BN + tid;
+      if (col < a.Ncols) a.colsum[(size_t)(cls * a.mtiles + mt) * a.Ncols + col] = t;
+    }
+  }
+}
+
+// ================================================================= wgrad ====
+struct WgArgs {
+  ConvDesc d;
+  const __bf16* G;  // [M][CO]
+  const void* X;    // NHWC conv input
+  float* out;       // [nsplit][CO][K2]
+  int M, K2, ktiles, mtiles, mt_per_split;
+  FastDiv f_pix, f_w, f_c, f_kw;
+};
+
+template <typename XT, bool VEC, class TC>
+__global__ void __launch_bounds__(256) wgrad_k(WgArgs a) {
+  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
+  constexpr int CPR_A = BM / 8, A_RPP = 256 / CPR_A, A_CH = 64 / A_RPP;
+  constexpr int CPR_B = BN / 8, B_RPP = 256 / CPR_B, B_CH = (64 + B_RPP - 1) / B_RPP;
+  constexpr int A_BYTES = 64 * BM * 2, B_BYTES = 64 * BN * 2, STAGE = A_BYTES + B_BYTES;
+  static_assert(TC::RED_BYTES <= 2 * STAGE, "reduction scratch exceeds LDS");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
+
+  const ConvDesc& d = a.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int ct = tile / a.ktiles, nt = tile - ct * a.ktiles;
+  const int split = blockIdx.y;
+  const int mt0 = split * a.mt_per_split;
+  const int mt1 = min(a.mtiles, mt0 + a.mt_per_split);
+
+  const int cha = tid % CPR_A, ra0 = tid / CPR_A;
+  const int co = ct * BM + 8 * cha;
+  const bool coka = co < d.CO;
+  const int chb = tid % CPR_B, rb0 = tid / CPR_B;
+  const XT* Xp = reinterpret_cast<const XT*>(a.X);
+  const int HWC = d.H * d.W * d.C;
+
+  // B-operand column coordinates (fixed per thread)
+  int kyv[VEC ? 1 : 8], kxv[VEC ? 1 : 8], civ[VEC ? 1 : 8];
+  bool kokv[VEC ? 1 : 8];
+#pragma unroll
+  for (int j = 0; j < (VEC ? 1 : 8); ++j) {
+    const int kp = nt * BN + 8 * chb + j;
+    kokv[j] = kp < a.K2;
+    const uint32_t tap = fdiv((uint32_t)(kokv[j] ? kp : 0), a.f_c);
+    civ[j] = (kokv[j] ? kp : 0) - (int)(tap * a.f_c.d);
+    const uint32_t ky = fdiv(tap, a.f_kw);
+    kyv[j] = (int)ky;
+    kxv[j] = (int)(tap - ky * a.f_kw.d);
+  }
+
+  bf16x8 ra[A_CH], rb[B_CH];
+  auto gload = [&](int mtile) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int m = mtile * 64 + ra0 + A_RPP * i;
+      const bool ok = coka && m < a.M;
+      const bf16x8 v = load_chunk<__bf16>(a.G + (ok ? (size_t)m * d.CO + co : 0));
+      ra[i] = ok ? v : zero8();
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int r = rb0 + B_RPP * i;
+      const int m = mtile * 64 + r;
+      const bool mok = r < 64 && m < a.M;
+      const uint32_t mm = mok ? (uint32_t)m : 0u;
+      const uint32_t n = fdiv(mm, a.f_pix);
+      const uint32_t rem = mm - n * a.f_pix.d;
+      const uint32_t oy = fdiv(rem, a.f_w);
+      const uint32_t ox = rem - oy * a.f_w.d;
+      const int iy0 = (int)oy * d.S - d.P, ix0 = (int)ox * d.S - d.P;
+      if constexpr (VEC) {
+        const int iy = iy0 + kyv[0], ix = ix0 + kxv[0];
+        const bool ok = mok && kokv[0] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        const bf16x8 v = load_chunk<XT>(Xp + (ok ? (int)n * HWC + (iy * d.W + ix) * d.C + civ[0] : 0));
+        rb[i] = ok ? v : zero8();
+      } else {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int iy = iy0 + kyv[j], ix = ix0 + kxv[j];
+          const bool ok = mok && kokv[j] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+          const float x = (float)Xp[ok ? (int)n * HWC + (iy * d.W + ix) * d.C + civ[j] : 0];
+          v[j] = ok ? x : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rb[i][j] = (__bf16)v[j];
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    uint8_t* As = lds + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int r = ra0 + A_RPP * i;
+      *reinterpret_cast<bf16x8*>(As + timg<BM>(r, cha)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int r = rb0 + B_RPP * i;
+      if (r < 64) *reinterpret_cast<bf16x8*>(Bs + timg<BN>(r, chb)) = rb[i];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const uint8_t* As = lds + buf * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2 / KWS; ++s) {
+      const int kb = 32 * (KWS == 2 ? wk : s);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) af[fm] = tr_frag<BM>(As, wm * (BM / WM) + 16 * fm, kb, lane);
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) bfr[fn] = tr_frag<BN>(Bs, wn * (BN / WN) + 16 * fn, kb, lane);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
+    }
+  };
+
+  if (mt0 < mt1) {
+    gload(mt0);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int mtile = mt0; mtile < mt1; ++mtile) {
+    const int buf = (mtile - mt0) & 1;
+    const bool more = mtile + 1 < mt1;
+    if (more) gload(mtile + 1);
+    compute(buf);
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  if constexpr (KWS == 2) {
+    float* red = reinterpret_cast<float*>(lds);
+    const int slot = w % (WM * WN);
+    if (wk == 1) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          *reinterpret_cast<f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4) = acc[fm][fn];
+    }
+    __syncthreads();
+    if (wk == 0) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] += *reinterpret_cast<const f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4);
+    }
+  }
+  if (KWS == 1 || wk == 0) {
+    float* out = a.out + (size_t)split * d.CO * a.K2;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int orow = ct * BM + wm * (BM / WM) + fm * 16 + 4 * (lane >> 4) + r;
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int kp = nt * BN + wn * (BN / WN) + fn * 16 + (lane & 15);
+          if (orow < d.CO && kp < a.K2) out[(size_t)orow * a.K2 + kp] = acc[fm][fn][r];
+        }
+      }
+  }
+}
+
+// ======================================================= small reductions ====
+// Split-K combine: y = sum_z slab[z] + bias (+relu) -> f32 and/or bf16.
+__global__ void __launch_bounds__(256) splitk_combine_k(const float* slab, int ksplit, int M, int N,
+                                                        const float* bias, int relu, float* y32, __bf16* y16) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long MN = (long long)M * N;
+  if (e >= MN) return;
+  float v = 0.f;
+  for (int z = 0; z < ksplit; ++z) v += slab[(size_t)z * MN + e];
+  if (bias) v += bias[e % N];
+  if (relu) v = fmaxf(v, 0.f);
+  if (y32) y32[e] = v;
+  if (y16) y16[e] = (__bf16)v;
+}
+
+// Column sums of a bf16 [M][N] matrix (N % 8 == 0): partial row blockIdx.y of
+// `slab` ([gridDim.y][N]) sums rows [y*rows_per, (y+1)*rows_per).
+__global__ void __launch_bounds__(256) colsum_k(const __bf16* G, int M, int N, int rows_per, float* slab) {
+  const int c8 = blockIdx.x * 256 + threadIdx.x;
+  if (c8 * 8 >= N) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = r0; r < r1; ++r) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(G + (size_t)r * N + 8 * c8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) slab[(size_t)blockIdx.y * N + 8 * c8 + j] = s[j];
+}
+
+}  // namespace mdt
+
+// =================================================================== host ====
+using namespace mdt;
+
+namespace {
+
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// forward-type tile configurations
+using F0 = TileCfg<128, 128, 2, 2>;
+using F1 = TileCfg<128, 64, 2, 2>;
+using F2 = TileCfg<128, 32, 4, 1>;
+using F3 = TileCfg<128, 16, 4, 1>;
+using F4 = TileCfg<64, 128, 2, 2>;
+using F5 = TileCfg<64, 64, 2, 2>;
+using F6 = TileCfg<64, 32, 2, 1>;
+using F7 = TileCfg<64, 16, 4, 1>;
+// weight-gradient tile configurations (co x k'), capped at 64x64 so the
+// m-split partial slabs stay small (slab bytes ~ blocks x BM x BN x 4)
+using W0 = TileCfg<64, 64, 2, 2>;
+using W1 = TileCfg<64, 32, 2, 1>;
+using W2 = TileCfg<64, 16, 4, 1>;
+using W3 = TileCfg<32, 64, 2, 2>;
+using W4 = TileCfg<32, 32, 2, 1>;
+using W5 = TileCfg<32, 16, 2, 1>;
+
+bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p) {
+  FwdPlan q{};
+  if (mode == kModeConv) {
+    q.classes = 1;
+    q.M = d.N * d.OH * d.OW;
+    q.Ncols = d.CO;
+    q.K = d.KH * d.KW * d.C;
+    q.thin = (d.C % 8) != 0;
+  } else {
+    if (d.KH % d.S || d.KW % d.S || d.H % d.S || d.W % d.S || d.CO % 8) return false;
+    q.classes = d.S * d.S;
+    q.M = d.N * (d.H / d.S) * (d.W / d.S);
+    q.Ncols = d.C;
+    q.K = (d.KH / d.S) * (d.KW / d.S) * d.CO;
+    q.thin = 0;
+  }
+  if (q.K % 8 || q.M <= 0) return false;
+  q.BN = q.Ncols >= 128 ? 128 : q.Ncols > 32 ? 64 : q.Ncols > 16 ? 32 : 16;
+  if (q.thin) q.BN = 32;
+  q.ntiles = cdiv(q.Ncols, q.BN);
+  q.ktiles = cdiv(q.K, 64);
+  q.BM = 128;
+  if ((long long)q.classes * cdiv(q.M, 128) * q.ntiles < 512) q.BM = 64;
+  q.mtiles = cdiv(q.M, q.BM);
+  const long long blocks = (long long)q.classes * q.mtiles * q.ntiles;
+  q.ksplit = 1;
+  if (allow_split && q.classes == 1 && blocks < 256 && q.ktiles >= 8) {
+    int ks = cdiv(512, blocks);
+    if (ks > q.ktiles / 4) ks = q.ktiles / 4;
+    if (ks < 1) ks = 1;
+    q.ksplit = ks;
+  }
+  q.kt_per_split = cdiv(q.ktiles, q.ksplit);
+  q.ksplit = cdiv(q.ktiles, q.kt_per_split);
+  q.colsum_rows = q.classes * q.mtiles;
+  const int bn_i = q.BN == 128 ? 0 : q.BN == 64 ? 1 : q.BN == 32 ? 2 : 3;
+  q.cfg = (q.BM == 128 ? 0 : 4) + bn_i;
+  *p = q;
+  return true;
+}
+
+bool plan_wgrad(const ConvDesc& d, WgradPlan* p) {
+  WgradPlan q{};
+  if (d.CO % 8) return false;
+  q.M = d.N * d.OH * d.OW;
+  q.K2 = d.KH * d.KW * d.C;
+  q.thin = (d.C % 8) != 0;
+  q.BM = d.CO > 32 ? 64 : 32;
+  q.BN = q.K2 > 32 ? 64 : q.K2 > 16 ? 32 : 16;
+  if (q.thin && q.BN == 32) q.BN = 64;
+  q.cotiles = cdiv(d.CO, q.BM);
+  q.ktiles = cdiv(q.K2, q.BN);
+  q.mtiles = cdiv(q.M, 64);
+  const int tiles = q.cotiles * q.ktiles;
+  int ns = cdiv(320, tiles);
+  if (ns > q.mtiles / 2) ns = q.mtiles / 2;
+  if (ns < 1) ns = 1;
+  q.mt_per_split = cdiv(q.mtiles, ns);
+  q.nsplit = cdiv(q.mtiles, q.mt_per_split);
+  q.cfg = (q.BM == 64 ? 0 : 3) + (q.BN == 64 ? 0 : q.BN == 32 ? 1 : 2);
+  *p = q;
+  return true;
+}
+
+template <int MODE, typename AT, bool VEC, class TC>
+void launch_fwd(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
+  dim3 grid(q.mtiles * q.ntiles, q.ksplit, q.classes);
+  hipLaunchKernelGGL((igemm_fwd_k<MODE, AT, VEC, TC>), grid, dim3(256), 0, s, a);
+}
+
+template <int MODE, typename AT, bool VEC>
+int dispatch_fwd_cfg(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
+  switch (q.cfg) {
+    case 0: launch_fwd<MODE, AT, VEC, F0>(a, q, s); return 0;
+    case 1: launch_fwd<MODE, AT, VEC, F1>(a, q, s); return 0;
+    case 2: launch_fwd<MODE, AT, VEC, F2>(a, q, s); return 0;
+    case 3: launch_fwd<MODE, AT, VEC, F3>(a, q, s); return 0;
+    case 4: launch_fwd<MODE, AT, VEC, F4>(a, q, s); return 0;
+    case 5: launch_fwd<MODE, AT, VEC, F5>(a, q, s); return 0;
+    case 6: launch_fwd<MODE, AT, VEC, F6>(a, q, s); return 0;
+    case 7: launch_fwd<MODE, AT, VEC, F7>(a, q, s); return 0;
+  }
+  return 2;
+}
+
+template <typename AT>
+int dispatch_thin(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
+  if (q.cfg == 2) { launch_fwd<kModeConv, AT, false, F2>(a, q, s); return 0; }
+  if (q.cfg == 6) { launch_fwd<kModeConv, AT, false, F6>(a, q, s); return 0; }
+  return 2;
+}
+
+template <typename XT, bool VEC, class TC>
+void launch_wg(const WgArgs& a, const WgradPlan& q, hipStream_t s) {
+  dim3 grid(q.cotiles * q.ktiles, q.nsplit);
+  hipLaunchKernelGGL((wgrad_k<XT, VEC, TC>), grid, dim3(256), 0, s, a);
+}
+
+}  // namespace
+
+extern "C" {
+
+// info[12] = {cfg, BM, BN, classes, M, Ncols, K, mtiles, ntiles, ktiles, ksplit, colsum_rows}
+int mdt_igemm_plan(int mode, ConvDesc d, int allow_split, int* info) {
+  FwdPlan q;
+  if (!plan_fwd(mode, d, allow_split != 0, &q)) return 1;
+  const int v[12] = {q.cfg, q.BM, q.BN, q.classes, q.M, q.Ncols, q.K, q.mtiles, q.ntiles, q.ktiles, q.ksplit,
+                     q.colsum_rows};
+  for (int i = 0; i < 12; ++i) info[i] = v[i];
+  return 0;
+}
+
+// info[8] = {cfg, BM, BN, cotiles, ktiles, mtiles, nsplit, mt_per_split}
+int mdt_wgrad_plan(ConvDesc d, int* info) {
+  WgradPlan q;
+  if (!plan_wgrad(d, &q)) return 1;
+  const int v[8] = {q.cfg, q.BM, q.BN, q.cotiles, q.ktiles, q.mtiles, q.nsplit, q.mt_per_split};
+  for (int i = 0; i < 8; ++i) info[i] = v[i];
+  return 0;
+}
+
+// Forward-type implicit GEMM. `ws` (f32, >= ksplit*M*Ncols) enables split-K
+// for deep, narrow problems (then bias/relu/y16/y32 are applied by a combine
+// pass; omask/colsum are not allowed with split-K).
+int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d, const float* bias, int relu,
+              void* y16, float* y32, const void* omask, float* colsum, float* ws, hipStream_t s) {
+  FwdPlan q;
+  const bool can_split = ws != nullptr && omask == nullptr && colsum == nullptr;
+  if (!plan_fwd(mode, d, can_split, &q)) return 1;
+  IgArgs a{};
+  a.d = d;
+  a.A = A;
+  a.B = reinterpret_cast<const __bf16*>(B16);
+  a.relu = relu;
+  a.M = q.M; a.Ncols = q.Ncols; a.K = q.K; a.mtiles = q.mtiles; a.ntiles = q.ntiles; a.ktiles = q.ktiles;
+  a.kt_per_split = q.kt_per_split;
+  if (mode == kModeConv) {
+    a.f_pix = make_fastdiv(d.OH * d.OW); a.f_w = make_fastdiv(d.OW);
+    a.f_ch = make_fastdiv(d.C); a.f_tw = make_fastdiv(d.KW);
+  } else {
+    a.f_pix = make_fastdiv((d.H / d.S) * (d.W / d.S)); a.f_w = make_fastdiv(d.W / d.S);
+    a.f_ch = make_fastdiv(d.CO); a.f_tw = make_fastdiv(d.KW / d.S);
+  }
+  if (q.ksplit > 1) {
+    a.slab = ws;
+  } else {
+    a.y16 = reinterpret_cast<__bf16*>(y16); a.y32 = y32; a.bias = bias;
+    a.omask = reinterpret_cast<const __bf16*>(omask); a.colsum = colsum;
+  }
+  int rc;
+  if (mode == kModeConv) {
+    if (q.thin) rc = a_is_f32 ? dispatch_thin<float>(a, q, s) : dispatch_thin<__bf16>(a, q, s);
+    else if (a_is_f32) rc = 3;
+    else rc = dispatch_fwd_cfg<kModeConv, __bf16, true>(a, q, s);
+  } else {
+    rc = a_is_f32 ? 3 : dispatch_fwd_cfg<kModeTconv, __bf16, true>(a, q, s);
+  }
+  if (rc) return rc;
+  if (q.ksplit > 1) {
+    const long long MN = (long long)q.M * q.Ncols;
+    hipLaunchKernelGGL(splitk_combine_k, dim3(cdiv(MN, 256)), dim3(256), 0, s, ws, q.ksplit, q.M, q.Ncols, bias,
+                       relu, y32, reinterpret_cast<__bf16*>(y16));
+  }
+  return (int)hipGetLastError();
+}
+
+int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* out, hipStream_t s) {
+  WgradPlan q;
+  if (!plan_wgrad(d, &q)) return 1;
+  WgArgs a{};
+  a.d = d;
+  a.G = reinterpret_cast<const __bf16*>(G16);
+  a.X = X;
+  a.out = out;
+  a.M = q.M; a.K2 = q.K2; a.ktiles = q.ktiles; a.mtiles = q.mtiles; a.mt_per_split = q.mt_per_split;
+  a.f_pix = make_fastdiv(d.OH * d.OW); a.f_w = make_fastdiv(d.OW);
+  a.f_c = make_fastdiv(d.C); a.f_kw = make_fastdiv(d.KW);
+  if (!q.thin) {
+    if (x_is_f32) return 3;
+    switch (q.cfg) {
+      case 0: launch_wg<__bf16, true, W0>(a, q, s); break;
+      case 1: launch_wg<__bf16, true, W1>(a, q, s); break;
+      case 2: launch_wg<__bf16, true, W2>(a, q, s); break;
+      case 3: launch_wg<__bf16, true, W3>(a, q, s); break;
+      case 4: launch_wg<__bf16, true, W4>(a, q, s); break;
+      case 5: launch_wg<__bf16, true, W5>(a, q, s); break;
+      default: return 2;
+    }
+  } else {
+    // thin inputs (C % 8 != 0): k' tiles of 16 or 64
+    switch (q.cfg) {
+      case 0: if (x_is_f32) launch_wg<float, false, W0>(a, q, s); else launch_wg<__bf16, false, W0>(a, q, s); break;
+      case 2: if (x_is_f32) launch_wg<float, false, W2>(a, q, s); else launch_wg<__bf16, false, W2>(a, q, s); break;
+      case 3: if (x_is_f32) launch_wg<float, false, W3>(a, q, s); else launch_wg<__bf16, false, W3>(a, q, s); break;
+      case 5: if (x_is_f32) launch_wg<float, false, W5>(a, q, s); else launch_wg<__bf16, false, W5>(a, q, s); break;
+      default: return 2;
+    }
+  }
+  return (int)hipGetLastError();
+}
+
+int mdt_colsum(const void* G16, int M, int N, int rows_per, float* slab, hipStream_t s) {
+  if (N % 8 || rows_per < 1) return 1;
+  dim3 grid(cdiv(N / 8, 256), cdiv(M, rows_per));
+  hipLaunchKernelGGL(colsum_k, grid, dim3(256), 0, s, reinterpret_cast<const __bf16*>(G16), M, N, rows_per, slab);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

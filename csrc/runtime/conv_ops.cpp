@@ -12,39 +12,29 @@
 
 #include "../kernels/vae_mlp.h"
 
-namespace mdt {
-struct ConvDesc {
-  int N, H, W, C;
-  int OH, OW, CO;
-  int KH, KW, S, P;
-};
-struct AdamSeg {
-  long long off, numel;
-  int co, taps, ci;
-  long long toff;
-};
-}  // namespace mdt
+#include "../kernels/conv_igemm.h"
 
 extern "C" {
-int mdt_conv_fwd(const void* X, int x_is_f32, const int* rows, const void* W16, mdt::ConvDesc d, const float* bias,
-                 int relu, void* y16, float* y32, const void* omask, hipStream_t s);
-int mdt_conv_dgrad(const void* G16, const void* mask16, const void* Wt16, mdt::ConvDesc d, const float* bias, int relu,
-                   void* y16, float* y32, const void* omask, hipStream_t s);
+int mdt_igemm_plan(int mode, mdt::ConvDesc d, int allow_split, int* info);
+int mdt_wgrad_plan(mdt::ConvDesc d, int* info);
+int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, mdt::ConvDesc d, const float* bias, int relu,
+              void* y16, float* y32, const void* omask, float* colsum, float* ws, hipStream_t s);
+int mdt_wgrad(const void* G16, const void* X, int x_is_f32, mdt::ConvDesc d, float* out, hipStream_t s);
+int mdt_colsum(const void* G16, int M, int N, int rows_per, float* slab, hipStream_t s);
 int mdt_gather_rows(const float* X, const int* idx, const void* st, int B, int M, int P, float* xb, hipStream_t s);
-int mdt_conv_wgrad(const void* G16, const void* mask16, const void* X, int x_is_f32, const int* rows, mdt::ConvDesc d,
-                   float* dW, float* db, hipStream_t s);
-int mdt_chan_sum(const void* G16, int M, int C, float* db, hipStream_t s);
 int mdt_reparam(const float* mulv, float* eps, void* z16, float* z32, int B, int Z, const void* st, const void* hp,
                 unsigned stream, float* kld_part, hipStream_t s);
 int mdt_reparam_bwd(const float* dz, const float* mulv, const float* eps, float* dmulv, void* dmulv16, int B, int Z,
                     const void* hp, hipStream_t s);
 int mdt_bce_logits(const float* logits, const float* X, const int* rows, int B, int P, void* dlog16, float* recon,
-                   float* part, hipStream_t s);
+                   float* part, float* gpart, hipStream_t s);
 int mdt_conv_loss_finalize(const float* bce_part, int nb, const float* kld_part, int nk, void* st, const void* hp,
                            int advance_cursor, hipStream_t s);
 int mdt_step_begin(void* st, const void* hp, hipStream_t s);
 int mdt_adam_cast(float* P, const float* G, float* Mo, float* Vo, void* w16, void* w16t, const void* segs, int nseg,
                   long long total, const void* st, const void* hp, int do_adam, hipStream_t s);
+int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, void* w16t, const void* segs,
+                      const void* units, int nunits, const void* st, const void* hp, int do_adam, hipStream_t s);
 }
 
 namespace mdt {
@@ -57,6 +47,7 @@ static const void* opt_ptr(const c10::optional<at::Tensor>& t) {
 
 static ConvDesc desc(const std::vector<int64_t>& v) {
   TORCH_CHECK(v.size() == 11, "conv desc needs 11 ints (N,H,W,C,OH,OW,CO,KH,KW,S,P)");
+  for (auto x : v) TORCH_CHECK(x >= 0 && x < (1 << 30), "conv desc value out of range");
   return ConvDesc{(int)v[0], (int)v[1], (int)v[2], (int)v[3], (int)v[4], (int)v[5],
                   (int)v[6], (int)v[7], (int)v[8], (int)v[9], (int)v[10]};
 }
@@ -65,51 +56,77 @@ static void check_bf16(const at::Tensor& t, const char* n) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16 && t.is_contiguous(), n,
               " must be a contiguous CUDA bfloat16 tensor");
 }
-
-void conv_fwd(const at::Tensor& X, const c10::optional<at::Tensor>& rows, const at::Tensor& W16,
-              const std::vector<int64_t>& dv, const c10::optional<at::Tensor>& bias, bool relu,
-              const c10::optional<at::Tensor>& y16, const c10::optional<at::Tensor>& y32,
-              const c10::optional<at::Tensor>& omask) {
-  const ConvDesc d = desc(dv);
-  TORCH_CHECK(X.is_cuda() && X.is_contiguous(), "X must be contiguous CUDA");
-  const bool f32 = X.scalar_type() == torch::kFloat32;
-  TORCH_CHECK(f32 || X.scalar_type() == torch::kBFloat16, "X must be f32 or bf16");
-  check_bf16(W16, "W16");
-  TORCH_CHECK(W16.numel() == (int64_t)d.CO * d.KH * d.KW * d.C, "W16 size mismatch");
-  rc(mdt_conv_fwd(X.data_ptr(), f32, (const int*)opt_ptr(rows), W16.data_ptr(), d, (const float*)opt_ptr(bias),
-                  relu, const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32), opt_ptr(omask), cur()),
-     "conv_fwd");
+static void check_f32(const at::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous(), n,
+              " must be a contiguous CUDA float32 tensor");
+}
+static void check_min(const c10::optional<at::Tensor>& t, int64_t n, const char* w) {
+  if (t.has_value() && t->defined()) TORCH_CHECK(t->numel() >= n, w, " too small: ", t->numel(), " < ", n);
 }
 
-void conv_dgrad(const at::Tensor& G16, const c10::optional<at::Tensor>& mask, const at::Tensor& Wt16,
-                const std::vector<int64_t>& dv, const c10::optional<at::Tensor>& bias, bool relu,
-                const c10::optional<at::Tensor>& y16, const c10::optional<at::Tensor>& y32,
-                const c10::optional<at::Tensor>& omask) {
+std::vector<int64_t> igemm_plan(int64_t mode, const std::vector<int64_t>& dv, bool allow_split) {
+  int info[12];
+  rc(mdt_igemm_plan((int)mode, desc(dv), allow_split ? 1 : 0, info), "igemm_plan (unsupported geometry)");
+  return std::vector<int64_t>(info, info + 12);
+}
+
+std::vector<int64_t> wgrad_plan(const std::vector<int64_t>& dv) {
+  int info[8];
+  rc(mdt_wgrad_plan(desc(dv), info), "wgrad_plan (unsupported geometry)");
+  return std::vector<int64_t>(info, info + 8);
+}
+
+// mode 0: conv (fwd / convT bwd-data), mode 1: parity-class transposed conv
+// (conv bwd-data / convT fwd; B16 = parity-ordered transposed weights).
+void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::vector<int64_t>& dv,
+           const c10::optional<at::Tensor>& bias, bool relu, const c10::optional<at::Tensor>& y16,
+           const c10::optional<at::Tensor>& y32, const c10::optional<at::Tensor>& omask,
+           const c10::optional<at::Tensor>& colsum, const c10::optional<at::Tensor>& ws) {
+  const ConvDesc d = desc(dv);
+  TORCH_CHECK(A.is_cuda() && A.is_contiguous(), "A must be contiguous CUDA");
+  const bool f32 = A.scalar_type() == torch::kFloat32;
+  TORCH_CHECK(f32 || A.scalar_type() == torch::kBFloat16, "A must be f32 or bf16");
+  check_bf16(B16, "B16");
+  int info[12];
+  rc(mdt_igemm_plan((int)mode, d, ws.has_value() && ws->defined() ? 1 : 0, info), "igemm_plan");
+  const int64_t classes = info[3], M = info[4], Ncols = info[5], K = info[6], ksplit = info[10];
+  const int64_t rows_total = classes * M;
+  const int64_t a_need = mode == kModeConv ? (int64_t)d.N * d.H * d.W * d.C : (int64_t)d.N * d.OH * d.OW * d.CO;
+  TORCH_CHECK(A.numel() >= a_need, "A too small: ", A.numel(), " < ", a_need);
+  TORCH_CHECK(B16.numel() >= classes * Ncols * K, "B16 too small");
+  check_min(y16, rows_total * Ncols, "y16");
+  check_min(y32, rows_total * Ncols, "y32");
+  check_min(omask, rows_total * Ncols, "omask");
+  check_min(bias, Ncols, "bias");
+  check_min(colsum, (int64_t)info[11] * Ncols, "colsum");
+  if (ksplit > 1) check_min(ws, ksplit * M * Ncols, "ws");
+  rc(mdt_igemm((int)mode, A.data_ptr(), f32, B16.data_ptr(), d, (const float*)opt_ptr(bias), relu,
+               const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32), opt_ptr(omask), (float*)opt_ptr(colsum),
+               (float*)opt_ptr(ws), cur()),
+     "igemm");
+}
+
+void wgrad(const at::Tensor& G16, const at::Tensor& X, const std::vector<int64_t>& dv, at::Tensor out) {
   const ConvDesc d = desc(dv);
   check_bf16(G16, "G16");
-  check_bf16(Wt16, "Wt16");
+  check_f32(out, "out");
+  const bool f32 = X.scalar_type() == torch::kFloat32;
+  TORCH_CHECK(X.is_cuda() && X.is_contiguous() && (f32 || X.scalar_type() == torch::kBFloat16), "X dtype/layout");
+  int info[8];
+  rc(mdt_wgrad_plan(d, info), "wgrad_plan");
   TORCH_CHECK(G16.numel() >= (int64_t)d.N * d.OH * d.OW * d.CO, "G16 too small");
-  rc(mdt_conv_dgrad(G16.data_ptr(), opt_ptr(mask), Wt16.data_ptr(), d, (const float*)opt_ptr(bias), relu,
-                    const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32), opt_ptr(omask), cur()),
-     "conv_dgrad");
+  TORCH_CHECK(X.numel() >= (int64_t)d.N * d.H * d.W * d.C, "X too small");
+  TORCH_CHECK(out.numel() >= (int64_t)info[6] * d.CO * d.KH * d.KW * d.C, "wgrad out too small for ", info[6],
+              " partial slabs");
+  rc(mdt_wgrad(G16.data_ptr(), X.data_ptr(), f32, d, out.data_ptr<float>(), cur()), "wgrad");
 }
 
-void conv_wgrad(const at::Tensor& G16, const c10::optional<at::Tensor>& mask, const at::Tensor& X,
-                const c10::optional<at::Tensor>& rows, const std::vector<int64_t>& dv, at::Tensor dW,
-                const c10::optional<at::Tensor>& db) {
-  const ConvDesc d = desc(dv);
+void colsum(const at::Tensor& G16, int64_t M, int64_t N, int64_t rows_per, at::Tensor slab) {
   check_bf16(G16, "G16");
-  const bool f32 = X.scalar_type() == torch::kFloat32;
-  TORCH_CHECK(dW.scalar_type() == torch::kFloat32 && dW.numel() == (int64_t)d.CO * d.KH * d.KW * d.C,
-              "dW must be f32 [CO*KH*KW*C]");
-  rc(mdt_conv_wgrad(G16.data_ptr(), opt_ptr(mask), X.data_ptr(), f32, (const int*)opt_ptr(rows), d,
-                    dW.data_ptr<float>(), (float*)opt_ptr(db), cur()),
-     "conv_wgrad");
-}
-
-void chan_sum(const at::Tensor& G16, int64_t M, int64_t C, at::Tensor db) {
-  check_bf16(G16, "G16");
-  rc(mdt_chan_sum(G16.data_ptr(), (int)M, (int)C, db.data_ptr<float>(), cur()), "chan_sum");
+  check_f32(slab, "slab");
+  TORCH_CHECK(G16.numel() >= M * N, "G16 too small");
+  TORCH_CHECK(slab.numel() >= ((M + rows_per - 1) / rows_per) * N, "colsum slab too small");
+  rc(mdt_colsum(G16.data_ptr(), (int)M, (int)N, (int)rows_per, slab.data_ptr<float>(), cur()), "colsum");
 }
 
 void reparam(const at::Tensor& mulv, at::Tensor eps, at::Tensor z16, const c10::optional<at::Tensor>& z32, int64_t B,
@@ -136,9 +153,10 @@ void gather_rows(const at::Tensor& X, const at::Tensor& idx, const at::Tensor& s
 
 void bce_logits(const at::Tensor& logits, const at::Tensor& X, const c10::optional<at::Tensor>& rows, int64_t B,
                 int64_t P, const c10::optional<at::Tensor>& dlog16, const c10::optional<at::Tensor>& recon,
-                at::Tensor part) {
+                at::Tensor part, const c10::optional<at::Tensor>& gpart) {
   rc(mdt_bce_logits(logits.data_ptr<float>(), X.data_ptr<float>(), (const int*)opt_ptr(rows), (int)B, (int)P,
-                    const_cast<void*>(opt_ptr(dlog16)), (float*)opt_ptr(recon), part.data_ptr<float>(), cur()),
+                    const_cast<void*>(opt_ptr(dlog16)), (float*)opt_ptr(recon), part.data_ptr<float>(),
+                    (float*)opt_ptr(gpart), cur()),
      "bce_logits");
 }
 
@@ -153,14 +171,32 @@ void step_begin(at::Tensor state, const at::Tensor& hparams) {
   rc(mdt_step_begin(state.data_ptr(), hparams.data_ptr(), cur()), "step_begin");
 }
 
-at::Tensor make_adam_segs(const std::vector<std::vector<int64_t>>& segs, int64_t device_index) {
-  std::vector<AdamSeg> v;
+// segment = (off, numel, slab_ptr, nsplit, co, k, s, ci, toff); slab_ptr is a
+// device address (tensor.data_ptr()) or 0. The caller keeps the slabs alive.
+at::Tensor make_grad_segs(const std::vector<std::vector<int64_t>>& segs, int64_t device_index) {
+  std::vector<GradSeg> v;
   for (auto& s : segs) {
-    TORCH_CHECK(s.size() == 6, "segment = (off, numel, co, taps, ci, toff)");
-    v.push_back(AdamSeg{s[0], s[1], (int)s[2], (int)s[3], (int)s[4], s[5]});
+    TORCH_CHECK(s.size() == 9, "segment = (off, numel, slab_ptr, nsplit, co, k, s, ci, toff)");
+    GradSeg g;
+    g.off = s[0]; g.numel = s[1];
+    g.slab = reinterpret_cast<const float*>((uintptr_t)s[2]);
+    g.nsplit = (int)s[3]; g.co = (int)s[4]; g.k = (int)s[5]; g.s = (int)s[6]; g.ci = (int)s[7]; g.toff = s[8];
+    TORCH_CHECK(g.toff < 0 || (g.s > 0 && g.k % g.s == 0), "transposed copy needs k % s == 0");
+    v.push_back(g);
   }
-  auto cpu = torch::empty({(int64_t)(v.size() * sizeof(AdamSeg))}, torch::kUInt8);
-  std::memcpy(cpu.data_ptr(), v.data(), v.size() * sizeof(AdamSeg));
+  auto cpu = torch::empty({(int64_t)(v.size() * sizeof(GradSeg))}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), v.data(), v.size() * sizeof(GradSeg));
+  return cpu.to(torch::Device(torch::kCUDA, device_index));
+}
+
+at::Tensor make_grad_units(const std::vector<std::vector<int64_t>>& units, int64_t device_index) {
+  std::vector<GradUnit> v;
+  for (auto& u : units) {
+    TORCH_CHECK(u.size() == 3 && u[2] >= 1 && u[2] <= 512, "unit = (seg, start, count<=512)");
+    v.push_back(GradUnit{(int)u[0], (int)u[1], (int)u[2]});
+  }
+  auto cpu = torch::empty({(int64_t)std::max<size_t>(1, v.size() * sizeof(GradUnit))}, torch::kUInt8);
+  if (!v.empty()) std::memcpy(cpu.data_ptr(), v.data(), v.size() * sizeof(GradUnit));
   return cpu.to(torch::Device(torch::kCUDA, device_index));
 }
 
@@ -171,6 +207,15 @@ void adam_cast(at::Tensor P, const at::Tensor& G, at::Tensor M, at::Tensor V, at
                    w16.data_ptr(), w16t.data_ptr(), segs.data_ptr(), (int)nseg, P.numel(), state.data_ptr(),
                    hparams.data_ptr(), do_adam ? 1 : 0, cur()),
      "adam_cast");
+}
+
+void grad_finalize(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::Tensor w16, at::Tensor w16t,
+                   const at::Tensor& segs, const at::Tensor& units, int64_t nunits, const at::Tensor& state,
+                   const at::Tensor& hparams, bool do_adam) {
+  rc(mdt_grad_finalize(P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(),
+                       w16.data_ptr(), w16t.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits,
+                       state.data_ptr(), hparams.data_ptr(), do_adam ? 1 : 0, cur()),
+     "grad_finalize");
 }
 
 // ------------------------------------------------------------------ state ----
@@ -242,21 +287,24 @@ class TrialStateBuf {
 
 void bind_conv(pybind11::module& m) {
   namespace py = pybind11;
-  m.def("conv_fwd", &conv_fwd, py::arg("X"), py::arg("rows"), py::arg("W16"), py::arg("desc"), py::arg("bias"),
-        py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none());
-  m.def("conv_dgrad", &conv_dgrad, py::arg("G16"), py::arg("mask"), py::arg("Wt16"), py::arg("desc"),
-        py::arg("bias"), py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none());
+  m.def("igemm_plan", &igemm_plan);
+  m.def("wgrad_plan", &wgrad_plan);
+  m.def("igemm", &igemm, py::arg("mode"), py::arg("A"), py::arg("B16"), py::arg("desc"), py::arg("bias"),
+        py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),
+        py::arg("colsum") = py::none(), py::arg("ws") = py::none());
+  m.def("wgrad", &wgrad);
+  m.def("colsum", &colsum);
   m.def("gather_rows", &gather_rows);
-  m.def("conv_wgrad", &conv_wgrad, py::arg("G16"), py::arg("mask"), py::arg("X"), py::arg("rows"), py::arg("desc"),
-        py::arg("dW"), py::arg("db"));
-  m.def("chan_sum", &chan_sum);
   m.def("reparam", &reparam);
   m.def("reparam_bwd", &reparam_bwd);
-  m.def("bce_logits", &bce_logits);
+  m.def("bce_logits", &bce_logits, py::arg("logits"), py::arg("X"), py::arg("rows"), py::arg("B"), py::arg("P"),
+        py::arg("dlog16"), py::arg("recon"), py::arg("part"), py::arg("gpart") = py::none());
   m.def("loss_finalize2", &loss_finalize2);
   m.def("step_begin", &step_begin);
-  m.def("make_adam_segs", &make_adam_segs);
+  m.def("make_grad_segs", &make_grad_segs);
+  m.def("make_grad_units", &make_grad_units);
   m.def("adam_cast", &adam_cast);
+  m.def("grad_finalize", &grad_finalize);
   py::class_<TrialStateBuf>(m, "TrialState")
       .def(py::init<int64_t>())
       .def("set_hparams", &TrialStateBuf::set_hparams)

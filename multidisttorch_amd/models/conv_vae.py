@@ -10,12 +10,15 @@ gradients + fp32 Adam moments in flat arenas (one ``adam_cast`` launch per step
 updates the masters and re-emits the bf16 weights AND their [Cin][KH][KW][Cout]
 transposes), f32 accumulation everywhere, f32 mu/logvar/logits and loss.
 
-Every layer is one of three implicit-GEMM kernels (csrc/kernels/conv_bf16.hip):
-  conv    fwd = conv_fwd,   d_in = conv_dgrad,  dW = conv_wgrad(G=d_out, X=in)
-  linear  = conv 1x1 on a 1x1 "image"
-  convT   fwd = conv_dgrad, d_in = conv_fwd,    dW = conv_wgrad(G=in, X=d_out), db = chan_sum
-ReLU backward is fused into the epilogue that produces each gradient (output
-mask), so no separate elementwise pass exists in the backward.
+Every layer maps onto the LDS-tiled implicit-GEMM kernels of
+csrc/kernels/conv_igemm.hip (conv view: a convT is the conv whose backward-data
+is its forward):
+  conv    fwd = igemm(conv mode),   d_in = igemm(parity mode, Wt),  dW = wgrad(G=d_out, X=in)
+  linear  = conv 1x1 on a 1x1 "image" (split-K when deep and narrow)
+  convT   fwd = igemm(parity mode, Wt), d_in = igemm(conv mode),    dW = wgrad(G=in, X=d_out)
+ReLU backward and the bias-gradient column sums are fused into the epilogue
+that produces each gradient; weight gradients are m-split partial slabs that
+one finalize launch reduces (deterministically) and feeds to a fused Adam.
 ``TorchConvVAE`` is the same network in stock torch ops (fp32, NCHW): the CPU
 backend and the numerical oracle of the GPU tests.
 """
@@ -338,20 +341,13 @@ class ConvVaeTrainer:
         bf = dict(dtype=torch.bfloat16, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
         self.w16 = torch.zeros(self.numel, **bf)
-        tl, toff = [], 0
-        segs = []
-        lay = {n: (o, s) for n, o, s in self.layout}
+        toff, self._toff = 0, {}
         for l in self.spec:
-            o, s = lay[l.name + ".weight"]
-            tl.append(toff)
-            segs.append([o, math.prod(s), s[0], s[1] * s[2], s[3], toff])
-            toff = (toff + math.prod(s) + 63) // 64 * 64
-            ob, sb = lay[l.name + ".bias"]
-            segs.append([ob, sb[0], 0, 0, 0, -1])
+            self._toff[l.name] = toff
+            toff = (toff + math.prod(_w_shape(l)) + 63) // 64 * 64
         self.w16t = torch.zeros(max(toff, 64), **bf)
-        self._toff = dict(zip([l.name for l in self.spec], tl))
-        self.segs = self.C.make_adam_segs(segs, dev.index or 0)
-        self.nseg = len(segs)
+        self.segs = self.C.make_grad_segs(self._seg_rows({}), dev.index or 0)
+        self.nseg = 2 * len(self.spec)
         self.xb = torch.zeros(B, self.D, **f32)
         self.acts, self.gacts = {}, {}
         for l in self.spec:
@@ -370,7 +366,88 @@ class ConvVaeTrainer:
         self.dlog16 = torch.zeros(B * self.D, **bf)
         self.bce_part = torch.zeros(-(-B * self.D // 256), **f32)
         self.kld_part = torch.zeros(-(-B * zf // 256), **f32)
+        self._plans = {}
         self._cast_weights()
+
+    def _seg_rows(self, slabs):
+        """GradSeg rows (off, numel, slab_ptr, nsplit, co, k, s, ci, toff) for every
+        weight and bias; ``slabs`` maps a parameter name to (tensor, nsplit)."""
+        rows = []
+        lay = {n: (o, s) for n, o, s in self.layout}
+        for l in self.spec:
+            for suffix in (".weight", ".bias"):
+                name = l.name + suffix
+                o, shp = lay[name]
+                t, ns = slabs.get(name, (None, 1))
+                ptr = t.data_ptr() if t is not None else 0
+                if suffix == ".weight":
+                    rows.append([o, math.prod(shp), ptr, ns, shp[0], shp[1], l.s, shp[3], self._toff[l.name]])
+                else:
+                    rows.append([o, shp[0], ptr, ns, 0, 0, 0, 0, -1])
+        return rows
+
+    def _plan(self, M):
+        """Per-batch-size backward plan: partial-slab buffers sized from the
+        native planners, the GradSeg/GradUnit tables of the finalize kernel and
+        the split-K workspace (built once per M, reused by every step/graph)."""
+        p = self._plans.get(M)
+        if p is not None:
+            return p
+        C, dev = self.C, self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        slabs, ws_need = {}, 0
+        spec = self.spec
+        names = [l.name for l in spec]
+        colsum = {}
+        for i, l in enumerate(spec):
+            d = self._desc(l, M)
+            info = C.wgrad_plan(d)
+            ns = info[6]
+            wn = math.prod(_w_shape(l))
+            if ns > 1:
+                slabs[l.name + ".weight"] = (torch.empty(ns * wn, **f32), ns)
+            # backward-data producing the previous layer's gradient
+            if i == 0:
+                continue
+            prev = spec[i - 1]
+            mode = 0 if l.kind == "convT" else 1
+            split_ok = l.name == "dec_fc"
+            q = C.igemm_plan(mode, d, split_ok)
+            if split_ok and q[10] > 1:
+                ws_need = max(ws_need, q[10] * q[4] * q[5])
+            if prev.name in ("dec_fc",) or l.name == "dec_fc":
+                continue  # per-feature / reparam biases: colsum kernel below
+            rows, ncols = q[11], q[5]
+            t = torch.empty(rows * ncols, **f32)
+            colsum[prev.name] = t
+            slabs[prev.name + ".bias"] = (t, rows * (ncols // prev.cout))
+        for l in spec:  # forward split-K (deep, narrow conv-mode layers such as enc_head)
+            if l.kind != "convT":
+                q = C.igemm_plan(0, self._desc(l, M), True)
+                if q[10] > 1:
+                    ws_need = max(ws_need, q[10] * q[4] * q[5])
+        last = spec[-1]
+        nb = -(-M * self.D // 256)
+        gpart = torch.empty(nb, **f32)
+        if self.channels == 1:
+            slabs[last.name + ".bias"] = (gpart, nb)
+        else:
+            raise NotImplementedError("conv-VAE HIP path: multi-channel images need the per-channel dlogits sum")
+        segs = self._seg_rows(slabs)
+        units = []
+        for si, (off, numel, ptr, ns, *_rest) in enumerate(segs):
+            rp = 1
+            if ptr:
+                while rp < 512 and rp * 16 < ns:
+                    rp *= 2
+            cnt = 512 // rp
+            for st in range(0, numel, cnt):
+                units.append([si, st, min(cnt, numel - st)])
+        p = dict(slabs=slabs, colsum=colsum, gpart=gpart, ws=torch.empty(max(ws_need, 1), **f32),
+                 segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
+                 nunits=len(units))
+        self._plans[M] = p
+        return p
 
     def _cast_weights(self):
         h = self.state
@@ -401,71 +478,73 @@ class ConvVaeTrainer:
             return [M, l.out_hw, l.out_hw, l.cout, l.in_hw, l.in_hw, l.cin, l.k, l.k, l.s, l.p]
         return [M, l.in_hw, l.in_hw, l.cin, l.out_hw, l.out_hw, l.cout, l.k, l.k, l.s, l.p]
 
+    def _layer_fwd(self, l, h, M, o16, o32, ws):
+        """conv / linear: conv-mode GEMM; convT: parity-class GEMM on the
+        transposed weights (no zero-insertion taps)."""
+        d = self._desc(l, M)
+        if l.kind == "convT":
+            self.C.igemm(1, h, self._wt(l), d, self._b(l), l.relu, o16, o32)
+        else:
+            self.C.igemm(0, h, self._w(l), d, self._b(l), l.relu, o16, o32, ws=ws)
+
     def _forward_hip(self, M, state, stream, want_recon=False, train=True):
         C = self.C
-        spec = self.spec
-        enc = [l for l in spec if l.name.startswith("enc")]
-        dec = [l for l in spec if l.name.startswith("dec")]
+        p = self._plan(M)
+        enc = [l for l in self.spec if l.name.startswith("enc")]
+        dec = [l for l in self.spec if l.name.startswith("dec")]
         h = self.xb
         for l in enc:
-            d = self._desc(l, M)
             last = l is enc[-1]
-            out16 = None if last else self.acts[l.name]
-            out32 = self.mulv if last else None
-            C.conv_fwd(h, None, self._w(l), d, self._b(l), l.relu, out16, out32)
+            self._layer_fwd(l, h, M, None if last else self.acts[l.name], self.mulv if last else None, p["ws"])
             h = self.acts[l.name]
         C.reparam(self.mulv, self.eps, self.z16, None, M, self.Z, state, self.state.hparams, stream, self.kld_part)
         h = self.z16
         for l in dec:
-            d = self._desc(l, M)
             last = l is dec[-1]
-            out16 = None if last else self.acts[l.name]
-            out32 = self.logits if last else None
-            if l.kind == "convT":
-                C.conv_dgrad(h, None, self._wt(l), d, self._b(l), l.relu, out16, out32)
-            else:
-                C.conv_fwd(h, None, self._w(l), d, self._b(l), l.relu, out16, out32)
+            self._layer_fwd(l, h, M, None if last else self.acts[l.name], self.logits if last else None, p["ws"])
             h = self.acts[l.name]
         C.bce_logits(self.logits, self.xb, None, M, self.D, self.dlog16 if train else None,
-                     self.recon if want_recon else None, self.bce_part)
+                     self.recon if want_recon else None, self.bce_part, p["gpart"] if train else None)
 
     def _backward_hip(self, M):
+        """Reverse sweep: per layer one weight-gradient GEMM (partial slabs) and
+        one backward-data GEMM whose epilogue applies the previous layer's ReLU
+        mask and emits its bias-gradient column sums."""
         C = self.C
+        p = self._plan(M)
         spec = self.spec
-        self.grads.zero_()
-        idx_of = {l.name: i for i, l in enumerate(spec)}
         g = self.dlog16
-        for l in reversed(spec):
-            i = idx_of[l.name]
+        for i in range(len(spec) - 1, -1, -1):
+            l = spec[i]
             prev = spec[i - 1] if i > 0 else None
             d = self._desc(l, M)
-            if l.name == "dec_fc":
-                a_in = self.z16
-            elif prev is None:
+            if i == 0:
                 a_in = self.xb
-            elif l.name == "enc_head":
-                a_in = self.acts[prev.name]
-            else:
-                a_in = self.acts[prev.name]
-            if prev is not None and prev.name == "enc_head":
+            elif l.name == "dec_fc":
                 a_in = self.z16
-            omask = a_in if (prev is not None and prev.relu and l.name != "dec_fc") else None
-            if l.kind == "convT":
-                C.conv_wgrad(a_in, None, g, None, d, self._gw(l), None)
-                C.chan_sum(g, M * l.out_hw * l.out_hw, l.cout, self._gb(l))
-                gin = self.gacts[prev.name]
-                C.conv_fwd(g, None, self._w(l), d, None, False, gin, None, omask)
             else:
-                C.conv_wgrad(g, None, a_in, None, d, self._gw(l), self._gb(l))
-                if prev is None:
-                    break
-                if l.name == "dec_fc":
-                    C.conv_dgrad(g, None, self._wt(l), d, None, False, None, self.dz)
-                    C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M, self.Z, self.state.hparams)
-                    gin = self.dmulv16
-                else:
-                    gin = self.gacts[prev.name]
-                    C.conv_dgrad(g, None, self._wt(l), d, None, False, gin, None, omask)
+                a_in = self.acts[prev.name]
+            wslab = p["slabs"].get(l.name + ".weight")
+            wout = wslab[0] if wslab is not None else self._gw(l)
+            if l.kind == "convT":  # conv view: output = convT input, input = convT output
+                C.wgrad(a_in, g, d, wout)
+            else:
+                C.wgrad(g, a_in, d, wout)
+            if prev is None:
+                break
+            omask = a_in if prev.relu else None
+            if l.name == "dec_fc":
+                C.igemm(1, g, self._wt(l), d, None, False, None, self.dz, ws=p["ws"])
+                C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M, self.Z, self.state.hparams)
+                C.colsum(self.dmulv16, M, 2 * self.Z, M, self._gb(prev))
+                gin = self.dmulv16
+            else:
+                gin = self.gacts[prev.name]
+                cs = p["colsum"].get(prev.name)
+                C.igemm(0 if l.kind == "convT" else 1, g, self._w(l) if l.kind == "convT" else self._wt(l), d,
+                        None, False, gin, None, omask, cs)
+                if prev.name == "dec_fc":
+                    C.colsum(gin, M, prev.cout, M, self._gb(prev))
             g = gin
 
     def _step_hip(self, M):
@@ -479,10 +558,20 @@ class ConvVaeTrainer:
                          st.train_state, st.hparams, True)
         self._backward_hip(M)
         if self.reducer is not None:
+            self._finalize_grads(M, False)
             self.reducer.launch_all()
             self.reducer.wait_all()
-        C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.w16t, self.segs,
-                    self.nseg, st.train_state, st.hparams, True)
+            C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.w16t, self.segs,
+                        self.nseg, st.train_state, st.hparams, True)
+        else:
+            self._finalize_grads(M, True)
+
+    def _finalize_grads(self, M, do_adam):
+        """Reduce the partial slabs into the gradient arena (deterministic order);
+        with ``do_adam`` also apply Adam and re-emit the bf16 weight copies."""
+        p, st = self._plan(M), self.state
+        self.C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.w16t, p["segs"],
+                             p["units"], p["nunits"], st.train_state, st.hparams, do_adam)
 
     # ----------------------------------------------------------- torch path
     def _step_torch(self, M):
@@ -610,14 +699,9 @@ class ConvVaeTrainer:
             self.z16[:M].copy_(zc.to(torch.bfloat16))
             h = self.z16
             for l in dec:
-                d = self._desc(l, M)
                 last = l is dec[-1]
-                o16 = None if last else self.acts[l.name]
-                o32 = self.logits if last else None
-                if l.kind == "convT":
-                    self.C.conv_dgrad(h, None, self._wt(l), d, self._b(l), l.relu, o16, o32)
-                else:
-                    self.C.conv_fwd(h, None, self._w(l), d, self._b(l), l.relu, o16, o32)
+                self._layer_fwd(l, h, M, None if last else self.acts[l.name], self.logits if last else None,
+                                self._plan(M)["ws"])
                 h = self.acts[l.name]
             outs.append(torch.sigmoid(self.logits[: M * self.D].view(M, self.D)).clone())
         return torch.cat(outs)
