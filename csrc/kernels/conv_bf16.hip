@@ -2,7 +2,7 @@
 // batch gather, reparameterisation (+KLD) and its backward, logit-form BCE
 // (+dlogits, +bias-gradient partials), loss ring update, and the optimizer
 // tail: gradient finalisation (deterministic partial-slab reduction) with a
-// fused Adam + bf16 cast + parity-ordered weight transpose.
+// fused Adam + bf16 cast, and the LDS-tiled parity-ordered weight transpose.
 #include "common.h"
 #include "vae_mlp.h"
 #include "adam_common.h"
@@ -131,26 +131,11 @@ __global__ void step_begin_k(TrainState* st, const HParams* hp) {
 }
 
 // ------------------------------------------------ optimizer tail ----
-// Element i of a [CO][k][k][ci] weight -> its slot in the parity-ordered
-// transposed copy [s][s][ci][k/s][k/s][CO] read by the kModeTconv GEMM
-// (class (a, b) holds taps ky = a + s*ty, kx = b + s*tx).
-__device__ __forceinline__ long long wt_index(const GradSeg& sg, long long i) {
-  const int k = sg.k, s = sg.s, ci_n = sg.ci;
-  const int per = k * k * ci_n;
-  const int co = (int)(i / per);
-  const int rem = (int)(i - (long long)co * per);
-  const int tap = rem / ci_n, ci = rem - tap * ci_n;
-  const int ky = tap / k, kx = tap - ky * k;
-  const int T = k / s;
-  const int a = ky % s, ty = ky / s, b = kx % s, tx = kx / s;
-  return sg.toff + (((((long long)(a * s + b) * ci_n + ci) * T + ty) * T + tx) * sg.co + co);
-}
-
-// Adam (optional) + bf16 cast (+ transposed copy) over every segment; used for
-// the initial cast, after checkpoint loads and after a DDP all-reduce.
+// Adam (optional) + bf16 cast over every segment; used for the initial cast,
+// after checkpoint loads and after a DDP all-reduce.
 __global__ void __launch_bounds__(256) adam_cast_k(float* P, const float* G, float* Mo, float* Vo, __bf16* w16,
-                                                   __bf16* w16t, const GradSeg* segs, int nseg,
-                                                   const TrainState* st, const HParams* hp, int do_adam) {
+                                                   const GradSeg* segs, int nseg, const TrainState* st,
+                                                   const HParams* hp, int do_adam) {
   __shared__ AdamC cs;
   const AdamC c = adam_consts_block(st, hp, &cs);
   for (int s = 0; s < nseg; ++s) {
@@ -164,9 +149,7 @@ __global__ void __launch_bounds__(256) adam_cast_k(float* P, const float* G, flo
         adam_update(p, m, v, G[o], c);
         P[o] = p; Mo[o] = m; Vo[o] = v;
       }
-      const __bf16 pb = (__bf16)p;
-      w16[o] = pb;
-      if (sg.toff >= 0) w16t[wt_index(sg, i)] = pb;
+      w16[o] = (__bf16)p;
     }
   }
 }
@@ -175,9 +158,9 @@ __global__ void __launch_bounds__(256) adam_cast_k(float* P, const float* G, flo
 // + col sum partial rows rl, rl+rp, ... (rp = 512/count) of column col, then
 // row lane 0 adds the rp sums in order: a fixed reduction tree, so results are
 // bitwise reproducible (unlike f32 atomics). With do_adam the same thread
-// applies Adam to the parameter and re-emits its bf16 copies.
+// applies Adam to the parameter and re-emits its bf16 copy.
 __global__ void __launch_bounds__(512) grad_finalize_k(float* P, float* G, float* Mo, float* Vo, __bf16* w16,
-                                                       __bf16* w16t, const GradSeg* segs, const GradUnit* units,
+                                                       const GradSeg* segs, const GradUnit* units,
                                                        const TrainState* st, const HParams* hp, int do_adam) {
   __shared__ float red[512];
   __shared__ AdamC cs;
@@ -205,13 +188,12 @@ __global__ void __launch_bounds__(512) grad_finalize_k(float* P, float* G, float
   red[t] = acc;
   __syncthreads();
   if (rl == 0) {
-    const long long i = (long long)u.start + col;
-    const long long o = sg.off + i;
+    const long long o = sg.off + u.start + col;
     float g;
     if (sg.slab) {
       g = 0.f;
       for (int r = 0; r < rp; ++r) g += red[r * cnt + col];
-      G[o] = g;
+      if (!do_adam) G[o] = g;  // the fused-Adam path consumes g in registers only
     } else {
       g = G[o];
     }
@@ -219,10 +201,35 @@ __global__ void __launch_bounds__(512) grad_finalize_k(float* P, float* G, float
       float p = P[o], m = Mo[o], v = Vo[o];
       adam_update(p, m, v, g, c);
       P[o] = p; Mo[o] = m; Vo[o] = v;
-      const __bf16 pb = (__bf16)p;
-      w16[o] = pb;
-      if (sg.toff >= 0) w16t[wt_index(sg, i)] = pb;
+      w16[o] = (__bf16)p;
     }
+  }
+}
+
+// bf16 weights [CO][k][k][CI] -> parity-ordered transpose [s][s][CI][k/s][k/s][CO]
+// (class (a, b) holds taps ky = a + s*ty, kx = b + s*tx) for the kModeTconv
+// GEMM. One 64x64 (co, ci) tile of one tap per block, staged through LDS so
+// both the read (ci-contiguous) and the write (co-contiguous) are coalesced.
+__global__ void __launch_bounds__(256) wtrans_k(const __bf16* w16, __bf16* w16t, const GradSeg* segs,
+                                                const TrUnit* units) {
+  __shared__ unsigned short tile[64][66];
+  const TrUnit u = units[blockIdx.x];
+  const GradSeg sg = segs[u.seg];
+  const int k = sg.k, s = sg.s, CI = sg.ci, CO = sg.co, T = k / s;
+  const int ky = u.tap / k, kx = u.tap - ky * k;
+  const int a = ky % s, ty = ky / s, b = kx % s, tx = kx / s;
+  const unsigned short* src = reinterpret_cast<const unsigned short*>(w16) + sg.off;
+  unsigned short* dst = reinterpret_cast<unsigned short*>(w16t) + sg.toff;
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int r = idx >> 6, c = idx & 63;
+    const int co = u.co0 + r, ci = u.ci0 + c;
+    if (co < CO && ci < CI) tile[r][c] = src[((long long)(co * k + ky) * k + kx) * CI + ci];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int r = idx >> 6, c = idx & 63;
+    const int ci = u.ci0 + r, co = u.co0 + c;
+    if (co < CO && ci < CI) dst[((((long long)(a * s + b) * CI + ci) * T + ty) * T + tx) * CO + co] = tile[c][r];
   }
 }
 
@@ -279,24 +286,31 @@ int mdt_step_begin(void* st, const void* hp, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int mdt_adam_cast(float* P, const float* G, float* Mo, float* Vo, void* w16, void* w16t, const void* segs, int nseg,
+int mdt_adam_cast(float* P, const float* G, float* Mo, float* Vo, void* w16, const void* segs, int nseg,
                   long long total, const void* st, const void* hp, int do_adam, hipStream_t s) {
   int blocks = cdivh(total, 256 * 4);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_cast_k, dim3(blocks), dim3(256), 0, s, P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16),
-                     reinterpret_cast<__bf16*>(w16t), reinterpret_cast<const GradSeg*>(segs), nseg,
+                     reinterpret_cast<const GradSeg*>(segs), nseg, reinterpret_cast<const TrainState*>(st),
+                     reinterpret_cast<const HParams*>(hp), do_adam);
+  return (int)hipGetLastError();
+}
+
+int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs, const void* units,
+                      int nunits, const void* st, const void* hp, int do_adam, hipStream_t s) {
+  if (nunits <= 0) return 0;
+  hipLaunchKernelGGL(grad_finalize_k, dim3(nunits), dim3(512), 0, s, P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16),
+                     reinterpret_cast<const GradSeg*>(segs), reinterpret_cast<const GradUnit*>(units),
                      reinterpret_cast<const TrainState*>(st), reinterpret_cast<const HParams*>(hp), do_adam);
   return (int)hipGetLastError();
 }
 
-int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, void* w16t, const void* segs,
-                      const void* units, int nunits, const void* st, const void* hp, int do_adam, hipStream_t s) {
+int mdt_wtrans(const void* w16, void* w16t, const void* segs, const void* units, int nunits, hipStream_t s) {
   if (nunits <= 0) return 0;
-  hipLaunchKernelGGL(grad_finalize_k, dim3(nunits), dim3(512), 0, s, P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16),
+  hipLaunchKernelGGL(wtrans_k, dim3(nunits), dim3(256), 0, s, reinterpret_cast<const __bf16*>(w16),
                      reinterpret_cast<__bf16*>(w16t), reinterpret_cast<const GradSeg*>(segs),
-                     reinterpret_cast<const GradUnit*>(units), reinterpret_cast<const TrainState*>(st),
-                     reinterpret_cast<const HParams*>(hp), do_adam);
+                     reinterpret_cast<const TrUnit*>(units));
   return (int)hipGetLastError();
 }
 

@@ -78,4 +78,10 @@ struct GradUnit {
   int seg, start, count;
 };
 
+// One 64(co) x 64(ci) tile of one tap of a weight segment for the transpose
+// into the parity-ordered copy.
+struct TrUnit {
+  int seg, tap, co0, ci0;
+};
+
 }  // namespace mdt

@@ -13,13 +13,16 @@
 //                  (coalesced 16-B rows) and read with ds_read_b64_tr_b16, the
 //                  CDNA4 transposing LDS read. Split over m into f32 partial
 //                  slabs reduced deterministically by grad_finalize_k.
-//  * grad_finalize_k — partial-slab reduction (+ fused Adam, bf16 cast and
-//                  parity-ordered weight transpose when no DDP reducer runs).
+//  * grad_finalize_k / wtrans_k (conv_bf16.hip) — partial-slab reduction
+//                  (+ fused Adam and bf16 cast), then an LDS-tiled transpose
+//                  into the parity-ordered weights the kModeTconv GEMM reads.
 // Tiles are 64-deep in k, double-buffered in LDS (register staging: loads for
 // tile k+1 are in flight while the MFMAs of tile k run), XOR-swizzled images,
 // blockIdx remapped so neighbouring tiles share an XCD's L2.
 // Epilogues fuse bias, ReLU, the ReLU-backward mask of the produced gradient
 // and the per-block column sums that become the next layer's bias gradient.
+#include <stdlib.h>
+
 #include "common.h"
 #include "conv_igemm.h"
 
@@ -121,6 +124,134 @@ struct IgArgs {
   int M, Ncols, K, mtiles, ntiles, ktiles, kt_per_split;
   FastDiv f_pix, f_w, f_ch, f_tw;
 };
+
+// Shared epilogue of the forward-type kernels: combine k-halves (KWS == 2),
+// then either raw split-K partials or bias + ReLU + output mask + bf16/f32
+// stores + per-block column sums. `lds` must be free (caller passed a barrier).
+template <int MODE, class TC>
+__device__ __forceinline__ void igemm_epilogue(const IgArgs& a, f32x4 (&acc)[TC::FM][TC::FN], uint8_t* lds, int mt,
+                                               int nt, int kz, int cls, int oa, int ob) {
+  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
+  const ConvDesc& d = a.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
+  if constexpr (KWS == 2) {  // combine the two k-halves
+    float* red = reinterpret_cast<float*>(lds);
+    const int slot = w % (WM * WN);
+    if (wk == 1) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          *reinterpret_cast<f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4) = acc[fm][fn];
+    }
+    __syncthreads();
+    if (wk == 0) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] += *reinterpret_cast<const f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4);
+    }
+  }
+
+  const bool epi = (KWS == 1) || wk == 0;
+  const int rbase = mt * BM + wm * (BM / WM) + 4 * (lane >> 4);
+  const int cbase = nt * BN + wn * (BN / WN) + (lane & 15);
+  if (a.slab) {
+    if (epi) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = rbase + fm * 16 + r;
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) {
+            const int col = cbase + fn * 16;
+            if (m < a.M && col < a.Ncols) a.slab[((size_t)kz * a.M + m) * a.Ncols + col] = acc[fm][fn][r];
+          }
+        }
+    }
+    return;
+  }
+  float cs[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) cs[fn] = 0.f;
+  if (epi) {
+    float bv[FN];
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int col = cbase + fn * 16;
+      bv[fn] = (a.bias && col < a.Ncols) ? a.bias[col] : 0.f;
+    }
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      int grow[4];
+      bool rok[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = rbase + fm * 16 + r;
+        rok[r] = m < a.M;
+        if constexpr (MODE == kModeConv) {
+          grow[r] = m;
+        } else {
+          const uint32_t mm = rok[r] ? (uint32_t)m : 0u;
+          const uint32_t n = fdiv(mm, a.f_pix);
+          const uint32_t rem = mm - n * a.f_pix.d;
+          const uint32_t yy = fdiv(rem, a.f_w);
+          const uint32_t xx = rem - yy * a.f_w.d;
+          grow[r] = ((int)n * d.H + (int)yy * d.S + oa) * d.W + (int)xx * d.S + ob;
+        }
+      }
+      float mk[4][FN];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int col = cbase + fn * 16;
+          const bool ok = rok[r] && col < a.Ncols;
+          mk[r][fn] = (a.omask && ok) ? (float)a.omask[(size_t)grow[r] * a.Ncols + col] : 1.f;
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int col = cbase + fn * 16;
+          const bool ok = rok[r] && col < a.Ncols;
+          float v = acc[fm][fn][r] + bv[fn];
+          if (a.relu) v = fmaxf(v, 0.f);
+          v = mk[r][fn] > 0.f ? v : 0.f;
+          if (ok) {
+            const size_t o = (size_t)grow[r] * a.Ncols + col;
+            if (a.y16) a.y16[o] = (__bf16)v;
+            if (a.y32) a.y32[o] = v;
+          }
+          cs[fn] += ok ? v : 0.f;
+        }
+    }
+  }
+  if (a.colsum) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      cs[fn] += __shfl_xor(cs[fn], 16, 64);
+      cs[fn] += __shfl_xor(cs[fn], 32, 64);
+    }
+    float* sc = reinterpret_cast<float*>(lds + TC::RED_BYTES);
+    if (epi && lane < 16) {
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) sc[wm * BN + wn * (BN / WN) + fn * 16 + lane] = cs[fn];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < WM; ++q) t += sc[q * BN + tid];
+      const int col = nt * BN + tid;
+      if (col < a.Ncols) a.colsum[(size_t)(cls * a.mtiles + mt) * a.Ncols + col] = t;
+    }
+  }
+}
 
 template <int MODE, typename AT, bool VEC, class TC>
 __global__ void __launch_bounds__(256) igemm_fwd_k(IgArgs a) {
@@ -291,7 +422,198 @@ __global__ void __launch_bounds__(256) igemm_fwd_k(IgArgs a) {
     __syncthreads();
   }
 
-  if constexpr (KWS == 2) {  // combine the two k-halves
+  igemm_epilogue<MODE, TC>(a, acc, lds, mt, nt, kz, cls, oa, ob);
+}
+
+// ---------------------------------------------------------- LDS-DMA helpers ----
+// Zero source for out-of-range chunks of an LDS-DMA tile load (static device
+// memory is zero-initialised): a global_load_lds has no per-lane predicate, so
+// masked lanes fetch 16 zero bytes instead.
+__device__ __attribute__((aligned(64))) uint8_t g_zero16[64];
+
+__device__ __forceinline__ void glds16(const void* src, uint8_t* lds_base) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// Counted wait on this wave's outstanding LDS-DMA loads: `n` newer tiles of
+// `NI` instructions each may stay in flight.
+template <int NI, int S>
+__device__ __forceinline__ void wait_tiles(int n) {
+  static_assert(NI * (S - 2) <= 63, "vmcnt range");
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory"); break;
+    case 2: if constexpr (S >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory"); break;
+    case 3: if constexpr (S >= 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NI) : "memory"); break;
+    default: if constexpr (S >= 6) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NI) : "memory"); break;
+  }
+}
+
+// Workgroup barrier that neither drains the LDS-DMA queue (unlike
+// __syncthreads, whose fence waits vmcnt(0)) nor lets this wave's LDS reads
+// of the previous stage still be in flight.
+__device__ __forceinline__ void stage_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Forward-type GEMM with an S-stage LDS ring filled by global_load_lds
+// (bf16 vector gathers only): S-1 k-tiles are in flight while one is
+// multiplied, with no staging registers. The per-lane global address does
+// the im2col gather AND the XOR swizzle (the LDS side of a DMA is lane-linear).
+template <int MODE, class TC, int S>
+__global__ void __launch_bounds__(256) igemm_glds_k(IgArgs a) {
+  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
+  constexpr int BR = BN < 32 ? 32 : BN;         // staged B rows (>= one DMA row group per wave)
+  constexpr int A_CH = BM / 32, B_CH = BR / 32;  // DMA instructions per wave per tile
+  constexpr int NI = A_CH + B_CH;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BR) * 128;
+  static_assert(TC::RED_BYTES + WM * BN * 4 <= S * STAGE, "epilogue scratch exceeds LDS");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[S * STAGE];
+
+  const ConvDesc& d = a.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / a.ntiles, nt = tile - mt * a.ntiles;
+  const int kz = blockIdx.y, cls = blockIdx.z;
+  const int kt0 = kz * a.kt_per_split;
+  const int nk = min(a.ktiles, kt0 + a.kt_per_split) - kt0;
+
+  int ea = 0, eb = 0, oa = 0, ob = 0;
+  if constexpr (MODE == kModeTconv) {
+    const int ca = cls / d.S, cb = cls - ca * d.S;
+    oa = ((ca - d.P) % d.S + d.S) % d.S;
+    ob = ((cb - d.P) % d.S + d.S) % d.S;
+    ea = (oa + d.P - ca) / d.S;
+    eb = (ob + d.P - cb) / d.S;
+  }
+  // lane-linear DMA: lane l of wave w fills row 32i + 8w + (l>>3), slot l&7,
+  // which must hold logical chunk slot ^ (row & 7)
+  const int ach = (tid & 7) ^ ((tid >> 3) & 7);
+  int abase[A_CH], ay[A_CH], ax[A_CH];
+  bool aok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int m = mt * BM + (tid >> 3) + 32 * i;
+    aok[i] = m < a.M;
+    const uint32_t mm = aok[i] ? (uint32_t)m : 0u;
+    const uint32_t n = fdiv(mm, a.f_pix);
+    const uint32_t rem = mm - n * a.f_pix.d;
+    const uint32_t yy = fdiv(rem, a.f_w);
+    const uint32_t xx = rem - yy * a.f_w.d;
+    if constexpr (MODE == kModeConv) {
+      abase[i] = (int)n * d.H * d.W * d.C;
+      ay[i] = (int)yy * d.S - d.P;
+      ax[i] = (int)xx * d.S - d.P;
+    } else {
+      abase[i] = (int)n * d.OH * d.OW * d.CO;
+      ay[i] = (int)yy + ea;
+      ax[i] = (int)xx + eb;
+    }
+  }
+  const __bf16* Ap = reinterpret_cast<const __bf16*>(a.A);
+  const __bf16* Bc = a.B + (size_t)cls * a.Ncols * a.K;
+
+  auto issue = [&](int kt, int buf) {
+    uint8_t* As = lds + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES;
+    const int kk = kt * 64 + 8 * ach;
+    const uint32_t tap = fdiv((uint32_t)kk, a.f_ch);
+    const int ch = kk - (int)(tap * a.f_ch.d);
+    const uint32_t t0 = fdiv(tap, a.f_tw);
+    const int t1 = (int)(tap - t0 * a.f_tw.d);
+    const bool kok = kk < a.K;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      int off;
+      bool ok;
+      if constexpr (MODE == kModeConv) {
+        const int iy = ay[i] + (int)t0, ix = ax[i] + t1;
+        ok = aok[i] && kok && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        off = abase[i] + (iy * d.W + ix) * d.C + ch;
+      } else {
+        const int oy = ay[i] - (int)t0, ox = ax[i] - t1;
+        ok = aok[i] && kok && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
+        off = abase[i] + (oy * d.OW + ox) * d.CO + ch;
+      }
+      glds16(ok ? (const void*)(Ap + off) : (const void*)g_zero16, As + (32 * i + 8 * w) * 128);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      const int col = nt * BN + r;
+      const bool ok = r < BN && col < a.Ncols && kk < a.K;
+      glds16(ok ? (const void*)(Bc + (size_t)col * a.K + kk) : (const void*)g_zero16, Bs + (32 * i + 8 * w) * 128);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const uint8_t* As = lds + buf * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2 / KWS; ++s) {
+      const int ks = KWS == 2 ? wk : s;
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+        af[fm] = *reinterpret_cast<const bf16x8*>(As + rimg(wm * (BM / WM) + fm * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
+        bfr[fn] = *reinterpret_cast<const bf16x8*>(Bs + rimg(wn * (BN / WN) + fn * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(kt0 + s, s);
+  for (int it = 0; it < nk; ++it) {
+    const int newer = min(nk - 1 - it, S - 2);
+    wait_tiles<NI, S>(newer);
+    stage_barrier();
+    if (it + S - 1 < nk) issue(kt0 + it + S - 1, (it + S - 1) % S);
+    compute(it % S);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stage_barrier();
+  igemm_epilogue<MODE, TC>(a, acc, lds, mt, nt, kz, cls, oa, ob);
+}
+
+// ================================================================= wgrad ====
+struct WgArgs {
+  ConvDesc d;
+  const __bf16* G;  // [M][CO]
+  const void* X;    // NHWC conv input
+  float* out;       // [nsplit][CO][K2]
+  int M, K2, cotiles, ktiles, mtiles, mt_per_split;
+  FastDiv f_pix, f_w, f_c, f_kw;
+};
+
+// Epilogue of the weight-gradient kernels: combine k-halves, store the f32
+// partial tile of this m-split.
+template <class TC>
+__device__ __forceinline__ void wgrad_epilogue(const WgArgs& a, f32x4 (&acc)[TC::FM][TC::FN], uint8_t* lds, int ct,
+                                               int nt, int split) {
+  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
+  const ConvDesc& d = a.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
+  if constexpr (KWS == 2) {
     float* red = reinterpret_cast<float*>(lds);
     const int slot = w % (WM * WN);
     if (wk == 1) {
@@ -310,113 +632,21 @@ __global__ void __launch_bounds__(256) igemm_fwd_k(IgArgs a) {
           acc[fm][fn] += *reinterpret_cast<const f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4);
     }
   }
-
-  const bool epi = (KWS == 1) || wk == 0;
-  const int rbase = mt * BM + wm * (BM / WM) + 4 * (lane >> 4);
-  const int cbase = nt * BN + wn * (BN / WN) + (lane & 15);
-  if (a.slab) {
-    if (epi) {
+  if (KWS == 1 || wk == 0) {
+    float* out = a.out + (size_t)split * d.CO * a.K2;
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = rbase + fm * 16 + r;
-#pragma unroll
-          for (int fn = 0; fn < FN; ++fn) {
-            const int col = cbase + fn * 16;
-            if (m < a.M && col < a.Ncols) a.slab[((size_t)kz * a.M + m) * a.Ncols + col] = acc[fm][fn][r];
-          }
-        }
-    }
-    return;
-  }
-  float cs[FN];
-#pragma unroll
-  for (int fn = 0; fn < FN; ++fn) cs[fn] = 0.f;
-  if (epi) {
-    float bv[FN];
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      const int col = cbase + fn * 16;
-      bv[fn] = (a.bias && col < a.Ncols) ? a.bias[col] : 0.f;
-    }
-#pragma unroll
-    for (int fm = 0; fm < FM; ++fm) {
-      int grow[4];
-      bool rok[4];
+    for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = rbase + fm * 16 + r;
-        rok[r] = m < a.M;
-        if constexpr (MODE == kModeConv) {
-          grow[r] = m;
-        } else {
-          const uint32_t mm = rok[r] ? (uint32_t)m : 0u;
-          const uint32_t n = fdiv(mm, a.f_pix);
-          const uint32_t rem = mm - n * a.f_pix.d;
-          const uint32_t yy = fdiv(rem, a.f_w);
-          const uint32_t xx = rem - yy * a.f_w.d;
-          grow[r] = ((int)n * d.H + (int)yy * d.S + oa) * d.W + (int)xx * d.S + ob;
+        const int orow = ct * BM + wm * (BM / WM) + fm * 16 + 4 * (lane >> 4) + r;
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int kp = nt * BN + wn * (BN / WN) + fn * 16 + (lane & 15);
+          if (orow < d.CO && kp < a.K2) out[(size_t)orow * a.K2 + kp] = acc[fm][fn][r];
         }
       }
-      float mk[4][FN];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int col = cbase + fn * 16;
-          const bool ok = rok[r] && col < a.Ncols;
-          mk[r][fn] = (a.omask && ok) ? (float)a.omask[(size_t)grow[r] * a.Ncols + col] : 1.f;
-        }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int col = cbase + fn * 16;
-          const bool ok = rok[r] && col < a.Ncols;
-          float v = acc[fm][fn][r] + bv[fn];
-          if (a.relu) v = fmaxf(v, 0.f);
-          v = mk[r][fn] > 0.f ? v : 0.f;
-          if (ok) {
-            const size_t o = (size_t)grow[r] * a.Ncols + col;
-            if (a.y16) a.y16[o] = (__bf16)v;
-            if (a.y32) a.y32[o] = v;
-          }
-          cs[fn] += ok ? v : 0.f;
-        }
-    }
-  }
-  if (a.colsum) {
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      cs[fn] += __shfl_xor(cs[fn], 16, 64);
-      cs[fn] += __shfl_xor(cs[fn], 32, 64);
-    }
-    float* sc = reinterpret_cast<float*>(lds + TC::RED_BYTES);
-    if (epi && lane < 16) {
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) sc[wm * BN + wn * (BN / WN) + fn * 16 + lane] = cs[fn];
-    }
-    __syncthreads();
-    if (tid < BN) {
-      float t = 0.f;
-#pragma unroll
-      for (int q = 0; q < WM; ++q) t += sc[q * BN + tid];
-      const int col = nt * BN + tid;
-      if (col < a.Ncols) a.colsum[(size_t)(cls * a.mtiles + mt) * a.Ncols + col] = t;
-    }
   }
 }
-
-// ================================================================= wgrad ====
-struct WgArgs {
-  ConvDesc d;
-  const __bf16* G;  // [M][CO]
-  const void* X;    // NHWC conv input
-  float* out;       // [nsplit][CO][K2]
-  int M, K2, ktiles, mtiles, mt_per_split;
-  FastDiv f_pix, f_w, f_c, f_kw;
-};
 
 template <typename XT, bool VEC, class TC>
 __global__ void __launch_bounds__(256) wgrad_k(WgArgs a) {
@@ -431,9 +661,14 @@ __global__ void __launch_bounds__(256) wgrad_k(WgArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // 1-D grid, split-major after the XCD remap: an XCD owns a contiguous
+  // m-range for ALL (co, k') tiles, so its slice of G and X is fetched into
+  // its L2 once instead of once per tile.
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = a.cotiles * a.ktiles;
+  const int split = wid / ntile;
+  const int tile = wid - split * ntile;
   const int ct = tile / a.ktiles, nt = tile - ct * a.ktiles;
-  const int split = blockIdx.y;
   const int mt0 = split * a.mt_per_split;
   const int mt1 = min(a.mtiles, mt0 + a.mt_per_split);
 
@@ -550,54 +785,144 @@ __global__ void __launch_bounds__(256) wgrad_k(WgArgs a) {
     __syncthreads();
   }
 
-  if constexpr (KWS == 2) {
-    float* red = reinterpret_cast<float*>(lds);
-    const int slot = w % (WM * WN);
-    if (wk == 1) {
+  wgrad_epilogue<TC>(a, acc, lds, ct, nt, split);
+}
+
+// Weight-gradient GEMM with an S-stage LDS-DMA ring (bf16 inputs, C % 8 == 0).
+// Both m-major images are filled lane-linearly; the tr_b16 XOR swizzle is
+// applied on the source side (lane slot p holds logical chunk p ^ trsw(row)).
+template <class TC, int S>
+__global__ void __launch_bounds__(256) wgrad_glds_k(WgArgs a) {
+  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
+  constexpr int CPR_A = BM / 8, A_RPP = 256 / CPR_A, A_CH = 64 / A_RPP;
+  constexpr int CPR_B = BN / 8, B_RPP = 256 / CPR_B, B_CH = (64 + B_RPP - 1) / B_RPP;
+  constexpr int NI = A_CH + B_CH;
+  constexpr int A_BYTES = 64 * BM * 2;
+  constexpr int B_BYTES = (B_RPP * B_CH) * BN * 2;  // rows past 64 only absorb zero DMAs
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  static_assert(TC::RED_BYTES <= S * STAGE, "reduction scratch exceeds LDS");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[S * STAGE];
+
+  const ConvDesc& d = a.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
+  // 1-D grid, split-major after the XCD remap: an XCD owns a contiguous
+  // m-range for ALL (co, k') tiles, so its slice of G and X is fetched into
+  // its L2 once instead of once per tile.
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = a.cotiles * a.ktiles;
+  const int split = wid / ntile;
+  const int tile = wid - split * ntile;
+  const int ct = tile / a.ktiles, nt = tile - ct * a.ktiles;
+  const int mt0 = split * a.mt_per_split;
+  const int nk = min(a.mtiles, mt0 + a.mt_per_split) - mt0;
+
+  const int rA0 = tid / CPR_A, rB0 = tid / CPR_B;
+  const int cA = (tid % CPR_A) ^ trsw<BM>(rA0);
+  const int cB = (tid % CPR_B) ^ trsw<BN>(rB0);
+  const int co = ct * BM + 8 * cA;
+  const bool coka = co < d.CO;
+  const int kp = nt * BN + 8 * cB;
+  const bool kokb = kp < a.K2;
+  const uint32_t tap = fdiv((uint32_t)(kokb ? kp : 0), a.f_c);
+  const int ci = (kokb ? kp : 0) - (int)(tap * a.f_c.d);
+  const uint32_t kyu = fdiv(tap, a.f_kw);
+  const int ky = (int)kyu, kx = (int)(tap - kyu * a.f_kw.d);
+  const __bf16* Xp = reinterpret_cast<const __bf16*>(a.X);
+  const int HWC = d.H * d.W * d.C;
+
+  auto issue = [&](int mtile, int buf) {
+    uint8_t* As = lds + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int m = mtile * 64 + rA0 + A_RPP * i;
+      const bool ok = coka && m < a.M;
+      glds16(ok ? (const void*)(a.G + (size_t)m * d.CO + co) : (const void*)g_zero16,
+             As + (A_RPP * i + w * (64 / CPR_A)) * (BM * 2));
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int r = rB0 + B_RPP * i;
+      const int m = mtile * 64 + r;
+      const bool mok = r < 64 && m < a.M;
+      const uint32_t mm = mok ? (uint32_t)m : 0u;
+      const uint32_t n = fdiv(mm, a.f_pix);
+      const uint32_t rem = mm - n * a.f_pix.d;
+      const uint32_t oy = fdiv(rem, a.f_w);
+      const uint32_t ox = rem - oy * a.f_w.d;
+      const int iy = (int)oy * d.S - d.P + ky, ix = (int)ox * d.S - d.P + kx;
+      const bool ok = mok && kokb && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+      glds16(ok ? (const void*)(Xp + (int)n * HWC + (iy * d.W + ix) * d.C + ci) : (const void*)g_zero16,
+             Bs + (B_RPP * i + w * (64 / CPR_B)) * (BN * 2));
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const uint8_t* As = lds + buf * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2 / KWS; ++s) {
+      const int kb = 32 * (KWS == 2 ? wk : s);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) af[fm] = tr_frag<BM>(As, wm * (BM / WM) + 16 * fm, kb, lane);
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) bfr[fn] = tr_frag<BN>(Bs, wn * (BN / WN) + 16 * fn, kb, lane);
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          *reinterpret_cast<f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4) = acc[fm][fn];
+        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
     }
-    __syncthreads();
-    if (wk == 0) {
+  };
+
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] += *reinterpret_cast<const f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4);
-    }
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(mt0 + s, s);
+  for (int it = 0; it < nk; ++it) {
+    const int newer = min(nk - 1 - it, S - 2);
+    wait_tiles<NI, S>(newer);
+    stage_barrier();
+    if (it + S - 1 < nk) issue(mt0 + it + S - 1, (it + S - 1) % S);
+    compute(it % S);
   }
-  if (KWS == 1 || wk == 0) {
-    float* out = a.out + (size_t)split * d.CO * a.K2;
-#pragma unroll
-    for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int orow = ct * BM + wm * (BM / WM) + fm * 16 + 4 * (lane >> 4) + r;
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int kp = nt * BN + wn * (BN / WN) + fn * 16 + (lane & 15);
-          if (orow < d.CO && kp < a.K2) out[(size_t)orow * a.K2 + kp] = acc[fm][fn][r];
-        }
-      }
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stage_barrier();
+  wgrad_epilogue<TC>(a, acc, lds, ct, nt, split);
 }
 
 // ======================================================= small reductions ====
 // Split-K combine: y = sum_z slab[z] + bias (+relu) -> f32 and/or bf16.
-__global__ void __launch_bounds__(256) splitk_combine_k(const float* slab, int ksplit, int M, int N,
+// `cnt` outputs per block, 256/cnt threads per output summing interleaved
+// z slices (independent loads in flight), then a fixed-order LDS combine.
+__global__ void __launch_bounds__(256) splitk_combine_k(const float* slab, int ksplit, int M, int N, int cnt,
                                                         const float* bias, int relu, float* y32, __bf16* y16) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float red[256];
+  const int t = threadIdx.x, rp = 256 / cnt, col = t % cnt, rl = t / cnt;
   const long long MN = (long long)M * N;
-  if (e >= MN) return;
+  const long long e = (long long)blockIdx.x * cnt + col;
   float v = 0.f;
-  for (int z = 0; z < ksplit; ++z) v += slab[(size_t)z * MN + e];
-  if (bias) v += bias[e % N];
-  if (relu) v = fmaxf(v, 0.f);
-  if (y32) y32[e] = v;
-  if (y16) y16[e] = (__bf16)v;
+  if (rl < rp && e < MN) {
+#pragma unroll 4
+    for (int z = rl; z < ksplit; z += rp) v += slab[(size_t)z * MN + e];
+  }
+  red[t] = v;
+  __syncthreads();
+  if (rl == 0 && e < MN) {
+    float acc = 0.f;
+    for (int r = 0; r < rp; ++r) acc += red[r * cnt + col];
+    if (bias) acc += bias[e % N];
+    if (relu) acc = fmaxf(acc, 0.f);
+    if (y32) y32[e] = acc;
+    if (y16) y16[e] = (__bf16)acc;
+  }
 }
 
 // Column sums of a bf16 [M][N] matrix (N % 8 == 0): partial row blockIdx.y of
@@ -607,6 +932,7 @@ __global__ void __launch_bounds__(256) colsum_k(const __bf16* G, int M, int N, i
   if (c8 * 8 >= N) return;
   const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
   for (int r = r0; r < r1; ++r) {
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(G + (size_t)r * N + 8 * c8);
 #pragma unroll
@@ -707,6 +1033,19 @@ bool plan_wgrad(const ConvDesc& d, WgradPlan* p) {
   return true;
 }
 
+// Staging path for bf16 vector-gather GEMMs: the register-staged double
+// buffer (default) or the S-stage LDS-DMA ring (MDT_CONV_GLDS=1). Measured on
+// MI355X (bench/gemm_calib.py, profiles/r1_conv_igemm/README.md): the DMA
+// ring needs 80-128 KB LDS, i.e. one block per CU, and loses 10-60 % at every
+// conv shape and at 4096^3, so it is kept only as an A/B option.
+bool use_glds() {
+  static const bool v = [] {
+    const char* e = getenv("MDT_CONV_GLDS");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 template <int MODE, typename AT, bool VEC, class TC>
 void launch_fwd(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
   dim3 grid(q.mtiles * q.ntiles, q.ksplit, q.classes);
@@ -728,6 +1067,28 @@ int dispatch_fwd_cfg(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
   return 2;
 }
 
+template <int MODE, class TC, int S>
+void launch_glds(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
+  dim3 grid(q.mtiles * q.ntiles, q.ksplit, q.classes);
+  hipLaunchKernelGGL((igemm_glds_k<MODE, TC, S>), grid, dim3(256), 0, s, a);
+}
+
+// bf16 vector-gather problems: S-stage LDS-DMA pipeline (S*STAGE <= 128 KB)
+template <int MODE>
+int dispatch_glds(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
+  switch (q.cfg) {
+    case 0: launch_glds<MODE, F0, 4>(a, q, s); return 0;
+    case 1: launch_glds<MODE, F1, 4>(a, q, s); return 0;
+    case 2: launch_glds<MODE, F2, 4>(a, q, s); return 0;
+    case 3: launch_glds<MODE, F3, 4>(a, q, s); return 0;
+    case 4: launch_glds<MODE, F4, 4>(a, q, s); return 0;
+    case 5: launch_glds<MODE, F5, 6>(a, q, s); return 0;
+    case 6: launch_glds<MODE, F6, 6>(a, q, s); return 0;
+    case 7: launch_glds<MODE, F7, 6>(a, q, s); return 0;
+  }
+  return 2;
+}
+
 template <typename AT>
 int dispatch_thin(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
   if (q.cfg == 2) { launch_fwd<kModeConv, AT, false, F2>(a, q, s); return 0; }
@@ -735,9 +1096,15 @@ int dispatch_thin(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
   return 2;
 }
 
+template <class TC, int S>
+void launch_wgg(const WgArgs& a, const WgradPlan& q, hipStream_t s) {
+  dim3 grid(q.cotiles * q.ktiles * q.nsplit);
+  hipLaunchKernelGGL((wgrad_glds_k<TC, S>), grid, dim3(256), 0, s, a);
+}
+
 template <typename XT, bool VEC, class TC>
 void launch_wg(const WgArgs& a, const WgradPlan& q, hipStream_t s) {
-  dim3 grid(q.cotiles * q.ktiles, q.nsplit);
+  dim3 grid(q.cotiles * q.ktiles * q.nsplit);
   hipLaunchKernelGGL((wgrad_k<XT, VEC, TC>), grid, dim3(256), 0, s, a);
 }
 
@@ -796,14 +1163,20 @@ int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d
   if (mode == kModeConv) {
     if (q.thin) rc = a_is_f32 ? dispatch_thin<float>(a, q, s) : dispatch_thin<__bf16>(a, q, s);
     else if (a_is_f32) rc = 3;
+    else if (use_glds()) rc = dispatch_glds<kModeConv>(a, q, s);
     else rc = dispatch_fwd_cfg<kModeConv, __bf16, true>(a, q, s);
+  } else if (a_is_f32) {
+    rc = 3;
   } else {
-    rc = a_is_f32 ? 3 : dispatch_fwd_cfg<kModeTconv, __bf16, true>(a, q, s);
+    rc = use_glds() ? dispatch_glds<kModeTconv>(a, q, s) : dispatch_fwd_cfg<kModeTconv, __bf16, true>(a, q, s);
   }
   if (rc) return rc;
   if (q.ksplit > 1) {
     const long long MN = (long long)q.M * q.Ncols;
-    hipLaunchKernelGGL(splitk_combine_k, dim3(cdiv(MN, 256)), dim3(256), 0, s, ws, q.ksplit, q.M, q.Ncols, bias,
+    int rp = 1;
+    while (rp < 64 && rp * 4 < q.ksplit) rp *= 2;
+    const int cnt = 256 / rp;
+    hipLaunchKernelGGL(splitk_combine_k, dim3(cdiv(MN, cnt)), dim3(256), 0, s, ws, q.ksplit, q.M, q.Ncols, cnt, bias,
                        relu, y32, reinterpret_cast<__bf16*>(y16));
   }
   return (int)hipGetLastError();
@@ -817,10 +1190,11 @@ int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* o
   a.G = reinterpret_cast<const __bf16*>(G16);
   a.X = X;
   a.out = out;
-  a.M = q.M; a.K2 = q.K2; a.ktiles = q.ktiles; a.mtiles = q.mtiles; a.mt_per_split = q.mt_per_split;
+  a.M = q.M; a.K2 = q.K2; a.cotiles = q.cotiles; a.ktiles = q.ktiles; a.mtiles = q.mtiles;
+  a.mt_per_split = q.mt_per_split;
   a.f_pix = make_fastdiv(d.OH * d.OW); a.f_w = make_fastdiv(d.OW);
   a.f_c = make_fastdiv(d.C); a.f_kw = make_fastdiv(d.KW);
-  if (!q.thin) {
+  if (!q.thin && !use_glds()) {
     if (x_is_f32) return 3;
     switch (q.cfg) {
       case 0: launch_wg<__bf16, true, W0>(a, q, s); break;
@@ -829,6 +1203,17 @@ int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* o
       case 3: launch_wg<__bf16, true, W3>(a, q, s); break;
       case 4: launch_wg<__bf16, true, W4>(a, q, s); break;
       case 5: launch_wg<__bf16, true, W5>(a, q, s); break;
+      default: return 2;
+    }
+  } else if (!q.thin) {
+    if (x_is_f32) return 3;
+    switch (q.cfg) {
+      case 0: launch_wgg<W0, 6>(a, q, s); break;
+      case 1: launch_wgg<W1, 6>(a, q, s); break;
+      case 2: launch_wgg<W2, 6>(a, q, s); break;
+      case 3: launch_wgg<W3, 6>(a, q, s); break;
+      case 4: launch_wgg<W4, 6>(a, q, s); break;
+      case 5: launch_wgg<W5, 6>(a, q, s); break;
       default: return 2;
     }
   } else {

@@ -31,10 +31,16 @@ int mdt_bce_logits(const float* logits, const float* X, const int* rows, int B, 
 int mdt_conv_loss_finalize(const float* bce_part, int nb, const float* kld_part, int nk, void* st, const void* hp,
                            int advance_cursor, hipStream_t s);
 int mdt_step_begin(void* st, const void* hp, hipStream_t s);
-int mdt_adam_cast(float* P, const float* G, float* Mo, float* Vo, void* w16, void* w16t, const void* segs, int nseg,
+int mdt_adam_cast(float* P, const float* G, float* Mo, float* Vo, void* w16, const void* segs, int nseg,
                   long long total, const void* st, const void* hp, int do_adam, hipStream_t s);
-int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, void* w16t, const void* segs,
-                      const void* units, int nunits, const void* st, const void* hp, int do_adam, hipStream_t s);
+int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs, const void* units,
+                      int nunits, const void* st, const void* hp, int do_adam, hipStream_t s);
+int mdt_wtrans(const void* w16, void* w16t, const void* segs, const void* units, int nunits, hipStream_t s);
+int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, mdt::ConvDesc d, const float* bias, int relu, void* y16,
+                  const void* omask, float* colsum, hipStream_t s);
+int mdt_thin_blocks(int tconv, mdt::ConvDesc d);
+int mdt_thin_tconv(const void* G16, const float* Wf, mdt::ConvDesc d, const float* bias, float* y32, const float* X,
+                   void* dlog16, float* recon, float* part, float* gpart, hipStream_t s);
 }
 
 namespace mdt {
@@ -121,6 +127,54 @@ void wgrad(const at::Tensor& G16, const at::Tensor& X, const std::vector<int64_t
   rc(mdt_wgrad(G16.data_ptr(), X.data_ptr(), f32, d, out.data_ptr<float>(), cur()), "wgrad");
 }
 
+// Single-channel edge layers (conv_thin.hip): Wf is the f32 master weight
+// [CO][KH][KW][1] (read with wave-uniform scalar loads).
+void thin_conv(const at::Tensor& X, const at::Tensor& Wf, const std::vector<int64_t>& dv,
+               const c10::optional<at::Tensor>& bias, bool relu, at::Tensor y16,
+               const c10::optional<at::Tensor>& omask, const c10::optional<at::Tensor>& colsum) {
+  const ConvDesc d = desc(dv);
+  const bool f32 = X.scalar_type() == torch::kFloat32;
+  TORCH_CHECK(X.is_cuda() && X.is_contiguous() && (f32 || X.scalar_type() == torch::kBFloat16), "X dtype/layout");
+  check_f32(Wf, "Wf");
+  check_bf16(y16, "y16");
+  const int64_t M = (int64_t)d.N * d.OH * d.OW;
+  TORCH_CHECK(X.numel() >= (int64_t)d.N * d.H * d.W, "X too small");
+  TORCH_CHECK(Wf.numel() >= (int64_t)d.CO * d.KH * d.KW, "Wf too small");
+  TORCH_CHECK(y16.numel() >= M * d.CO, "y16 too small");
+  check_min(omask, M * d.CO, "omask");
+  check_min(colsum, (int64_t)mdt_thin_blocks(0, d) * d.CO, "colsum");
+  check_min(bias, d.CO, "bias");
+  rc(mdt_thin_conv(X.data_ptr(), f32, Wf.data_ptr<float>(), d, (const float*)opt_ptr(bias), relu, y16.data_ptr(),
+                   opt_ptr(omask), (float*)opt_ptr(colsum), cur()),
+     "thin_conv");
+}
+
+int64_t thin_blocks(bool tconv, const std::vector<int64_t>& dv) { return mdt_thin_blocks(tconv ? 1 : 0, desc(dv)); }
+
+void thin_tconv(const at::Tensor& G16, const at::Tensor& Wf, const std::vector<int64_t>& dv,
+                const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& y32,
+                const c10::optional<at::Tensor>& X, const c10::optional<at::Tensor>& dlog16,
+                const c10::optional<at::Tensor>& recon, const c10::optional<at::Tensor>& part,
+                const c10::optional<at::Tensor>& gpart) {
+  const ConvDesc d = desc(dv);
+  check_bf16(G16, "G16");
+  check_f32(Wf, "Wf");
+  const int64_t npix = (int64_t)d.N * d.H * d.W;
+  const int64_t nb = mdt_thin_blocks(1, d);
+  TORCH_CHECK(G16.numel() >= (int64_t)d.N * d.OH * d.OW * d.CO, "G16 too small");
+  TORCH_CHECK(Wf.numel() >= (int64_t)d.CO * d.KH * d.KW, "Wf too small");
+  check_min(y32, npix, "y32");
+  check_min(X, npix, "X");
+  check_min(dlog16, npix, "dlog16");
+  check_min(recon, npix, "recon");
+  check_min(part, nb, "part");
+  check_min(gpart, nb, "gpart");
+  rc(mdt_thin_tconv(G16.data_ptr(), Wf.data_ptr<float>(), d, (const float*)opt_ptr(bias), (float*)opt_ptr(y32),
+                    (const float*)opt_ptr(X), const_cast<void*>(opt_ptr(dlog16)), (float*)opt_ptr(recon),
+                    (float*)opt_ptr(part), (float*)opt_ptr(gpart), cur()),
+     "thin_tconv");
+}
+
 void colsum(const at::Tensor& G16, int64_t M, int64_t N, int64_t rows_per, at::Tensor slab) {
   check_bf16(G16, "G16");
   check_f32(slab, "slab");
@@ -200,22 +254,38 @@ at::Tensor make_grad_units(const std::vector<std::vector<int64_t>>& units, int64
   return cpu.to(torch::Device(torch::kCUDA, device_index));
 }
 
-void adam_cast(at::Tensor P, const at::Tensor& G, at::Tensor M, at::Tensor V, at::Tensor w16, at::Tensor w16t,
-               const at::Tensor& segs, int64_t nseg, const at::Tensor& state, const at::Tensor& hparams,
-               bool do_adam) {
+at::Tensor make_tr_units(const std::vector<std::vector<int64_t>>& units, int64_t device_index) {
+  std::vector<TrUnit> v;
+  for (auto& u : units) {
+    TORCH_CHECK(u.size() == 4, "unit = (seg, tap, co0, ci0)");
+    v.push_back(TrUnit{(int)u[0], (int)u[1], (int)u[2], (int)u[3]});
+  }
+  auto cpu = torch::empty({(int64_t)std::max<size_t>(1, v.size() * sizeof(TrUnit))}, torch::kUInt8);
+  if (!v.empty()) std::memcpy(cpu.data_ptr(), v.data(), v.size() * sizeof(TrUnit));
+  return cpu.to(torch::Device(torch::kCUDA, device_index));
+}
+
+void adam_cast(at::Tensor P, const at::Tensor& G, at::Tensor M, at::Tensor V, at::Tensor w16, const at::Tensor& segs,
+               int64_t nseg, const at::Tensor& state, const at::Tensor& hparams, bool do_adam) {
   rc(mdt_adam_cast(P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(),
-                   w16.data_ptr(), w16t.data_ptr(), segs.data_ptr(), (int)nseg, P.numel(), state.data_ptr(),
-                   hparams.data_ptr(), do_adam ? 1 : 0, cur()),
+                   w16.data_ptr(), segs.data_ptr(), (int)nseg, P.numel(), state.data_ptr(), hparams.data_ptr(),
+                   do_adam ? 1 : 0, cur()),
      "adam_cast");
 }
 
-void grad_finalize(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::Tensor w16, at::Tensor w16t,
-                   const at::Tensor& segs, const at::Tensor& units, int64_t nunits, const at::Tensor& state,
-                   const at::Tensor& hparams, bool do_adam) {
+void grad_finalize(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::Tensor w16, const at::Tensor& segs,
+                   const at::Tensor& units, int64_t nunits, const at::Tensor& state, const at::Tensor& hparams,
+                   bool do_adam) {
   rc(mdt_grad_finalize(P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(),
-                       w16.data_ptr(), w16t.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits,
-                       state.data_ptr(), hparams.data_ptr(), do_adam ? 1 : 0, cur()),
+                       w16.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits, state.data_ptr(),
+                       hparams.data_ptr(), do_adam ? 1 : 0, cur()),
      "grad_finalize");
+}
+
+void wtrans(const at::Tensor& w16, at::Tensor w16t, const at::Tensor& segs, const at::Tensor& units, int64_t nunits) {
+  check_bf16(w16, "w16");
+  check_bf16(w16t, "w16t");
+  rc(mdt_wtrans(w16.data_ptr(), w16t.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits, cur()), "wtrans");
 }
 
 // ------------------------------------------------------------------ state ----
@@ -294,6 +364,12 @@ void bind_conv(pybind11::module& m) {
         py::arg("colsum") = py::none(), py::arg("ws") = py::none());
   m.def("wgrad", &wgrad);
   m.def("colsum", &colsum);
+  m.def("thin_conv", &thin_conv, py::arg("X"), py::arg("Wf"), py::arg("desc"), py::arg("bias"), py::arg("relu"),
+        py::arg("y16"), py::arg("omask") = py::none(), py::arg("colsum") = py::none());
+  m.def("thin_blocks", &thin_blocks);
+  m.def("thin_tconv", &thin_tconv, py::arg("G16"), py::arg("Wf"), py::arg("desc"), py::arg("bias"),
+        py::arg("y32") = py::none(), py::arg("X") = py::none(), py::arg("dlog16") = py::none(),
+        py::arg("recon") = py::none(), py::arg("part") = py::none(), py::arg("gpart") = py::none());
   m.def("gather_rows", &gather_rows);
   m.def("reparam", &reparam);
   m.def("reparam_bwd", &reparam_bwd);
@@ -303,8 +379,10 @@ void bind_conv(pybind11::module& m) {
   m.def("step_begin", &step_begin);
   m.def("make_grad_segs", &make_grad_segs);
   m.def("make_grad_units", &make_grad_units);
+  m.def("make_tr_units", &make_tr_units);
   m.def("adam_cast", &adam_cast);
   m.def("grad_finalize", &grad_finalize);
+  m.def("wtrans", &wtrans);
   py::class_<TrialStateBuf>(m, "TrialState")
       .def(py::init<int64_t>())
       .def("set_hparams", &TrialStateBuf::set_hparams)

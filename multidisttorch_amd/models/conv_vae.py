@@ -346,8 +346,20 @@ class ConvVaeTrainer:
             self._toff[l.name] = toff
             toff = (toff + math.prod(_w_shape(l)) + 63) // 64 * 64
         self.w16t = torch.zeros(max(toff, 64), **bf)
-        self.segs = self.C.make_grad_segs(self._seg_rows({}), dev.index or 0)
+        rows = self._seg_rows({})
+        self.segs = self.C.make_grad_segs(rows, dev.index or 0)
         self.nseg = 2 * len(self.spec)
+        tr = []
+        for si, r in enumerate(rows):
+            if r[8] < 0:
+                continue
+            co, k, ci = r[4], r[5], r[7]
+            for tap in range(k * k):
+                for co0 in range(0, co, 64):
+                    for ci0 in range(0, ci, 64):
+                        tr.append([si, tap, co0, ci0])
+        self.tr_units = self.C.make_tr_units(tr, dev.index or 0)
+        self.n_tr = len(tr)
         self.xb = torch.zeros(B, self.D, **f32)
         self.acts, self.gacts = {}, {}
         for l in self.spec:
@@ -364,10 +376,26 @@ class ConvVaeTrainer:
         self.logits = torch.zeros(B * self.D, **f32)
         self.recon = torch.zeros(B * self.D, **f32)
         self.dlog16 = torch.zeros(B * self.D, **bf)
-        self.bce_part = torch.zeros(-(-B * self.D // 256), **f32)
+        first, last = self.spec[0], self.spec[-1]
+        # single-channel edge layers run on the direct kernels of conv_thin.hip
+        self._thin_first = first.kind == "conv" and first.cin == 1 and first.cout in (16, 32, 64) and first.k <= 4
+        self._thin_last = (last.kind == "convT" and last.cout == 1 and last.cin in (16, 32, 64) and last.k % last.s == 0
+                           and last.out_hw % last.s == 0)
+        self.bce_part = torch.zeros(max(self._n_bce(B), 1), **f32)
         self.kld_part = torch.zeros(-(-B * zf // 256), **f32)
         self._plans = {}
         self._cast_weights()
+
+    def _n_bce(self, M):
+        """Number of BCE loss partials the forward writes for a batch of M."""
+        if self._thin_last:
+            return self.C.thin_blocks(True, self._desc(self.spec[-1], M))
+        return -(-M * self.D // 256)
+
+    def _wf32(self, l):
+        """f32 master weight of a layer (read directly by the thin kernels)."""
+        o, s = next((o, s) for n, o, s in self.layout if n == l.name + ".weight")
+        return self.params.narrow(0, o, math.prod(s))
 
     def _seg_rows(self, slabs):
         """GradSeg rows (off, numel, slab_ptr, nsplit, co, k, s, ci, toff) for every
@@ -410,6 +438,12 @@ class ConvVaeTrainer:
             if i == 0:
                 continue
             prev = spec[i - 1]
+            if i == len(spec) - 1 and self._thin_last:
+                rows, ncols = C.thin_blocks(False, d), prev.cout
+                t = torch.empty(rows * ncols, **f32)
+                colsum[prev.name] = t
+                slabs[prev.name + ".bias"] = (t, rows)
+                continue
             mode = 0 if l.kind == "convT" else 1
             split_ok = l.name == "dec_fc"
             q = C.igemm_plan(mode, d, split_ok)
@@ -426,8 +460,15 @@ class ConvVaeTrainer:
                 q = C.igemm_plan(0, self._desc(l, M), True)
                 if q[10] > 1:
                     ws_need = max(ws_need, q[10] * q[4] * q[5])
+        rows_per = 8  # colsum kernel partial rows for the per-feature biases
+        ncs = -(-M // rows_per)
+        for l in spec:
+            if l.name in ("dec_fc", "enc_head"):
+                t = torch.empty(ncs * l.cout, **f32)
+                colsum[l.name] = t
+                slabs[l.name + ".bias"] = (t, ncs)
         last = spec[-1]
-        nb = -(-M * self.D // 256)
+        nb = self._n_bce(M)
         gpart = torch.empty(nb, **f32)
         if self.channels == 1:
             slabs[last.name + ".bias"] = (gpart, nb)
@@ -443,7 +484,7 @@ class ConvVaeTrainer:
             cnt = 512 // rp
             for st in range(0, numel, cnt):
                 units.append([si, st, min(cnt, numel - st)])
-        p = dict(slabs=slabs, colsum=colsum, gpart=gpart, ws=torch.empty(max(ws_need, 1), **f32),
+        p = dict(slabs=slabs, colsum=colsum, gpart=gpart, ws=torch.empty(max(ws_need, 1), **f32), rows_per=rows_per,
                  segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
                  nunits=len(units))
         self._plans[M] = p
@@ -451,8 +492,13 @@ class ConvVaeTrainer:
 
     def _cast_weights(self):
         h = self.state
-        self.C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.w16t, self.segs,
-                         self.nseg, h.train_state, h.hparams, False)
+        self.C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
+                         h.train_state, h.hparams, False)
+        self._transpose_weights()
+
+    def _transpose_weights(self):
+        """bf16 weights -> parity-ordered transposed copies (one coalesced launch)."""
+        self.C.wtrans(self.w16, self.w16t, self.segs, self.tr_units, self.n_tr)
 
     def _w(self, l):
         o, s = next((o, s) for n, o, s in self.layout if n == l.name + ".weight")
@@ -480,9 +526,14 @@ class ConvVaeTrainer:
 
     def _layer_fwd(self, l, h, M, o16, o32, ws):
         """conv / linear: conv-mode GEMM; convT: parity-class GEMM on the
-        transposed weights (no zero-insertion taps)."""
+        transposed weights (no zero-insertion taps); single-channel edge
+        layers: direct kernels."""
         d = self._desc(l, M)
-        if l.kind == "convT":
+        if l is self.spec[0] and self._thin_first:
+            self.C.thin_conv(h, self._wf32(l), d, self._b(l), l.relu, o16)
+        elif l is self.spec[-1] and self._thin_last:
+            self.C.thin_tconv(h, self._wf32(l), d, self._b(l), y32=o32)
+        elif l.kind == "convT":
             self.C.igemm(1, h, self._wt(l), d, self._b(l), l.relu, o16, o32)
         else:
             self.C.igemm(0, h, self._w(l), d, self._b(l), l.relu, o16, o32, ws=ws)
@@ -501,6 +552,11 @@ class ConvVaeTrainer:
         h = self.z16
         for l in dec:
             last = l is dec[-1]
+            if last and self._thin_last:  # last layer + BCE + dlogits + bias-grad partials, one launch
+                C.thin_tconv(h, self._wf32(l), self._desc(l, M), self._b(l), X=self.xb,
+                             dlog16=self.dlog16 if train else None, recon=self.recon if want_recon else None,
+                             part=self.bce_part, gpart=p["gpart"] if train else None)
+                return
             self._layer_fwd(l, h, M, None if last else self.acts[l.name], self.logits if last else None, p["ws"])
             h = self.acts[l.name]
         C.bce_logits(self.logits, self.xb, None, M, self.D, self.dlog16 if train else None,
@@ -536,15 +592,18 @@ class ConvVaeTrainer:
             if l.name == "dec_fc":
                 C.igemm(1, g, self._wt(l), d, None, False, None, self.dz, ws=p["ws"])
                 C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M, self.Z, self.state.hparams)
-                C.colsum(self.dmulv16, M, 2 * self.Z, M, self._gb(prev))
+                C.colsum(self.dmulv16, M, 2 * self.Z, p["rows_per"], p["colsum"][prev.name])
                 gin = self.dmulv16
+            elif i == len(spec) - 1 and self._thin_last:
+                gin = self.gacts[prev.name]
+                C.thin_conv(g, self._wf32(l), d, None, False, gin, omask, p["colsum"][prev.name])
             else:
                 gin = self.gacts[prev.name]
-                cs = p["colsum"].get(prev.name)
+                cs = None if prev.name == "dec_fc" else p["colsum"].get(prev.name)
                 C.igemm(0 if l.kind == "convT" else 1, g, self._w(l) if l.kind == "convT" else self._wt(l), d,
                         None, False, gin, None, omask, cs)
                 if prev.name == "dec_fc":
-                    C.colsum(gin, M, prev.cout, M, self._gb(prev))
+                    C.colsum(gin, M, prev.cout, p["rows_per"], p["colsum"][prev.name])
             g = gin
 
     def _step_hip(self, M):
@@ -554,24 +613,25 @@ class ConvVaeTrainer:
         C.step_begin(st.train_state, st.hparams)
         C.gather_rows(X, idx, st.train_state, self.B, M, self.xb)
         self._forward_hip(M, st.train_state, self.rng_stream)
-        C.loss_finalize2(self.bce_part, -(-M * self.D // 256), self.kld_part, -(-M * self.Z // 256),
+        C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, -(-M * self.Z // 256),
                          st.train_state, st.hparams, True)
         self._backward_hip(M)
         if self.reducer is not None:
             self._finalize_grads(M, False)
             self.reducer.launch_all()
             self.reducer.wait_all()
-            C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.w16t, self.segs,
-                        self.nseg, st.train_state, st.hparams, True)
+            C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
+                        st.train_state, st.hparams, True)
         else:
             self._finalize_grads(M, True)
+        self._transpose_weights()
 
     def _finalize_grads(self, M, do_adam):
         """Reduce the partial slabs into the gradient arena (deterministic order);
         with ``do_adam`` also apply Adam and re-emit the bf16 weight copies."""
         p, st = self._plan(M), self.state
-        self.C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.w16t, p["segs"],
-                             p["units"], p["nunits"], st.train_state, st.hparams, do_adam)
+        self.C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
+                             p["nunits"], st.train_state, st.hparams, do_adam)
 
     # ----------------------------------------------------------- torch path
     def _step_torch(self, M):
@@ -665,7 +725,7 @@ class ConvVaeTrainer:
                 self.C.gather_rows(X.contiguous(), idx, st.eval_state, self.B, M, self.xb)
                 want = want_first_recon and b == 0
                 self._forward_hip(M, st.eval_state, EVAL_STREAM + self.rng_stream, want_recon=want, train=False)
-                self.C.loss_finalize2(self.bce_part, -(-M * self.D // 256), self.kld_part, -(-M * self.Z // 256),
+                self.C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, -(-M * self.Z // 256),
                                       st.eval_state, st.hparams, True)
                 if want:
                     first = self.recon[: M * self.D].view(M, self.D).clone()

@@ -171,9 +171,63 @@ def test_grad_finalize_is_deterministic_and_fuses_adam(native_ext):
     outs = []
     for _ in range(2):
         G = z()
-        C.grad_finalize(P.clone(), G, z(), z(), torch.zeros(numel, dtype=torch.bfloat16, device=dev),
-                        torch.zeros(64, dtype=torch.bfloat16, device=dev), segs, U, len(units),
-                        state.train_state, state.hparams, False)
+        C.grad_finalize(P.clone(), G, z(), z(), torch.zeros(numel, dtype=torch.bfloat16, device=dev), segs, U,
+                        len(units), state.train_state, state.hparams, False)
         outs.append(G)
     assert torch.equal(outs[0], outs[1])
     assert _rel(outs[0], slab.view(ns, numel).sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("f32_in", [True, False])
+def test_thin_conv_matches_conv2d(f32_in, native_ext):
+    """Single-input-channel conv (encoder conv 1 / last layer backward-data)."""
+    C = native_ext
+    N, H, CO = 5, 28, 32
+    torch.manual_seed(3)
+    x = torch.rand(N, H, H, 1, device=DEV)
+    if not f32_in:
+        x = _bf(x)
+    w = torch.randn(CO, 4, 4, 1, device=DEV) / 4
+    b = torch.randn(CO, device=DEV)
+    d = conv_desc(N, H, H, 1, CO, 4, 2, 1)
+    M = N * 14 * 14
+    y16 = torch.zeros(M * CO, device=DEV, dtype=torch.bfloat16)
+    mask = _bf(torch.randn(M, CO, device=DEV))
+    nb = C.thin_blocks(False, d)
+    cs = torch.full((nb * CO,), float("nan"), device=DEV)
+    ref = F.conv2d(nchw(x.float()), torch_weight(w), None if f32_in else None, 2, 1)
+    if f32_in:  # encoder conv 1: bias + ReLU
+        C.thin_conv(x, w.flatten(), d, b, True, y16)
+        ref = nhwc(F.relu(ref + b.view(1, -1, 1, 1))).reshape(M, CO)
+    else:       # backward-data of the last layer: output mask + column sums
+        C.thin_conv(x, w.flatten(), d, None, False, y16, mask, cs)
+        ref = nhwc(ref).reshape(M, CO) * (mask.float() > 0)
+        assert _rel(cs.view(nb, CO).sum(0), ref.sum(0)) < 1e-5
+    assert _rel(y16.float().view(M, CO), ref) < 1e-2
+
+
+def test_thin_tconv_fused_bce(native_ext):
+    """Last decoder layer (32 -> 1 transposed conv) fused with logit BCE."""
+    C = native_ext
+    N, OH, CI = 4, 14, 32
+    torch.manual_seed(4)
+    d = conv_desc(N, 2 * OH, 2 * OH, 1, CI, 4, 2, 1)
+    g = _bf(torch.randn(N, OH, OH, CI, device=DEV))
+    w = torch.randn(CI, 4, 4, 1, device=DEV) / 8
+    b = torch.randn(1, device=DEV)
+    x = torch.rand(N, 2 * OH * 2 * OH, device=DEV)
+    npix = x.numel()
+    nb = C.thin_blocks(True, d)
+    logits = torch.zeros(npix, device=DEV)
+    dlog = torch.zeros(npix, device=DEV, dtype=torch.bfloat16)
+    part = torch.zeros(nb, device=DEV)
+    gpart = torch.zeros(nb, device=DEV)
+    C.thin_tconv(g, w.flatten(), d, b, y32=logits)
+    C.thin_tconv(g, w.flatten(), d, b, X=x, dlog16=dlog, part=part, gpart=gpart)
+    t = F.conv_transpose2d(nchw(g.float()), torch_weight(w), b, 2, 1).reshape(N, -1)
+    assert _rel(logits.view(N, -1), t) < 1e-5
+    p = torch.sigmoid(t)
+    bce = F.binary_cross_entropy(p.double(), x.double(), reduction="sum")
+    assert abs(float(part.sum()) - float(bce)) / float(bce) < 1e-4
+    assert _rel(dlog.float().view(N, -1), p - x) < 1e-2
+    assert abs(float(gpart.sum()) - float((p - x).sum())) < 1e-2 * float((p - x).abs().sum())
