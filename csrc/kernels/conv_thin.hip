@@ -39,10 +39,11 @@ __device__ __forceinline__ void block_colsum(const float (&v)[CO], float* red, f
   }
 }
 
-template <int CO, typename TIN>
+template <int CO, int K, typename TIN>
 __global__ void __launch_bounds__(256) thin_conv_k(const TIN* X, const float* Wf, ConvDesc d, const float* bias,
                                                    int relu, __bf16* y16, const __bf16* omask, float* colsum) {
   extern __shared__ float red[];  // 256 * (CO + 1) floats when colsum != null
+  constexpr int TAPS = K * K;
   const int M = d.N * d.OH * d.OW;
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = m < M;
@@ -52,29 +53,35 @@ __global__ void __launch_bounds__(256) thin_conv_k(const TIN* X, const float* Wf
   const int oy = rem / d.OW, ox = rem - oy * d.OW;
   const int iy0 = oy * d.S - d.P, ix0 = ox * d.S - d.P;
   const TIN* img = X + (size_t)n * d.H * d.W;
-  const int taps = d.KH * d.KW;  // <= 16 (host-checked); loops fully unrolled so xin stays in VGPRs
-  float xin[16];
+  float xin[TAPS];
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    float v = 0.f;
-    if (t < taps) {
-      const int ky = t / d.KW, kx = t - ky * d.KW;
-      const int iy = iy0 + ky, ix = ix0 + kx;
-      const bool ok = live && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-      const float x = ld1(img + (ok ? iy * d.W + ix : 0));
-      v = ok ? x : 0.f;
-    }
-    xin[t] = v;
+  for (int t = 0; t < TAPS; ++t) {
+    const int iy = iy0 + t / K, ix = ix0 + t % K;
+    const bool ok = live && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+    const float x = ld1(img + (ok ? iy * d.W + ix : 0));
+    xin[t] = ok ? x : 0.f;
   }
+  // weights staged once per block in LDS as [tap][co]; the FMA loop reads
+  // them with wave-uniform (broadcast) ds_read_b128, 4 channels per read
+  __shared__ __attribute__((aligned(16))) float wl[TAPS * CO];
+  for (int e = threadIdx.x; e < TAPS * CO; e += blockDim.x) {
+    const int c = e / TAPS, t = e - c * TAPS;
+    wl[t * CO + c] = Wf[e];
+  }
+  __syncthreads();
   float acc[CO];
 #pragma unroll
   for (int c = 0; c < CO; ++c) acc[c] = bias ? bias[c] : 0.f;
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    if (t < taps) {
-      const float x = xin[t];
+  for (int t = 0; t < TAPS; ++t) {
+    const float x = xin[t];
 #pragma unroll
-      for (int c = 0; c < CO; ++c) acc[c] = fmaf(x, Wf[c * taps + t], acc[c]);
+    for (int c4 = 0; c4 < CO / 4; ++c4) {
+      const float4 w = *reinterpret_cast<const float4*>(wl + t * CO + 4 * c4);
+      acc[4 * c4 + 0] = fmaf(x, w.x, acc[4 * c4 + 0]);
+      acc[4 * c4 + 1] = fmaf(x, w.y, acc[4 * c4 + 1]);
+      acc[4 * c4 + 2] = fmaf(x, w.z, acc[4 * c4 + 2]);
+      acc[4 * c4 + 3] = fmaf(x, w.w, acc[4 * c4 + 3]);
     }
   }
   if (relu) {
@@ -111,16 +118,17 @@ __global__ void __launch_bounds__(256) thin_conv_k(const TIN* X, const float* Wf
 // convT output, CO = convT input channels): y[n, iy, ix] = bias +
 // sum over the class taps (ty, tx) and co of G[n, oy, ox, co] * W[co][ky][kx].
 // blockIdx.y = parity class (a, b); threads walk the class's pixels.
-template <int CO>
+template <int CO, int K, int S>
 __global__ void __launch_bounds__(256) thin_tconv_k(const __bf16* G, const float* Wf, ConvDesc d, const float* bias,
                                                     float* y32, const float* X, __bf16* dlog, float* recon,
                                                     float* part, float* gpart) {
   __shared__ float scratch[16];
+  constexpr int T = K / S;
   const int cls = blockIdx.y;
-  const int ca = cls / d.S, cb = cls - ca * d.S;
-  const int oa = ((ca - d.P) % d.S + d.S) % d.S, ob = ((cb - d.P) % d.S + d.S) % d.S;
-  const int ea = (oa + d.P - ca) / d.S, eb = (ob + d.P - cb) / d.S;
-  const int HS = d.H / d.S, WS = d.W / d.S, T = d.KH / d.S;
+  const int ca = cls / S, cb = cls - ca * S;
+  const int oa = ((ca - d.P) % S + S) % S, ob = ((cb - d.P) % S + S) % S;
+  const int ea = (oa + d.P - ca) / S, eb = (ob + d.P - cb) / S;
+  const int HS = d.H / S, WS = d.W / S;
   const int Mc = d.N * HS * WS;
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = m < Mc;
@@ -128,26 +136,42 @@ __global__ void __launch_bounds__(256) thin_tconv_k(const __bf16* G, const float
   const int n = mm / (HS * WS);
   const int rem = mm - n * HS * WS;
   const int j = rem / WS, i = rem - j * WS;
-  float acc = bias ? bias[0] : 0.f;
-  for (int ty = 0; ty < T; ++ty) {
+  // gather the T*T input rows of CO channels once (16-byte loads)
+  float gv[T * T][CO];
+#pragma unroll
+  for (int ty = 0; ty < T; ++ty)
+#pragma unroll
     for (int tx = 0; tx < T; ++tx) {
       const int oy = j + ea - ty, ox = i + eb - tx;
       const bool ok = live && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
-      const int ky = ca + d.S * ty, kx = cb + d.S * tx;
       const __bf16* g = G + (((size_t)n * d.OH + (ok ? oy : 0)) * d.OW + (ok ? ox : 0)) * CO;
 #pragma unroll
       for (int c8 = 0; c8 < CO / 8; ++c8) {
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(g + 8 * c8);
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const int c = 8 * c8 + jj;
-          const float gv = ok ? (float)v[jj] : 0.f;
-          acc = fmaf(gv, Wf[(c * d.KH + ky) * d.KW + kx], acc);
-        }
+        for (int jj = 0; jj < 8; ++jj) gv[ty * T + tx][8 * c8 + jj] = ok ? (float)v[jj] : 0.f;
       }
     }
+  // this class's T*T taps x CO weights staged in LDS as [tap][co]
+  __shared__ __attribute__((aligned(16))) float wl[T * T * CO];
+  for (int e = threadIdx.x; e < T * T * CO; e += blockDim.x) {
+    const int tp = e / CO, c = e - tp * CO;
+    const int ky = ca + S * (tp / T), kx = cb + S * (tp % T);
+    wl[e] = Wf[(c * K + ky) * K + kx];
   }
-  const int iy = d.S * j + oa, ix = d.S * i + ob;
+  __syncthreads();
+  float acc = bias ? bias[0] : 0.f;
+#pragma unroll
+  for (int tp = 0; tp < T * T; ++tp)
+#pragma unroll
+    for (int c4 = 0; c4 < CO / 4; ++c4) {
+      const float4 w = *reinterpret_cast<const float4*>(wl + tp * CO + 4 * c4);
+      acc = fmaf(gv[tp][4 * c4 + 0], w.x, acc);
+      acc = fmaf(gv[tp][4 * c4 + 1], w.y, acc);
+      acc = fmaf(gv[tp][4 * c4 + 2], w.z, acc);
+      acc = fmaf(gv[tp][4 * c4 + 3], w.w, acc);
+    }
+  const int iy = S * j + oa, ix = S * i + ob;
   const size_t e = ((size_t)n * d.H + iy) * d.W + ix;
   if (live && y32) y32[e] = acc;
   float loss = 0.f, gsum = 0.f;
@@ -184,7 +208,7 @@ extern "C" {
 // conv with a single input channel; x_is_f32 selects f32 / bf16 input.
 int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, const float* bias, int relu, void* y16,
                   const void* omask, float* colsum, hipStream_t s) {
-  if (d.C != 1 || d.KH * d.KW > 16) return 1;
+  if (d.C != 1 || d.KH != 4 || d.KW != 4) return 1;
   const long long M = (long long)d.N * d.OH * d.OW;
   dim3 grid(cdiv_t(M, 256)), blk(256);
   __bf16* y = reinterpret_cast<__bf16*>(y16);
@@ -193,11 +217,11 @@ int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, cons
   {                                                                                                                \
     const size_t sh = colsum ? 256 * (CO_ + 1) * sizeof(float) : 0;                                                \
     if (x_is_f32)                                                                                                  \
-      hipLaunchKernelGGL((thin_conv_k<CO_, float>), grid, blk, sh, s, reinterpret_cast<const float*>(X), Wf, d,   \
+      hipLaunchKernelGGL((thin_conv_k<CO_, 4, float>), grid, blk, sh, s, reinterpret_cast<const float*>(X), Wf, d, \
                          bias, relu, y, mk, colsum);                                                               \
     else                                                                                                           \
-      hipLaunchKernelGGL((thin_conv_k<CO_, __bf16>), grid, blk, sh, s, reinterpret_cast<const __bf16*>(X), Wf, d, \
-                         bias, relu, y, mk, colsum);                                                               \
+      hipLaunchKernelGGL((thin_conv_k<CO_, 4, __bf16>), grid, blk, sh, s, reinterpret_cast<const __bf16*>(X), Wf,  \
+                         d, bias, relu, y, mk, colsum);                                                            \
   }
   switch (d.CO) {
     case 16: THIN(16); break;
@@ -218,16 +242,16 @@ int mdt_thin_blocks(int tconv, ConvDesc d) {
 
 int mdt_thin_tconv(const void* G16, const float* Wf, ConvDesc d, const float* bias, float* y32, const float* X,
                    void* dlog16, float* recon, float* part, float* gpart, hipStream_t s) {
-  if (d.C != 1 || d.KH % d.S || d.KW % d.S || d.H % d.S || d.W % d.S || d.KH != d.KW) return 1;
+  if (d.C != 1 || d.KH != 4 || d.KW != 4 || d.S != 2 || d.H % 2 || d.W % 2) return 1;
   if (X && !part) return 1;
   const long long Mc = (long long)d.N * (d.H / d.S) * (d.W / d.S);
   dim3 grid(cdiv_t(Mc, 256), d.S * d.S), blk(256);
   const __bf16* G = reinterpret_cast<const __bf16*>(G16);
   __bf16* dl = reinterpret_cast<__bf16*>(dlog16);
   switch (d.CO) {
-    case 16: hipLaunchKernelGGL((thin_tconv_k<16>), grid, blk, 0, s, G, Wf, d, bias, y32, X, dl, recon, part, gpart); break;
-    case 32: hipLaunchKernelGGL((thin_tconv_k<32>), grid, blk, 0, s, G, Wf, d, bias, y32, X, dl, recon, part, gpart); break;
-    case 64: hipLaunchKernelGGL((thin_tconv_k<64>), grid, blk, 0, s, G, Wf, d, bias, y32, X, dl, recon, part, gpart); break;
+    case 16: hipLaunchKernelGGL((thin_tconv_k<16, 4, 2>), grid, blk, 0, s, G, Wf, d, bias, y32, X, dl, recon, part, gpart); break;
+    case 32: hipLaunchKernelGGL((thin_tconv_k<32, 4, 2>), grid, blk, 0, s, G, Wf, d, bias, y32, X, dl, recon, part, gpart); break;
+    case 64: hipLaunchKernelGGL((thin_tconv_k<64, 4, 2>), grid, blk, 0, s, G, Wf, d, bias, y32, X, dl, recon, part, gpart); break;
     default: return 2;
   }
   return (int)hipGetLastError();

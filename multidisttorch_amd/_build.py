@@ -88,7 +88,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     host_flags = ["-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                   "-DHIPBLAS_V2", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C",
                   f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-Wno-deprecated-declarations",
-                  "-I" + CSRC, "-I" + pyinc] + ["-I" + p for p in inc]
+                  "-I" + CSRC, "-I" + pyinc] + ["-I" + p for p in inc] + ["-I" + os.path.join(ROCM, "include")]
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     jobsl = []
     for s in kern:
@@ -113,7 +113,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
         link = ["g++", "-shared", "-o", OUT + ".tmp"] + objs + [
             "-L" + tlib, "-Wl,-rpath," + tlib,
             "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
-            "-lamdhip64"]
+            "-lamdhip64", "-lrccl"]  # torch's bundled librccl: the same runtime ProcessGroupNCCL uses
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(link)}\n{r.stdout}\n{r.stderr}")

@@ -13,14 +13,17 @@ MI355X-first design:
     ~153 GB/s link per GPU, so per-bucket time is alpha + 2(s-1)/s * bytes/BW;
     buckets are sized so each one's transfer hides behind the backward compute
     that follows it, and tiny models get 1-2 buckets (latency-bound regime);
-  * the collectives are issued by the native C++ ``BucketReducer`` (csrc/
-    runtime/reducer.cpp) on the c10d process group of the trial: RCCL on GPU
-    (own stream, AVG as pre-mul-sum, graph-capturable), gloo on CPU tests.
+  * the collectives are issued natively: on GPU by ``RcclBucketReducer``
+    (csrc/runtime/xgmi_comm.cpp) directly on the trial group's RCCL
+    communicator (PreMulSum(1/s) averaging, high-priority comm stream, event
+    fences, graph-capturable); on gloo (CPU tests) by the c10d-based
+    ``BucketReducer`` (csrc/runtime/reducer.cpp).
 """
 
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Iterable, List, Optional, Sequence
 
 import torch
@@ -30,7 +33,7 @@ from torch import nn
 from ..ops import native
 
 __all__ = ["XgmiModel", "plan_buckets", "make_arena_reducer", "PyBucketReducer", "ArenaDDP",
-           "broadcast_params"]
+           "broadcast_params", "rccl_comm_ptr", "reducer_kind"]
 
 
 class XgmiModel:
@@ -148,12 +151,52 @@ class PyBucketReducer:
         return self._launched
 
 
+def rccl_comm_ptr(pg, device: torch.device) -> int:
+    """ncclComm_t (as int) of a trial group's ProcessGroupNCCL on `device`.
+
+    torch creates RCCL communicators lazily; one tiny all-reduce forces the
+    communicator into existence so the native reducer can reuse it (one
+    communicator and one RCCL runtime per group, shared with c10d)."""
+    backend = pg._get_backend(device)
+    if not hasattr(backend, "_comm_ptr"):
+        raise RuntimeError(f"process group backend {type(backend).__name__} is not RCCL")
+    t = torch.zeros(1, device=device)
+    dist.all_reduce(t, group=pg)
+    torch.cuda.current_stream(device).synchronize()
+    return int(backend._comm_ptr())
+
+
+def reducer_kind(pg, flat: torch.Tensor) -> str:
+    """'rccl' (direct RCCL on torch's communicator), 'c10d' (native reducer over
+    the ProcessGroup) or 'python'. MDT_REDUCER overrides the choice."""
+    forced = os.getenv("MDT_REDUCER", "")
+    if forced:
+        return forced
+    if not native.available():
+        return "python"
+    if flat.is_cuda and dist.get_backend(pg) == "nccl":
+        return "rccl"
+    return "c10d"
+
+
 def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: bool = True,
-                       prefer_native: bool = True):
+                       prefer_native: bool = True, kind: Optional[str] = None):
+    """Bucket reducer over a flat gradient arena ([begin, end) buckets).
+
+    On MI355X trial groups (RCCL) this is the direct-RCCL reducer of
+    csrc/runtime/xgmi_comm.cpp: PreMulSum(1/s) averaging fused into the
+    collective, a dedicated high-priority comm stream, event fences only.
+    gloo groups (CPU tests, control plane) use the c10d-based native reducer.
+    """
     if pg is None:
         pg = dist.distributed_c10d._get_default_group()
-    if prefer_native and native.available():
-        return native.require().BucketReducer(pg, flat, [int(b) for b in bounds], average)
+    kind = kind or (reducer_kind(pg, flat) if prefer_native else "python")
+    b = [int(x) for x in bounds]
+    if kind == "rccl":
+        size = dist.get_world_size(pg)
+        return native.require().RcclBucketReducer(rccl_comm_ptr(pg, flat.device), size, flat, b, average)
+    if kind == "c10d" and native.available():
+        return native.require().BucketReducer(pg, flat, b, average)
     if flat.is_cuda:
         native.require()  # on GPU the native reducer is mandatory: fail loudly
     return PyBucketReducer(pg, flat, bounds, average)
