@@ -51,6 +51,7 @@ def main(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--backend", default=None, help="hip|torch (default: hip on GPU)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--bucket-mb", default=None, help="intra-group buckets: MiB cap, 0 = one bucket")
     a = ap.parse_args(argv)
 
     from multidisttorch_amd.runtime import setup_ddp, global_barrier, control_group
@@ -89,7 +90,9 @@ def main(argv=None):
         # replicas of a group start from group rank 0's weights (DDP broadcast)
         if n_per > 1:
             dist.broadcast(trainer.params, src=dist.get_global_rank(pg, 0), group=pg)
-            trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, [0, trainer.split, trainer.numel]))
+            trainer.refresh_weights()
+            mb = None if a.bucket_mb in (None, "") else float(a.bucket_mb)
+            trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, trainer.bucket_bounds(mb)))
         img = 28 if a.model in ("mlp", "conv28") else 128
         train = mnist_like(True, synthetic=True, device=dev, size=img,
                            n=None if img == 28 else 4096 * max(1, a.batch_size // 32))

@@ -34,6 +34,7 @@ from ..ckpt import checkpoint as ckpt
 from ..data.sampler import shard_indices
 from ..obs.metrics import TrialMetrics
 from ..obs import trace
+from ..parallel.autotune import autotune_buckets
 from ..parallel.ddp import broadcast_params, make_arena_reducer
 from ..parallel.groups import print0
 from ..runtime.bootstrap import bound_device, global_barrier
@@ -64,6 +65,7 @@ class RunOptions:
     image_size: int = 28
     data_dir: str = "data"
     synthetic: Optional[bool] = True
+    bucket_mb: Optional[object] = None     # None: model default; 0: one bucket; float: MiB cap; "auto": measured
 
 
 @dataclass
@@ -168,7 +170,16 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
     if gsize > 1:
         # DDP's _sync_module_states: replicas start from group rank 0's weights
         broadcast_params([trainer.params], group)
-        trainer.attach_reducer(make_arena_reducer(group, trainer.grads, [0, trainer.split, trainer.numel]))
+        trainer.refresh_weights()
+        if opts.bucket_mb == "auto":
+            idx0 = shard_indices(len(train), K, spec.group_id)
+            key = f"{opts.model}-{opts.image_size}-b{opts.batch_size}-n{trainer.numel}-s{gsize}"
+            bounds, timings = autotune_buckets(lambda: _make_trainer(spec, opts, device, grank, D), group,
+                                               train.data, idx0, key=key)
+            print0(f"bucket autotune (group of {gsize}): {timings} -> {bounds}", process_group=group)
+        else:
+            bounds = trainer.bucket_bounds(opts.bucket_mb)
+        trainer.attach_reducer(make_arena_reducer(group, trainer.grads, bounds))
     start_epoch = 1
     if opts.ckpt_dir and opts.resume:
         prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer)
@@ -177,6 +188,7 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
             print0(f"resumed trial {spec.group_id} from {prog['path']} (epoch {prog['epoch']})", process_group=group)
         if gsize > 1:
             broadcast_params([trainer.params, trainer.exp_avg, trainer.exp_avg_sq], group)
+            trainer.refresh_weights()
     metrics = TrialMetrics(opts.metrics_dir, spec.group_id, enabled=(grank == 0))
 
     # Parity with the reference's download barrier (vae-hpo.py:133-144).

@@ -217,7 +217,8 @@ class ConvVaeTrainer:
         self.decoupled_wd = decoupled_wd
         self.spec = conv_vae_spec(image, channels, z)
         self.layout, self.numel = conv_layout(self.spec)
-        self.split = self.layout[-2][1] if len(self.layout) >= 2 else 0
+        # first decoder parameter: the default bucket boundary (decoder grads are ready first)
+        self.split = next(o for n, o, _ in self.layout if n.startswith("dec"))
         self.use_graphs = use_graphs and backend == "hip"
         self.graph_steps = max(1, graph_steps)
         self._graphs = {}
@@ -331,8 +332,52 @@ class ConvVaeTrainer:
         self._graphs.clear()
 
     def attach_reducer(self, reducer):
+        """Reducer over ``self.grads`` whose bucket bounds fall on layer starts
+        (see ``bucket_bounds``); buckets launch as their layers' backward ends."""
         self.reducer = reducer
         self._graphs.clear()
+
+    def layer_ranges(self):
+        """[(layer, begin, end)] arena range of each layer's (weight, bias)."""
+        lay = {n: (o, s) for n, o, s in self.layout}
+        out = []
+        for l in self.spec:
+            b = lay[l.name + ".weight"][0]
+            ob, sb = lay[l.name + ".bias"]
+            out.append((l, b, ob + sb[0]))
+        return out
+
+    def bucket_bounds(self, bucket_mb=None):
+        """Bucket bounds in gradient-ready (reverse-layer) order, closed at layer
+        boundaries once a bucket holds >= bucket_mb MiB of f32 gradients.
+        None -> two buckets (decoder | encoder); 0 -> one bucket."""
+        ranges = self.layer_ranges()
+        if bucket_mb == 0:
+            return [0, self.numel]
+        if bucket_mb is None:
+            dec0 = next(b for l, b, e in ranges if l.name.startswith("dec"))
+            return [0, dec0, self.numel]
+        cap = float(bucket_mb) * (1 << 20)
+        bounds, acc = [self.numel], 0.0
+        for l, b, e in reversed(ranges):
+            acc += 4.0 * (e - b)
+            if acc >= cap and b > 0:
+                bounds.append(b)
+                acc = 0.0
+        bounds.append(0)
+        return sorted(set(bounds))
+
+    def default_bucket_bounds(self):
+        return self.bucket_bounds(None)
+
+    @torch.no_grad()
+    def refresh_weights(self):
+        """Re-derive the bf16 compute copies after ``params`` changed outside a
+        step (replica broadcast, checkpoint load)."""
+        if self.backend == "hip":
+            self._cast_weights()
+        else:
+            self.model.from_arena(self.named_parameters())
 
     # ----------------------------------------------------------- HIP path
     def _alloc_hip(self):
@@ -475,8 +520,10 @@ class ConvVaeTrainer:
         else:
             raise NotImplementedError("conv-VAE HIP path: multi-channel images need the per-channel dlogits sum")
         segs = self._seg_rows(slabs)
-        units = []
+        units, layer_units = [], []
         for si, (off, numel, ptr, ns, *_rest) in enumerate(segs):
+            if si % 2 == 0:
+                layer_units.append(len(units))
             rp = 1
             if ptr:
                 while rp < 512 and rp * 16 < ns:
@@ -484,9 +531,10 @@ class ConvVaeTrainer:
             cnt = 512 // rp
             for st in range(0, numel, cnt):
                 units.append([si, st, min(cnt, numel - st)])
+        layer_units.append(len(units))  # layer i owns units [layer_units[i], layer_units[i+1])
         p = dict(slabs=slabs, colsum=colsum, gpart=gpart, ws=torch.empty(max(ws_need, 1), **f32), rows_per=rows_per,
                  segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
-                 nunits=len(units))
+                 nunits=len(units), layer_units=layer_units)
         self._plans[M] = p
         return p
 
@@ -570,7 +618,14 @@ class ConvVaeTrainer:
         p = self._plan(M)
         spec = self.spec
         g = self.dlog16
+        red = self.reducer
+        if red is not None:
+            bounds = list(red.bounds())
+            starts = {b: i for i, (l, b, e) in enumerate(self.layer_ranges())}
+            assert all(b in starts or b == self.numel for b in bounds), "bucket bounds must fall on layer starts"
         for i in range(len(spec) - 1, -1, -1):
+            if red is not None and i + 1 < len(spec):
+                self._maybe_launch_bucket(red, bounds, starts, i + 1, M)
             l = spec[i]
             prev = spec[i - 1] if i > 0 else None
             d = self._desc(l, M)
@@ -587,6 +642,8 @@ class ConvVaeTrainer:
             else:
                 C.wgrad(g, a_in, d, wout)
             if prev is None:
+                if red is not None:
+                    self._maybe_launch_bucket(red, bounds, starts, 0, M)
                 break
             omask = a_in if prev.relu else None
             if l.name == "dec_fc":
@@ -606,6 +663,23 @@ class ConvVaeTrainer:
                     C.colsum(gin, M, prev.cout, p["rows_per"], p["colsum"][prev.name])
             g = gin
 
+    def _maybe_launch_bucket(self, red, bounds, starts, i, M):
+        """Layer i's gradients just became final (all layers >= i are done): if
+        i starts a bucket, reduce that bucket's partial slabs into the arena and
+        launch its all-reduce (it overlaps the rest of the backward)."""
+        _, b, _ = self.layer_ranges()[i]
+        if b not in bounds[:-1]:
+            return
+        k = bounds.index(b)
+        end = bounds[k + 1]
+        last = next((j for j, (l, bb, e) in enumerate(self.layer_ranges()) if bb >= end), len(self.spec))
+        p, st = self._plan(M), self.state
+        u0, u1 = p["layer_units"][i], p["layer_units"][last]
+        units = p["units"].narrow(0, u0 * 12, (u1 - u0) * 12)
+        self.C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], units,
+                             u1 - u0, st.train_state, st.hparams, False)
+        red.launch(k)
+
     def _step_hip(self, M):
         C = self.C
         X, idx = self._data[0], self._data[1]
@@ -615,10 +689,8 @@ class ConvVaeTrainer:
         self._forward_hip(M, st.train_state, self.rng_stream)
         C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, -(-M * self.Z // 256),
                          st.train_state, st.hparams, True)
-        self._backward_hip(M)
+        self._backward_hip(M)  # with a reducer: finalizes + launches each bucket as it completes
         if self.reducer is not None:
-            self._finalize_grads(M, False)
-            self.reducer.launch_all()
             self.reducer.wait_all()
             C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
                         st.train_state, st.hparams, True)

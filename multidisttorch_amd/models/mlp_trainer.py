@@ -179,20 +179,37 @@ class MlpVaeTrainer:
 
     # ------------------------------------------------------------------ step
     def attach_reducer(self, reducer):
-        """BucketReducer over ``self.grads`` with bounds [0, split, numel]."""
+        """BucketReducer over ``self.grads`` with bounds [0, split, numel] (fc4
+        first, overlapping the rest of the backward) or [0, numel]."""
         self.reducer = reducer
         self._graphs.clear()
+
+    def bucket_bounds(self, bucket_mb=None):
+        """The fused step finishes gradients in two groups (fc4 after B1, the
+        rest after B3): two buckets, or one when bucket_mb == 0."""
+        return [0, self.numel] if bucket_mb == 0 else [0, self.split, self.numel]
+
+    def default_bucket_bounds(self):
+        return self.bucket_bounds(None)
+
+    def refresh_weights(self):
+        """Params are the compute weights here (fp32 views): nothing to re-derive."""
 
     def _step_hip(self, M: int):
         X, idx = self._data[0], self._data[1]
         e = self.engine
         e.forward(X, idx, M, True, False, self.rng_stream, False)
-        if self.reducer is not None:
+        if self.reducer is not None and self.reducer.num_buckets() == 2:
             e.backward(X, idx, M, 1, False)
             self.reducer.launch(1)          # fc4 bucket: overlaps B2/B3
             e.backward(X, idx, M, 2, False)
             e.backward(X, idx, M, 3, False)
             self.reducer.launch(0)
+            self.reducer.wait_all()
+            e.adam()
+        elif self.reducer is not None:      # single bucket after the whole backward
+            e.backward(X, idx, M, 0, False)
+            self.reducer.launch_all()
             self.reducer.wait_all()
             e.adam()
         else:

@@ -103,11 +103,19 @@ def setup_ddp_groups(num_groups: int, verbose: bool = True, backend: Optional[st
 
     from ..runtime.faults import group_timeout_s
 
+    from ..runtime.bootstrap import bound_device, world_is_device_bound
+
+    # On an eager, device-bound RCCL world, passing device_id makes torch
+    # derive each trial communicator with ncclCommSplit from the world
+    # communicator (every rank takes part; non-members split with NOCOLOR).
+    split = backend in (None, "nccl") and world_is_device_bound()
     for g in range(num_groups):
         # bounded collective timeout: a dead replica fails its group fast
         kw = {"ranks": plan.ranks(g), "timeout": _dt.timedelta(seconds=group_timeout_s())}
         if backend is not None:
             kw["backend"] = backend
+        if split:
+            kw["device_id"] = bound_device()
         handles.append(dist.new_group(**kw))
     for g in range(num_groups):
         if dist.get_rank(handles[g]) >= 0:

@@ -58,6 +58,20 @@ def get_comm_size_and_rank():
     return 1, 0
 
 
+def eager_comm_requested() -> bool:
+    """MDT_EAGER_COMM=1: bind the world communicator to the local device at
+    init (eager RCCL world) so trial groups are split from it (ncclCommSplit)
+    instead of being bootstrapped from scratch at their first collective."""
+    return os.getenv("MDT_EAGER_COMM", "0") == "1"
+
+
+def world_is_device_bound() -> bool:
+    """True when the default group is an eagerly initialised, device-bound RCCL world."""
+    if not dist.is_initialized() or dist.get_backend() != "nccl":
+        return False
+    return getattr(dist.distributed_c10d._get_default_group(), "bound_device_id", None) is not None
+
+
 def bound_device() -> torch.device:
     """Device this process computes on (``cuda:<local_rank>`` or ``cpu``)."""
     if _STATE["device"] is not None:
@@ -113,8 +127,7 @@ def setup_ddp(backend: Optional[str] = None, verbose: bool = True,
         kwargs = {}
         if timeout_s is not None:
             kwargs["timeout"] = _dt.timedelta(seconds=timeout_s)
-        if (backend == "nccl" and os.getenv("MDT_EAGER_COMM", "0") == "1"
-                and _STATE["device"].type == "cuda"):
+        if backend == "nccl" and eager_comm_requested() and _STATE["device"].type == "cuda":
             kwargs["device_id"] = _STATE["device"]
         dist.init_process_group(backend=backend, init_method="env://",
                                 world_size=world_size, rank=world_rank, **kwargs)

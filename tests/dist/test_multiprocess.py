@@ -84,6 +84,21 @@ def test_trainer_replicas_stay_in_sync():
         assert r["maxdiff"] == 0.0 and r["step"] == 5
 
 
+def test_bucket_autotune_agrees_across_group(tmp_path):
+    old = dict(ENV)
+    ENV["MDT_BUCKET_CACHE"] = str(tmp_path / "buckets.json")
+    try:
+        rc, outs = _run([WORKER, "autotune"], 2)
+    finally:
+        ENV.clear()
+        ENV.update(old)
+    assert rc == 0, "\n".join(outs)
+    res = _results(outs)
+    assert len(res) == 2 and res[0]["best"] == res[1]["best"]
+    assert res[0]["n"] == 3 and res[0]["cached"]
+    assert all(r["maxdiff"] == 0.0 for r in res)
+
+
 def test_example_subgroup_world4(tmp_path):
     old = dict(ENV)
     ENV["MDT_EXAMPLE_WORLD"] = "4"

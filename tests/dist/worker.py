@@ -123,6 +123,37 @@ def mode_trainer_ddp():
     dist.destroy_process_group()
 
 
+def mode_autotune():
+    """Bucket autotune over a group of 2 (gloo, CPU): both members must pick
+    the same layout; conv-VAE replicas with per-layer buckets stay in sync."""
+    from multidisttorch_amd.runtime.bootstrap import setup_ddp
+    from multidisttorch_amd.parallel.autotune import autotune_buckets
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer, broadcast_params
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    ws, wr = setup_ddp(verbose=False)
+    pg = dist.new_group(list(range(ws)))
+    X = torch.rand(64, 784, generator=torch.Generator().manual_seed(4))
+    idx = torch.arange(64, dtype=torch.int32)
+    make = lambda: ConvVaeTrainer(batch_size=16, image=28, backend="torch", seed=1, rng_stream=wr)
+    cache = os.environ["MDT_BUCKET_CACHE"]
+    best, timings = autotune_buckets(make, pg, X, idx, candidates=(None, 0, 0.05), steps=2, warmup=1,
+                                     key="test-key", cache=cache)
+    tr = make()
+    broadcast_params([tr.params], pg)
+    tr.refresh_weights()
+    tr.attach_reducer(make_arena_reducer(pg, tr.grads, best))
+    tr.bind_train_data(X, idx)
+    tr.set_cursor(0, 4)
+    tr.train_steps(3)
+    p = tr.params.clone()
+    allp = [torch.zeros_like(p) for _ in range(ws)]
+    dist.all_gather(allp, p)
+    out(rank=wr, best=best, n=len(timings), maxdiff=float(max((a - allp[0]).abs().max() for a in allp)),
+        cached=os.path.exists(cache))
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
     mode = sys.argv[1]
     if mode == "groups":
@@ -133,5 +164,7 @@ if __name__ == "__main__":
         mode_arena_ddp()
     elif mode == "trainer_ddp":
         mode_trainer_ddp()
+    elif mode == "autotune":
+        mode_autotune()
     else:
         raise SystemExit(f"unknown mode {mode}")

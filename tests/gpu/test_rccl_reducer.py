@@ -105,3 +105,22 @@ def test_mlp_trainer_with_rccl_reducer(nccl_world, native_ext):
     # one rank: the all-reduce is an identity, only the Adam path differs
     # (separate flat Adam instead of the fused epilogue) -> same losses
     np.testing.assert_allclose(hist[0], hist[1], rtol=1e-5)
+
+
+def test_trial_groups_split_from_device_bound_world(nccl_world, native_ext):
+    """Eager device-bound world -> trial communicators via ncclCommSplit; the
+    direct-RCCL reducer then runs on the split communicator."""
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+    from multidisttorch_amd.parallel.groups import setup_ddp_groups
+    from multidisttorch_amd.runtime.bootstrap import world_is_device_bound
+
+    assert world_is_device_bound()
+    (pg,) = setup_ddp_groups(1, verbose=False)
+    assert dist.get_rank(pg) == 0
+    flat = torch.randn(4096, device="cuda")
+    ref = flat.clone()
+    red = make_arena_reducer(pg, flat, [0, 1024, 4096])
+    red.launch_all()
+    red.wait_all()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(flat, ref)

@@ -44,3 +44,17 @@ def test_torch_backend_trains():
     total, first = tr.evaluate(X.float(), torch.arange(40, dtype=torch.int32))
     assert first.shape == (32, 784) and np.isfinite(total)
     assert tr.decode(torch.randn(4, 32)).shape == (4, 784)
+
+
+def test_conv_bucket_bounds_fall_on_layer_starts():
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    tr = ConvVaeTrainer(batch_size=4, image=128, z=64, backend="torch", seed=0)
+    starts = {b for _, b, _ in tr.layer_ranges()}
+    assert tr.bucket_bounds(None) == [0, tr.split, tr.numel]
+    assert tr.bucket_bounds(0) == [0, tr.numel]
+    for mb in (0.5, 2, 8):
+        b = tr.bucket_bounds(mb)
+        assert b[0] == 0 and b[-1] == tr.numel and b == sorted(b)
+        assert all(x in starts for x in b[:-1])
+    assert len(tr.bucket_bounds(0.5)) > len(tr.bucket_bounds(8)) >= 2

@@ -9,7 +9,7 @@ epochs). Launch one process per GPU with any launcher the reference supports
 
 Extensions (opt-in, default output unchanged): ``--lr`` / ``--beta`` (scalar or
 comma list, one per trial), ``--seed``, ``--ckpt-dir`` + ``--resume``,
-``--metrics-dir`` (JSONL + aggregate samples/s), ``--per-group-results``,
+``--metrics-dir`` (JSONL + aggregate samples/s), ``--per-group-results``, ``--bucket-mb``,
 ``--no-graphs``, ``--backend {hip,torch}``, ``--synthetic/--real-data``.
 """
 
@@ -25,6 +25,7 @@ from utils import *  # noqa: F401,F403  (reference-compatible API + re-exports)
 
 from multidisttorch_amd.hpo.runner import RunOptions, idle_rank, run_trial
 from multidisttorch_amd.hpo.trial import build_specs, parse_list
+from multidisttorch_amd.parallel.autotune import parse_bucket_mb
 from multidisttorch_amd.runtime.bootstrap import control_group
 
 
@@ -56,6 +57,8 @@ def parse_args(argv=None):
     parser.add_argument("--model", type=str, default="mlp", choices=["mlp", "conv"],
                         help="mlp = reference MLP-VAE (fp32); conv = bf16 conv/deconv VAE")
     parser.add_argument("--image-size", type=int, default=28, choices=[28, 128])
+    parser.add_argument("--bucket-mb", type=str, default=None,
+                        help="intra-group all-reduce buckets: MiB cap, 0 = one bucket, 'auto' = measured")
     return parser.parse_args(argv)
 
 
@@ -74,7 +77,7 @@ def main(argv=None):
                       results=not args.no_results, per_group_results=args.per_group_results,
                       train_samples=args.train_samples, test_samples=args.test_samples,
                       data_dir=args.data_dir, synthetic=False if args.real_data else True,
-                      model=args.model, image_size=args.image_size)
+                      model=args.model, image_size=args.image_size, bucket_mb=parse_bucket_mb(args.bucket_mb))
     results = []
     member = False
     for group_id, group in enumerate(processes_groups):
