@@ -52,6 +52,9 @@ def main(argv=None):
     ap.add_argument("--backend", default=None, help="hip|torch (default: hip on GPU)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--bucket-mb", default=None, help="intra-group buckets: MiB cap, 0 = one bucket")
+    ap.add_argument("--trials-per-gpu", type=int, default=1,
+                    help="trial packing: T concurrent trials per single-rank group (one HIP stream each); "
+                         "the headline config is T=1 (K = N trials)")
     a = ap.parse_args(argv)
 
     from multidisttorch_amd.runtime import setup_ddp, global_barrier, control_group
@@ -69,45 +72,69 @@ def main(argv=None):
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     n_per = world // K
     gid = rank // n_per if rank < K * n_per else None
-    specs = default_sweep(K)
 
-    trainer = None
+
+    T = max(1, a.trials_per_gpu)
+    if T > 1 and n_per != 1:
+        raise SystemExit("--trials-per-gpu > 1 needs single-rank groups (no intra-group all-reduce)")
+    specs = default_sweep(K * T)
+
+    def make_trainer(spec, grank):
+        if a.model == "mlp":
+            return MlpVaeTrainer(batch_size=a.batch_size, device=dev, backend=a.backend,
+                                 seed=spec.seed, lr=spec.lr, kl_beta=spec.beta, rng_stream=grank,
+                                 use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
+        from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+        im = 28 if a.model == "conv28" else 128
+        return ConvVaeTrainer(batch_size=a.batch_size, image=im, z=32 if im == 28 else 64, device=dev,
+                              backend=a.backend, seed=spec.seed, lr=spec.lr, kl_beta=spec.beta,
+                              rng_stream=grank, use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
+
+    trainers, streams = [], []
+    img = 28 if a.model in ("mlp", "conv28") else 128
     if gid is not None:
         pg = handles[gid]
         grank = dist.get_rank(pg)
-        spec = specs[gid]
-        if a.model == "mlp":
-            trainer = MlpVaeTrainer(batch_size=a.batch_size, device=dev, backend=a.backend,
-                                    seed=spec.seed, lr=spec.lr, kl_beta=spec.beta, rng_stream=grank,
-                                    use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
-        else:
-            from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
-
-            img = 28 if a.model == "conv28" else 128
-            trainer = ConvVaeTrainer(batch_size=a.batch_size, image=img, z=32 if img == 28 else 64, device=dev,
-                                     backend=a.backend, seed=spec.seed, lr=spec.lr, kl_beta=spec.beta,
-                                     rng_stream=grank, use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
-        # replicas of a group start from group rank 0's weights (DDP broadcast)
-        if n_per > 1:
-            dist.broadcast(trainer.params, src=dist.get_global_rank(pg, 0), group=pg)
-            trainer.refresh_weights()
-            mb = None if a.bucket_mb in (None, "") else float(a.bucket_mb)
-            trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, trainer.bucket_bounds(mb)))
-        img = 28 if a.model in ("mlp", "conv28") else 128
         train = mnist_like(True, synthetic=True, device=dev, size=img,
                            n=None if img == 28 else 4096 * max(1, a.batch_size // 32))
-        idx = shard_indices(len(train), K, gid)
-        trainer.bind_train_data(train.data, idx)
-        trainer.set_cursor(0, idx.numel() // a.batch_size)  # full batches only
-        trainer.train_steps(a.warmup)
+        for t in range(T):
+            tid = gid * T + t
+            trainer = make_trainer(specs[tid], grank)
+            # replicas of a group start from group rank 0's weights (DDP broadcast)
+            if n_per > 1:
+                dist.broadcast(trainer.params, src=dist.get_global_rank(pg, 0), group=pg)
+                trainer.refresh_weights()
+                mb = None if a.bucket_mb in (None, "") else float(a.bucket_mb)
+                trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, trainer.bucket_bounds(mb)))
+            idx = shard_indices(len(train), K * T, tid)
+            trainer.bind_train_data(train.data, idx)
+            trainer.set_cursor(0, idx.numel() // a.batch_size)  # full batches only
+            s = torch.cuda.Stream(dev) if (T > 1 and dev.type == "cuda") else None
+            if s is not None:
+                with torch.cuda.stream(s):
+                    trainer.train_steps(a.warmup)
+            else:
+                trainer.train_steps(a.warmup)
+            trainers.append(trainer)
+            streams.append(s)
+    trainer = trainers[0] if trainers else None
+
+    def run_all(n):
+        for tr, s in zip(trainers, streams):
+            if s is not None:
+                with torch.cuda.stream(s):
+                    tr.train_steps(n)
+            else:
+                tr.train_steps(n)
+
     if dev.type == "cuda":
         torch.cuda.synchronize()
     global_barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if trainer is not None:
-        trainer.train_steps(a.steps)
+    run_all(a.steps)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     global_barrier()
@@ -118,15 +145,15 @@ def main(argv=None):
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctrl)
         dt = float(t.item())
-    samples = K * a.batch_size * a.steps
+    samples = K * T * a.batch_size * a.steps
     value = samples / dt
     # sanity: training actually progressed and the loss is finite
     ok = True
-    if trainer is not None:
-        st = trainer.read_state()
-        hist = trainer.loss_history()
+    for tr in trainers:
+        st = tr.read_state()
+        hist = tr.loss_history()
         last = float(hist[(st["step"] - 1) % len(hist)])
-        ok = st["step"] == a.warmup + a.steps and last == last and last < 1e9
+        ok = ok and st["step"] == a.warmup + a.steps and last == last and last < 1e9
     flag = torch.tensor([1.0 if ok else 0.0])
     if world > 1:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ctrl)
@@ -141,7 +168,7 @@ def main(argv=None):
             "ms_per_step": round(dt / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / (REF_SAMPLES_PER_S_PER_TRIAL * K), 2),
+            "vs_baseline": round(value / (REF_SAMPLES_PER_S_PER_TRIAL * K * T), 2),
             "dtype": "fp32" if a.model == "mlp" else "bf16",
             "data": ("synthetic (MNIST-shaped 60000x1x28x28, random-init weights)" if a.model != "conv128"
                      else "synthetic (1x128x128 images, random-init weights)"),
@@ -149,12 +176,12 @@ def main(argv=None):
                 "model": {"mlp": "MLP-VAE 784-400-20 (reference vae-hpo.py topology)",
                           "conv28": "conv-VAE 28x28 (2 conv + 2 deconv, z=32)",
                           "conv128": "conv-VAE 128x128 (4 conv + 4 deconv, z=64)"}[a.model],
-                "global_batch": a.batch_size * K,
+                "global_batch": a.batch_size * K * T,
                 "per_trial_batch": a.batch_size,
                 "seq_len": None,
                 "image": img,
-                "parallelism": f"groups{K}x{n_per}",
-                "trials": K,
+                "parallelism": f"groups{K}x{n_per}" + (f"+pack{T}" if T > 1 else ""),
+                "trials": K * T,
                 "backend": trainer.backend if trainer is not None else None,
                 "graphs": (not a.no_graphs),
                 "valid": bool(flag.item() > 0),

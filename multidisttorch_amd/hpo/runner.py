@@ -42,7 +42,7 @@ from ..runtime.faults import guarded, maybe_inject
 from ..utils.images import save_image
 from .trial import TrialSpec
 
-__all__ = ["RunOptions", "TrialResult", "run_trial", "idle_rank"]
+__all__ = ["RunOptions", "TrialResult", "run_trial", "run_packed_trials", "idle_rank"]
 
 
 @dataclass
@@ -115,7 +115,9 @@ def _load_data(opts: RunOptions, device):
     return train, test
 
 
-def _train_epoch(trainer, epoch: int, n_shard: int, n_dataset: int, opts: RunOptions, group) -> float:
+def _launch_epoch(trainer, epoch: int, n_shard: int, opts: RunOptions) -> int:
+    """Enqueue one epoch of steps on the current stream (no host sync); returns
+    the step counter before the epoch."""
     B = opts.batch_size
     full, tail = n_shard // B, n_shard % B
     nb = full + (1 if tail else 0)
@@ -126,20 +128,32 @@ def _train_epoch(trainer, epoch: int, n_shard: int, n_dataset: int, opts: RunOpt
         trainer.train_steps(full, B)
         if tail:
             trainer.train_steps(1, tail)
+    return step0
+
+
+def _train_epoch(trainer, epoch: int, n_shard: int, n_dataset: int, opts: RunOptions, group,
+                 step0: Optional[int] = None, tag: str = "") -> float:
+    B = opts.batch_size
+    full, tail = n_shard // B, n_shard % B
+    nb = full + (1 if tail else 0)
+    if step0 is None:
+        step0 = _launch_epoch(trainer, epoch, n_shard, opts)
     hist = trainer.loss_history()
     st = trainer.read_state()
     if not opts.quiet_train_log:
         for batch_idx in range(0, nb, opts.log_interval):
             bsz = B if batch_idx < full else tail
             loss_b = float(hist[(step0 + batch_idx) % len(hist)])
-            print0("Train Epoch: {} [{}/{} ({:.0f}%)]\tLoss: {:.6f}".format(
+            print0(tag + "Train Epoch: {} [{}/{} ({:.0f}%)]\tLoss: {:.6f}".format(
                 epoch, batch_idx * bsz, n_dataset, 100.0 * batch_idx / nb, loss_b / bsz), process_group=group)
     # The reference divides by the FULL dataset size, not the shard (Q6).
-    print0("====> Epoch: {} Average loss: {:.4f}".format(epoch, st["epoch_loss"] / n_dataset), process_group=group)
+    print0(tag + "====> Epoch: {} Average loss: {:.4f}".format(epoch, st["epoch_loss"] / n_dataset),
+           process_group=group)
     return st["epoch_loss"]
 
 
-def _test_epoch(trainer, epoch: int, test, opts: RunOptions, group, rdir: Optional[str], shape) -> float:
+def _test_epoch(trainer, epoch: int, test, opts: RunOptions, group, rdir: Optional[str], shape,
+                tag: str = "") -> float:
     idx = torch.arange(len(test), dtype=torch.int32, device=test.data.device)
     with trace.range(f"test_epoch_{epoch}"):
         total, first = trainer.evaluate(test.data, idx, want_first_recon=rdir is not None)
@@ -151,7 +165,7 @@ def _test_epoch(trainer, epoch: int, test, opts: RunOptions, group, rdir: Option
         os.makedirs(rdir, exist_ok=True)
         save_image(comparison, f"{rdir}/reconstruction_" + str(epoch) + ".png", nrow=n)
     test_loss = total / len(test)
-    print0("====> Test set loss: {:.4f}".format(test_loss), process_group=group)
+    print0(tag + "====> Test set loss: {:.4f}".format(test_loss), process_group=group)
     return test_loss
 
 
@@ -224,13 +238,15 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
                        train_loss / len(train), test_loss, failed=bool(failure), error=failure.get("error", ""))
 
 
-def _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape, gen, device, spec, grank, metrics):
+def _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape, gen, device, spec, grank, metrics,
+               step0=None, t_train=None, tag=""):
     te = time.perf_counter()
-    train_loss = _train_epoch(trainer, epoch, n_shard, len(train), opts, group)
-    t_train = time.perf_counter() - te
+    train_loss = _train_epoch(trainer, epoch, n_shard, len(train), opts, group, step0=step0, tag=tag)
+    if t_train is None:
+        t_train = time.perf_counter() - te
     test_loss = float("nan")
     if opts.eval_each_epoch:
-        test_loss = _test_epoch(trainer, epoch, test, opts, group, rdir, shape)
+        test_loss = _test_epoch(trainer, epoch, test, opts, group, rdir, shape, tag=tag)
     if rdir is not None:
         with torch.no_grad():
             sample = torch.randn(64, trainer.Z, generator=gen).to(device)
@@ -243,6 +259,80 @@ def _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape, g
                 test_loss=test_loss, epoch_train_s=t_train, samples=n_shard,
                 train_samples_per_s=n_shard / max(t_train, 1e-9), lr=spec.lr, beta=spec.beta)
     return train_loss, test_loss
+
+
+def run_packed_trials(specs, group, opts: RunOptions, data=None, num_trials: Optional[int] = None):
+    """Train several trials concurrently on this rank's GPU (trial packing).
+
+    MI355X-first extension (no reference counterpart): one small VAE step
+    fills only part of the 256 CUs, so T trials of a size-1 group each get a
+    HIP stream and their captured step graphs are replayed concurrently
+    (measured 1.6-1.8x aggregate throughput at T = 2, profiles/r1_packing).
+    Per epoch: every live trial's steps are enqueued on its stream, one
+    device sync, then per-trial logging / eval / samples / checkpoints exactly
+    as ``run_trial`` does (lines carry a ``(trial t)`` tag). Each trial is
+    failure-isolated; uneven epoch counts are handled per trial.
+    """
+    world_rank = dist.get_rank() if dist.is_initialized() else 0
+    world_size = dist.get_world_size() if dist.is_initialized() else 1
+    gsize = dist.get_world_size(group) if dist.is_initialized() else 1
+    if gsize != 1:
+        raise ValueError("trial packing runs independent trials: it needs groups of one rank")
+    total = num_trials if num_trials is not None else world_size * len(specs)
+    device = bound_device()
+    train, test = data if data is not None else _load_data(opts, device)
+    D = int(train.data.shape[1])
+    shape = (1, opts.image_size, opts.image_size)
+    tr = []
+    for spec in specs:
+        trainer = _make_trainer(spec, opts, device, 0, D)
+        start = 1
+        if opts.ckpt_dir and opts.resume:
+            prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer)
+            if prog is not None:
+                start = prog["epoch"] + 1
+        idx = shard_indices(len(train), total, spec.group_id)
+        trainer.bind_train_data(train.data, idx)
+        rdir = (f"results-t{spec.group_id}-0" if opts.results else None)
+        tr.append(dict(spec=spec, trainer=trainer, start=start, n_shard=idx.numel(), rdir=rdir,
+                       stream=torch.cuda.Stream(device) if device.type == "cuda" else None,
+                       metrics=TrialMetrics(opts.metrics_dir, spec.group_id, enabled=True),
+                       gen=torch.Generator(device="cpu").manual_seed(spec.seed * 7919 + 17),
+                       done=0, train_loss=float("nan"), test_loss=float("nan"), failure={}))
+    global_barrier()
+    t0 = time.time()
+    last = max(t["spec"].epochs for t in tr)
+    for epoch in range(1, last + 1):
+        live = [t for t in tr if t["start"] <= epoch <= t["spec"].epochs and not t["failure"]]
+        te = time.perf_counter()
+        for t in live:  # enqueue every trial's epoch on its own stream
+            with guarded(f"trial {t['spec'].group_id} (world rank {world_rank})", None,
+                         lambda e, t=t: t["failure"].setdefault("error", f"{type(e).__name__}: {e}")):
+                maybe_inject(trial=t["spec"].group_id, epoch=epoch, rank=world_rank)
+                if t["stream"] is not None:
+                    with torch.cuda.stream(t["stream"]):
+                        t["step0"] = _launch_epoch(t["trainer"], epoch, t["n_shard"], opts)
+                else:
+                    t["step0"] = _launch_epoch(t["trainer"], epoch, t["n_shard"], opts)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        t_train = time.perf_counter() - te
+        for t in live:
+            if t["failure"]:
+                continue
+            spec = t["spec"]
+            with guarded(f"trial {spec.group_id} (world rank {world_rank})", None,
+                         lambda e, t=t: t["failure"].setdefault("error", f"{type(e).__name__}: {e}")):
+                t["train_loss"], t["test_loss"] = _run_epoch(
+                    t["trainer"], epoch, t["n_shard"], train, test, opts, group, t["rdir"], shape, t["gen"], device,
+                    spec, 0, t["metrics"], step0=t["step0"], t_train=t_train, tag=f"(trial {spec.group_id}) ")
+                t["done"] += 1
+    global_barrier()
+    t1 = time.time()
+    print(world_rank, "Done. time: %f" % (t1 - t0), flush=True)
+    return [TrialResult(t["spec"].group_id, t["done"], t["n_shard"], t["done"] * t["n_shard"], t1 - t0,
+                        t["train_loss"] / len(train), t["test_loss"], failed=bool(t["failure"]),
+                        error=t["failure"].get("error", "")) for t in tr]
 
 
 def idle_rank():

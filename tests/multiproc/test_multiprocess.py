@@ -169,3 +169,17 @@ def test_failed_trial_is_isolated(tmp_path):
     assert re.search(r"^\[0:0\] ====> Test set loss", text, re.M)
     agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
     assert agg["failed_trials"] == [1] and agg["samples"] == 512
+
+
+def test_vae_hpo_packed_trials(tmp_path):
+    """Two single-rank groups x two packed trials = four concurrent trials."""
+    rc, outs = _vae_hpo(tmp_path, 2, "--epochs", "1", "--ngroups", "2", "--trials-per-group", "2",
+                        "--metrics-dir", "m")
+    text = "\n".join(outs)
+    assert rc == 0, text
+    agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
+    # trial t trains 1+t epochs on a 1/4 shard (256 samples)
+    assert agg["trials"] == 4 and agg["samples"] == 256 * (1 + 2 + 3 + 4) and agg["failed_trials"] == []
+    assert re.search(r"^\[1:0\] \(trial 3\) ====> Epoch: 4 Average loss: \d+\.\d{4}$", text, re.M)
+    assert (tmp_path / "results-t2-0" / "sample_3.png").exists()
+    assert (tmp_path / "m" / "trial-3.jsonl").exists()

@@ -10,7 +10,9 @@ epochs). Launch one process per GPU with any launcher the reference supports
 Extensions (opt-in, default output unchanged): ``--lr`` / ``--beta`` (scalar or
 comma list, one per trial), ``--seed``, ``--ckpt-dir`` + ``--resume``,
 ``--metrics-dir`` (JSONL + aggregate samples/s), ``--per-group-results``, ``--bucket-mb``,
-``--no-graphs``, ``--backend {hip,torch}``, ``--synthetic/--real-data``.
+``--no-graphs``, ``--backend {hip,torch}``, ``--synthetic/--real-data``,
+``--trials-per-group T`` (T concurrent trials per single-rank group, one HIP
+stream each: trial packing on MI355X).
 """
 
 import argparse
@@ -23,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from utils import *  # noqa: F401,F403  (reference-compatible API + re-exports)
 
-from multidisttorch_amd.hpo.runner import RunOptions, idle_rank, run_trial
+from multidisttorch_amd.hpo.runner import RunOptions, idle_rank, run_packed_trials, run_trial
 from multidisttorch_amd.hpo.trial import build_specs, parse_list
 from multidisttorch_amd.parallel.autotune import parse_bucket_mb
 from multidisttorch_amd.runtime.bootstrap import control_group
@@ -57,6 +59,8 @@ def parse_args(argv=None):
     parser.add_argument("--model", type=str, default="mlp", choices=["mlp", "conv"],
                         help="mlp = reference MLP-VAE (fp32); conv = bf16 conv/deconv VAE")
     parser.add_argument("--image-size", type=int, default=28, choices=[28, 128])
+    parser.add_argument("--trials-per-group", type=int, default=1,
+                        help="train T trials concurrently per (single-rank) group, one HIP stream each")
     parser.add_argument("--bucket-mb", type=str, default=None,
                         help="intra-group all-reduce buckets: MiB cap, 0 = one bucket, 'auto' = measured")
     return parser.parse_args(argv)
@@ -69,7 +73,8 @@ def main(argv=None):
     processes_groups = setup_ddp_groups(ngroups)
     control_group()  # world collective: create the gloo control plane on every rank
 
-    specs = build_specs(ngroups, args.epochs, parse_list(args.lr), parse_list(args.beta), args.seed,
+    T = max(1, args.trials_per_group)
+    specs = build_specs(ngroups * T, args.epochs, parse_list(args.lr), parse_list(args.beta), args.seed,
                         epoch_offset=not args.no_epoch_offset)
     opts = RunOptions(batch_size=args.batch_size, log_interval=args.log_interval,
                       backend=args.backend, use_graphs=not args.no_graphs, graph_steps=args.graph_steps,
@@ -83,7 +88,11 @@ def main(argv=None):
     for group_id, group in enumerate(processes_groups):
         if dist.get_rank(group) >= 0:
             member = True
-            results.append(run_trial(specs[group_id], group, opts, num_trials=ngroups))
+            if T == 1:
+                results.append(run_trial(specs[group_id], group, opts, num_trials=ngroups))
+            else:
+                results.extend(run_packed_trials(specs[group_id * T:(group_id + 1) * T], group, opts,
+                                                 num_trials=ngroups * T))
     if not member:
         idle_rank()
 
