@@ -42,3 +42,28 @@ def test_bench_gpu_contract():
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["config"]["backend"] == "hip" and out["config"]["valid"] and out["value"] > 1e5
+
+
+def test_vae_hpo_packed_trials_gpu(tmp_path):
+    """Two trials packed on one MI355X (one HIP stream each), conv model."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29613")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "vae-hpo.py"), "--ngroups", "1", "--epochs", "1",
+                        "--trials-per-group", "2", "--model", "conv", "--train-samples", "4096",
+                        "--test-samples", "512", "--metrics-dir", "m"],
+                       capture_output=True, text=True, timeout=600, cwd=str(tmp_path), env=env)
+    text = r.stdout + r.stderr
+    assert r.returncode == 0, text[-4000:]
+    agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
+    assert agg["trials"] == 2 and agg["samples"] == 2048 * 1 + 2048 * 2 and agg["failed_trials"] == []
+    assert re.search(r"^\[0:0\] \(trial 1\) ====> Epoch: 2 Average loss: \d+\.\d{4}$", text, re.M)
+    assert (tmp_path / "results-t1-0" / "sample_2.png").exists()
+
+
+def test_bench_trial_packing():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "50", "--warmup", "10",
+                        "--trials-per-gpu", "2"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29614"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["config"]["trials"] == 2 and out["config"]["valid"]
