@@ -66,6 +66,7 @@ class RunOptions:
     data_dir: str = "data"
     synthetic: Optional[bool] = True
     bucket_mb: Optional[object] = None     # None: model default; 0: one bucket; float: MiB cap; "auto": measured
+    profile: bool = False                  # roctx ranges + device-synced phase timings in the metrics JSONL
 
 
 @dataclass
@@ -244,20 +245,33 @@ def _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape, g
     train_loss = _train_epoch(trainer, epoch, n_shard, len(train), opts, group, step0=step0, tag=tag)
     if t_train is None:
         t_train = time.perf_counter() - te
+    phases = {}
+
+    def _mark(name, t):
+        if opts.profile and device.type == "cuda":
+            torch.cuda.synchronize(device)
+        phases[name] = round(time.perf_counter() - t, 6)
+        return time.perf_counter()
+
+    t = time.perf_counter()
     test_loss = float("nan")
     if opts.eval_each_epoch:
         test_loss = _test_epoch(trainer, epoch, test, opts, group, rdir, shape, tag=tag)
+    t = _mark("eval_s", t)
     if rdir is not None:
-        with torch.no_grad():
+        with torch.no_grad(), trace.range(f"sample_{epoch}"):
             sample = torch.randn(64, trainer.Z, generator=gen).to(device)
             sample = trainer.decode(sample).cpu()
             os.makedirs(rdir, exist_ok=True)
             save_image(sample.view(64, *shape), f"{rdir}/sample_" + str(epoch) + ".png")
+    t = _mark("sample_s", t)
     if opts.ckpt_dir and grank == 0:
-        ckpt.save_trial(opts.ckpt_dir, trainer, spec, epoch)
+        with trace.range(f"ckpt_{epoch}"):
+            ckpt.save_trial(opts.ckpt_dir, trainer, spec, epoch)
+    _mark("ckpt_s", t)
     metrics.log(epoch=epoch, train_loss_sum=train_loss, train_loss=train_loss / len(train),
                 test_loss=test_loss, epoch_train_s=t_train, samples=n_shard,
-                train_samples_per_s=n_shard / max(t_train, 1e-9), lr=spec.lr, beta=spec.beta)
+                train_samples_per_s=n_shard / max(t_train, 1e-9), lr=spec.lr, beta=spec.beta, **phases)
     return train_loss, test_loss
 
 

@@ -183,3 +183,13 @@ def test_vae_hpo_packed_trials(tmp_path):
     assert re.search(r"^\[1:0\] \(trial 3\) ====> Epoch: 4 Average loss: \d+\.\d{4}$", text, re.M)
     assert (tmp_path / "results-t2-0" / "sample_3.png").exists()
     assert (tmp_path / "m" / "trial-3.jsonl").exists()
+
+
+def test_vae_hpo_profile_and_dtype_flags(tmp_path):
+    rc, outs = _vae_hpo(tmp_path, 1, "--epochs", "1", "--ngroups", "1", "--profile", "--dtype", "fp32")
+    assert rc == 0, "\n".join(outs)
+    rec = [json.loads(l) for l in open(tmp_path / "metrics" / "trial-0.jsonl")]
+    ep = [r for r in rec if r.get("epoch") == 1][0]
+    assert {"eval_s", "sample_s", "ckpt_s", "epoch_train_s"} <= set(ep)
+    rc, outs = _vae_hpo(tmp_path, 1, "--epochs", "1", "--ngroups", "1", "--dtype", "bf16")
+    assert rc != 0 and "computes in fp32" in "\n".join(outs)

@@ -59,6 +59,12 @@ def parse_args(argv=None):
     parser.add_argument("--model", type=str, default="mlp", choices=["mlp", "conv"],
                         help="mlp = reference MLP-VAE (fp32); conv = bf16 conv/deconv VAE")
     parser.add_argument("--image-size", type=int, default=28, choices=[28, 128])
+    parser.add_argument("--dtype", type=str, default=None, choices=[None, "fp32", "bf16"],
+                        help="compute dtype; mlp runs fp32 (the reference's precision), conv runs bf16 MFMA")
+    parser.add_argument("--profile", action="store_true",
+                        help="roctx ranges around phases (rocprofv3 --marker-trace) + synced phase timings in metrics")
+    parser.add_argument("--debug-sync", action="store_true",
+                        help="serialize every kernel launch (AMD_SERIALIZE_KERNEL=3): race / fault triage")
     parser.add_argument("--trials-per-group", type=int, default=1,
                         help="train T trials concurrently per (single-rank) group, one HIP stream each")
     parser.add_argument("--bucket-mb", type=str, default=None,
@@ -68,6 +74,18 @@ def parse_args(argv=None):
 
 def main(argv=None):
     args = parse_args(argv)
+    if args.debug_sync:  # must precede any HIP initialisation
+        os.environ["AMD_SERIALIZE_KERNEL"] = "3"
+        os.environ["AMD_SERIALIZE_COPY"] = "3"
+    want = {"mlp": "fp32", "conv": "bf16"}[args.model]
+    if args.dtype is not None and args.dtype != want:
+        raise SystemExit(f"--model {args.model} computes in {want} (requested {args.dtype})")
+    if args.profile:
+        from multidisttorch_amd.obs import trace
+
+        trace.enable()
+        if args.metrics_dir is None:
+            args.metrics_dir = "metrics"
     ngroups = args.ngroups
     comm_size, rank = setup_ddp()
     processes_groups = setup_ddp_groups(ngroups)
@@ -82,7 +100,8 @@ def main(argv=None):
                       results=not args.no_results, per_group_results=args.per_group_results,
                       train_samples=args.train_samples, test_samples=args.test_samples,
                       data_dir=args.data_dir, synthetic=False if args.real_data else True,
-                      model=args.model, image_size=args.image_size, bucket_mb=parse_bucket_mb(args.bucket_mb))
+                      model=args.model, image_size=args.image_size, bucket_mb=parse_bucket_mb(args.bucket_mb),
+                      profile=args.profile)
     results = []
     member = False
     for group_id, group in enumerate(processes_groups):
