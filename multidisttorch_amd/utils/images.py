@@ -19,7 +19,7 @@ import zlib
 import numpy as np
 import torch
 
-__all__ = ["make_grid", "save_image", "write_png"]
+__all__ = ["make_grid", "save_image", "write_png", "save_image_async", "flush_images"]
 
 
 def make_grid(t: torch.Tensor, nrow: int = 8, padding: int = 2, pad_value: float = 0.0) -> torch.Tensor:
@@ -68,3 +68,29 @@ def save_image(t: torch.Tensor, path: str, nrow: int = 8, padding: int = 2):
         Image.fromarray(arr).save(path)
     except Exception:
         write_png(path, np.ascontiguousarray(arr))
+
+
+# --------------------------------------------------------------------------
+# Asynchronous writer: the grid is assembled and PNG-encoded on a background
+# thread, so image output overlaps the next epoch's (asynchronous) graph
+# replays instead of stalling the host between epochs. Order of writes to the
+# same path is preserved (one worker).
+_POOL = None
+
+
+def save_image_async(t: torch.Tensor, path: str, nrow: int = 8, padding: int = 2):
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mdt-png")
+    host = t.detach().float().cpu()  # snapshot now; the device buffer may be reused
+    return _POOL.submit(save_image, host, path, nrow, padding)
+
+
+def flush_images():
+    """Block until every queued image is on disk (called before a run ends)."""
+    global _POOL
+    if _POOL is not None:
+        _POOL.shutdown(wait=True)
+        _POOL = None
