@@ -12,6 +12,11 @@ with stock PyTorch-ROCm, mirroring /root/reference/vae-hpo.py:
     [0,1] (stand-in for torchvision MNIST + ToTensor; no PIL decode, so this
     is generous to the reference) (vae-hpo.py:146-150)
   * BCE(sum) + KLD loss and loss.item() each step (vae-hpo.py:49-58, :73)
+With ``--model conv28|conv128`` the same loop trains the conv-VAE of
+``multidisttorch_amd/models/conv_vae.py`` in stock torch ops (MIOpen convs,
+bf16 autocast, channels-last left to torch's defaults): the reference's
+training loop with the north-star model swapped in, so bench.py's conv numbers
+have a same-GPU torch-eager anchor.
 Reports the hot training-loop throughput (samples/s over full epochs of the
 shard), and optionally the full reference epoch (train + test pass + 64-sample
 decode) as one JSON line. Single process or torchrun (one trial per rank).
@@ -55,12 +60,32 @@ def ref_loss(recon_x, x, mu, logvar):
     return bce + kld
 
 
+class ConvRef(nn.Module):
+    """Conv-VAE whose forward returns the ELBO (randn_like eps like the
+    reference's reparameterize), so DDP sees one module call per step."""
+
+    def __init__(self, net):
+        super().__init__()
+        self.net = net
+
+    def forward(self, x):
+        n = self.net
+        mu, lv = n.encode(x)
+        zz = mu + torch.randn_like(mu) * torch.exp(0.5 * lv)
+        t = n.decode_logits(zz).float()
+        bce = F.binary_cross_entropy_with_logits(t, x.view_as(t), reduction="sum")
+        mu, lv = mu.float(), lv.float()
+        return bce - 0.5 * torch.sum(1 + lv - mu.pow(2) - lv.exp())
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--batch-size", type=int, default=128)
     ap.add_argument("--ngroups", type=int, default=None)
     ap.add_argument("--full-epoch", action="store_true", help="also time test pass + sampling like the reference")
+    ap.add_argument("--model", default="mlp", choices=["mlp", "conv28", "conv128"])
+    ap.add_argument("--max-steps", type=int, default=None, help="cap the timed steps per epoch")
     a = ap.parse_args(argv)
 
     from multidisttorch_amd.runtime import setup_ddp
@@ -75,26 +100,46 @@ def main(argv=None):
     group = groups[gid]
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
-    train = synthetic_images(60000, seed=0).view(60000, 1, 28, 28)
-    test = synthetic_images(10000, seed=1).view(10000, 1, 28, 28)
-    trainset = torch.utils.data.TensorDataset(train, torch.zeros(60000))
-    testset = torch.utils.data.TensorDataset(test, torch.zeros(10000))
+    img = 128 if a.model == "conv128" else 28
+    ntr, nte = (60000, 10000) if img == 28 else (8192, 1024)
+    train = synthetic_images(ntr, seed=0, size=img).view(ntr, 1, img, img)
+    test = synthetic_images(nte, seed=1, size=img).view(nte, 1, img, img)
+    trainset = torch.utils.data.TensorDataset(train, torch.zeros(ntr))
+    testset = torch.utils.data.TensorDataset(test, torch.zeros(nte))
     sampler = torch.utils.data.distributed.DistributedSampler(trainset, rank=gid, num_replicas=world // n_per)
     loader = torch.utils.data.DataLoader(trainset, batch_size=a.batch_size, shuffle=False, sampler=sampler)
     test_loader = torch.utils.data.DataLoader(testset, batch_size=a.batch_size, shuffle=False)
 
-    model = RefVAE().to(dev)
+    if a.model == "mlp":
+        model = RefVAE().to(dev)
+        amp = None
+    else:
+        from multidisttorch_amd.models.conv_vae import TorchConvVAE, conv_vae_spec
+
+        z = 32 if img == 28 else 64
+        model = ConvRef(TorchConvVAE(conv_vae_spec(img, 1, z), img, 1, z)).to(dev)
+        amp = torch.bfloat16 if dev.type == "cuda" else None
     model = torch.nn.parallel.DistributedDataParallel(model, process_group=group)
     opt = optim.Adam(model.parameters(), lr=1e-3)
+
+    def step_loss(data):
+        if a.model == "mlp":
+            recon, mu, lv = model(data)
+            return ref_loss(recon, data, mu, lv)
+        if amp is None:
+            return model(data)
+        with torch.autocast(device_type="cuda", dtype=amp):
+            return model(data)
 
     def train_epoch():
         model.train()
         n = 0
-        for data, _ in loader:
+        for bi, (data, _) in enumerate(loader):
+            if a.max_steps is not None and bi >= a.max_steps:
+                break
             data = data.to(dev)
             opt.zero_grad()
-            recon, mu, lv = model(data)
-            loss = ref_loss(recon, data, mu, lv)
+            loss = step_loss(data)
             loss.backward()
             loss.item()
             opt.step()
@@ -107,8 +152,7 @@ def main(argv=None):
         data, _ = next(it)
         data = data.to(dev)
         opt.zero_grad()
-        r, mu, lv = model(data)
-        ref_loss(r, data, mu, lv).backward()
+        step_loss(data).backward()
         opt.step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -117,7 +161,7 @@ def main(argv=None):
     samples = 0
     for _ in range(a.epochs):
         samples += train_epoch()
-        if a.full_epoch:
+        if a.full_epoch and a.model == "mlp":
             model.eval()
             with torch.no_grad():
                 for data, _ in test_loader:
@@ -138,6 +182,7 @@ def main(argv=None):
     total = samples * K  # samples counted once per trial
     if rank == 0:
         print(json.dumps({"what": "reference-equivalent torch eager (DDP + DataLoader + .item())",
+                          "model": a.model, "amp": str(amp),
                           "device": str(dev), "trials": K, "world": world, "epochs": a.epochs,
                           "full_epoch": a.full_epoch, "samples_per_trial": samples, "wall_s": round(dt, 4),
                           "aggregate_samples_per_s": round(total / dt, 1),

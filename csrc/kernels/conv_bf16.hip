@@ -7,6 +7,7 @@
 #include "vae_mlp.h"
 #include "adam_common.h"
 #include "conv_igemm.h"
+#include "conv_small.h"
 
 namespace mdt {
 
@@ -99,26 +100,9 @@ __global__ void __launch_bounds__(256) bce_logits_k(const float* logits, const f
 }
 
 // Sum loss partials -> loss ring; advance step (optionally cursor).
-__global__ void __launch_bounds__(256) conv_loss_finalize_k(const float* bce_part, int nb, const float* kld_part, int nk,
-                                                            TrainState* st, const HParams* hp, int advance_cursor) {
+__global__ void __launch_bounds__(256) conv_loss_finalize_k(LossArgs la) {
   __shared__ float scratch[16];
-  float sb = 0.f, sk = 0.f;
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) sb += bce_part[i];
-  for (int i = threadIdx.x; i < nk; i += blockDim.x) sk += kld_part[i];
-  const float bce = block_sum(sb, scratch);
-  __syncthreads();
-  const float kld = block_sum(sk, scratch);
-  if (threadIdx.x == 0) {
-    const float loss = bce + hp->kl_beta * kld;
-    st->loss_hist[(st->step - 1) % kLossHist] = loss;
-    st->epoch_loss += (double)loss;
-    st->epoch_count += 1.0;
-    if (advance_cursor) {
-      int c = st->cursor + 1;
-      if (st->nbatches > 0 && c >= st->nbatches) c = 0;
-      st->cursor = c;
-    }
-  }
+  loss_finalize_body(la, scratch);
 }
 
 // step++ and the Adam beta^t running products (first launch of a step).
@@ -275,8 +259,9 @@ int mdt_bce_logits(const float* logits, const float* X, const int* rows, int B, 
 
 int mdt_conv_loss_finalize(const float* bce_part, int nb, const float* kld_part, int nk, void* st, const void* hp,
                            int advance_cursor, hipStream_t s) {
-  hipLaunchKernelGGL(conv_loss_finalize_k, dim3(1), dim3(256), 0, s, bce_part, nb, kld_part, nk,
-                     reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), advance_cursor);
+  const LossArgs la{bce_part, nb, kld_part, nk, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp),
+                    advance_cursor};
+  hipLaunchKernelGGL(conv_loss_finalize_k, dim3(1), dim3(256), 0, s, la);
   return (int)hipGetLastError();
 }
 

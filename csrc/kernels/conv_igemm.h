@@ -84,4 +84,28 @@ struct TrUnit {
   int seg, tap, co0, ci0;
 };
 
+// One job of a horizontally fused launch (conv_jobs.hip): an independent
+// piece of work (a GEMM, a weight gradient, a column sum, ...) that runs on
+// its own range of workgroups of a shared launch. `args` holds the job's
+// kernel-argument struct; `kind` names the device body that interprets it.
+constexpr int kJobArgBytes = 256;
+struct JobBlob {
+  int kind;       // 0 = none / not fusable
+  int nblk;       // workgroups of this job (256 threads each)
+  int aux[6];     // per-kind geometry (e.g. GEMM tiles per plane, k-splits)
+  alignas(16) unsigned char args[kJobArgBytes];
+};
+
+// Job kind ids (see conv_jobs.hip for the instantiated combinations).
+enum JobKindBase : int {
+  kJobIgemm = 1000,      // + mode*100 + cfg  (bf16, vector gathers)
+  kJobWgrad = 2000,      // + cfg              (bf16, vector gathers)
+  kJobWgradThin = 2050,  // + 20*f32 + cfg     (per-element gathers)
+  kJobThinConv = 3000,   // + CO + 100*f32
+  kJobThinTconv = 4000,  // + CO
+  kJobColsum = 5000,
+  kJobLoss = 5001,
+  kJobCombine = 5002,
+};
+
 }  // namespace mdt

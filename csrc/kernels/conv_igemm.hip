@@ -21,926 +21,16 @@
 // blockIdx remapped so neighbouring tiles share an XCD's L2.
 // Epilogues fuse bias, ReLU, the ReLU-backward mask of the produced gradient
 // and the per-block column sums that become the next layer's bias gradient.
-#include <stdlib.h>
-
-#include "common.h"
-#include "conv_igemm.h"
+#include "conv_igemm_dev.h"
 
 namespace mdt {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.mul) + n) >> f.shr; }
-
-// Bijective XCD-aware remap: blocks dispatched to the same XCD (orig % 8)
-// receive consecutive tile ids, so a tile row's A panel stays in one L2.
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-}
-
-__device__ __forceinline__ bf16x8 zero8() {
-  bf16x8 z;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
-  return z;
-}
-
-__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-template <typename T>
-__device__ __forceinline__ bf16x8 load_chunk(const T* p);
-template <>
-__device__ __forceinline__ bf16x8 load_chunk<__bf16>(const __bf16* p) {
-  return *reinterpret_cast<const bf16x8*>(p);
-}
-template <>
-__device__ __forceinline__ bf16x8 load_chunk<float>(const float* p) {
-  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
-  bf16x8 r;
-  r[0] = (__bf16)a.x; r[1] = (__bf16)a.y; r[2] = (__bf16)a.z; r[3] = (__bf16)a.w;
-  r[4] = (__bf16)b.x; r[5] = (__bf16)b.y; r[6] = (__bf16)b.z; r[7] = (__bf16)b.w;
-  return r;
-}
-
-// Row-major [rows][64] bf16 image (128-B rows) read by rows: 16-B chunk ch of
-// row r lives at chunk slot ch ^ (r & 7).
-__device__ __forceinline__ int rimg(int r, int ch) { return (r << 7) + (((ch ^ r) & 7) << 4); }
-
-// m-major [64][WD] bf16 image read with ds_read_b64_tr_b16: the XOR keeps the
-// eight 32-B row segments a 32-lane half reads (rows 8g+q and 8g+8+q) on
-// disjoint banks for every row width used here.
-template <int WD>
-__device__ __forceinline__ int trsw(int r) {
-  if constexpr (WD == 128) return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
-  else if constexpr (WD == 64) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
-  else if constexpr (WD == 32) return 2 * ((r >> 3) & 1);
-  else return 0;
-}
-template <int WD>
-__device__ __forceinline__ int timg(int r, int ch) { return r * (WD * 2) + ((ch ^ trsw<WD>(r)) << 4); }
-
-// 16x16x32 MFMA operand whose 16 "rows" are image columns c0..c0+15 and whose
-// 32 k values are image rows kb..kb+31: lane l gets column l&15, rows
-// kb + 8(l>>4) + 0..7, via two transposing reads of 4 rows each.
-template <int WD>
-__device__ __forceinline__ bf16x8 tr_frag(const uint8_t* img, int c0, int kb, int lane) {
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int r0 = kb + 8 * g + q, r1 = r0 + 4;
-  const int ch = (c0 >> 3) + (p >> 1);
-  const int sub = (p & 1) << 3;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + timg<WD>(r0, ch) + sub));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + timg<WD>(r1, ch) + sub));
-  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-template <int BM_, int BN_, int WM_, int WN_>
-struct TileCfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
-  static constexpr int KWS = 4 / (WM * WN);  // waves splitting the 64-deep k tile
-  static constexpr int FM = BM / (16 * WM), FN = BN / (16 * WN);
-  static_assert(WM * WN * KWS == 4 && KWS <= 2 && FM >= 1 && FN >= 1, "bad tile config");
-  static constexpr int RED_BYTES = KWS == 2 ? WM * WN * FM * FN * 64 * 16 : 0;
-};
-
-// ================================================================ forward ====
-struct IgArgs {
-  ConvDesc d;
-  const void* A;
-  const __bf16* B;  // [classes][Ncols][K]
-  __bf16* y16;
-  float* y32;
-  const float* bias;
-  const __bf16* omask;
-  float* colsum;    // [classes*mtiles][Ncols] or null
-  float* slab;      // split-K partials [ksplit][M][Ncols] (then no epilogue) or null
-  int relu;
-  int M, Ncols, K, mtiles, ntiles, ktiles, kt_per_split;
-  FastDiv f_pix, f_w, f_ch, f_tw;
-};
-
-// Shared epilogue of the forward-type kernels: combine k-halves (KWS == 2),
-// then either raw split-K partials or bias + ReLU + output mask + bf16/f32
-// stores + per-block column sums. `lds` must be free (caller passed a barrier).
-template <int MODE, class TC>
-__device__ __forceinline__ void igemm_epilogue(const IgArgs& a, f32x4 (&acc)[TC::FM][TC::FN], uint8_t* lds, int mt,
-                                               int nt, int kz, int cls, int oa, int ob) {
-  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
-  const ConvDesc& d = a.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
-  if constexpr (KWS == 2) {  // combine the two k-halves
-    float* red = reinterpret_cast<float*>(lds);
-    const int slot = w % (WM * WN);
-    if (wk == 1) {
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          *reinterpret_cast<f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4) = acc[fm][fn];
-    }
-    __syncthreads();
-    if (wk == 0) {
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] += *reinterpret_cast<const f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4);
-    }
-  }
-
-  const bool epi = (KWS == 1) || wk == 0;
-  const int rbase = mt * BM + wm * (BM / WM) + 4 * (lane >> 4);
-  const int cbase = nt * BN + wn * (BN / WN) + (lane & 15);
-  if (a.slab) {
-    if (epi) {
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = rbase + fm * 16 + r;
-#pragma unroll
-          for (int fn = 0; fn < FN; ++fn) {
-            const int col = cbase + fn * 16;
-            if (m < a.M && col < a.Ncols) a.slab[((size_t)kz * a.M + m) * a.Ncols + col] = acc[fm][fn][r];
-          }
-        }
-    }
-    return;
-  }
-  float cs[FN];
-#pragma unroll
-  for (int fn = 0; fn < FN; ++fn) cs[fn] = 0.f;
-  if (epi) {
-    float bv[FN];
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      const int col = cbase + fn * 16;
-      bv[fn] = (a.bias && col < a.Ncols) ? a.bias[col] : 0.f;
-    }
-#pragma unroll
-    for (int fm = 0; fm < FM; ++fm) {
-      int grow[4];
-      bool rok[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = rbase + fm * 16 + r;
-        rok[r] = m < a.M;
-        if constexpr (MODE == kModeConv) {
-          grow[r] = m;
-        } else {
-          const uint32_t mm = rok[r] ? (uint32_t)m : 0u;
-          const uint32_t n = fdiv(mm, a.f_pix);
-          const uint32_t rem = mm - n * a.f_pix.d;
-          const uint32_t yy = fdiv(rem, a.f_w);
-          const uint32_t xx = rem - yy * a.f_w.d;
-          grow[r] = ((int)n * d.H + (int)yy * d.S + oa) * d.W + (int)xx * d.S + ob;
-        }
-      }
-      float mk[4][FN];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int col = cbase + fn * 16;
-          const bool ok = rok[r] && col < a.Ncols;
-          mk[r][fn] = (a.omask && ok) ? (float)a.omask[(size_t)grow[r] * a.Ncols + col] : 1.f;
-        }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int col = cbase + fn * 16;
-          const bool ok = rok[r] && col < a.Ncols;
-          float v = acc[fm][fn][r] + bv[fn];
-          if (a.relu) v = fmaxf(v, 0.f);
-          v = mk[r][fn] > 0.f ? v : 0.f;
-          if (ok) {
-            const size_t o = (size_t)grow[r] * a.Ncols + col;
-            if (a.y16) a.y16[o] = (__bf16)v;
-            if (a.y32) a.y32[o] = v;
-          }
-          cs[fn] += ok ? v : 0.f;
-        }
-    }
-  }
-  if (a.colsum) {
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      cs[fn] += __shfl_xor(cs[fn], 16, 64);
-      cs[fn] += __shfl_xor(cs[fn], 32, 64);
-    }
-    float* sc = reinterpret_cast<float*>(lds + TC::RED_BYTES);
-    if (epi && lane < 16) {
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) sc[wm * BN + wn * (BN / WN) + fn * 16 + lane] = cs[fn];
-    }
-    __syncthreads();
-    if (tid < BN) {
-      float t = 0.f;
-#pragma unroll
-      for (int q = 0; q < WM; ++q) t += sc[q * BN + tid];
-      const int col = nt * BN + tid;
-      if (col < a.Ncols) a.colsum[(size_t)(cls * a.mtiles + mt) * a.Ncols + col] = t;
-    }
-  }
-}
-
-template <int MODE, typename AT, bool VEC, class TC>
-__global__ void __launch_bounds__(256) igemm_fwd_k(IgArgs a) {
-  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
-  constexpr int A_CH = BM / 32;                // 16-B chunks per thread of the BM x 64 A tile
-  constexpr int B_CH = (BN * 8 + 255) / 256;   // ... of the BN x 64 B tile
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-  static_assert(TC::RED_BYTES + WM * BN * 4 <= 2 * STAGE, "epilogue scratch exceeds LDS");
-  static_assert(VEC || MODE == kModeConv, "thin gathers exist for conv mode only");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
-
-  const ConvDesc& d = a.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = tile / a.ntiles, nt = tile - mt * a.ntiles;
-  const int kz = blockIdx.y, cls = blockIdx.z;
-  const int kt0 = kz * a.kt_per_split;
-  const int kt1 = min(a.ktiles, kt0 + a.kt_per_split);
-
-  int ea = 0, eb = 0, oa = 0, ob = 0;
-  if constexpr (MODE == kModeTconv) {
-    const int ca = cls / d.S, cb = cls - ca * d.S;
-    oa = ((ca - d.P) % d.S + d.S) % d.S;
-    ob = ((cb - d.P) % d.S + d.S) % d.S;
-    ea = (oa + d.P - ca) / d.S;
-    eb = (ob + d.P - cb) / d.S;
-  }
-
-  // ---- per-thread staging coordinates (fixed for the whole k loop)
-  const int ach = tid & 7;
-  int abase[A_CH], ay[A_CH], ax[A_CH];
-  bool aok[A_CH];
-#pragma unroll
-  for (int i = 0; i < A_CH; ++i) {
-    const int m = mt * BM + (tid >> 3) + 32 * i;
-    aok[i] = m < a.M;
-    const uint32_t mm = aok[i] ? (uint32_t)m : 0u;
-    const uint32_t n = fdiv(mm, a.f_pix);
-    const uint32_t rem = mm - n * a.f_pix.d;
-    const uint32_t yy = fdiv(rem, a.f_w);
-    const uint32_t xx = rem - yy * a.f_w.d;
-    if constexpr (MODE == kModeConv) {
-      abase[i] = (int)n * d.H * d.W * d.C;
-      ay[i] = (int)yy * d.S - d.P;
-      ax[i] = (int)xx * d.S - d.P;
-    } else {
-      abase[i] = (int)n * d.OH * d.OW * d.CO;
-      ay[i] = (int)yy + ea;
-      ax[i] = (int)xx + eb;
-    }
-  }
-  const AT* Ap = reinterpret_cast<const AT*>(a.A);
-  const __bf16* Bc = a.B + (size_t)cls * a.Ncols * a.K;
-
-  bf16x8 ra[A_CH], rb[B_CH];
-  auto gload = [&](int kt) {
-    const int kk = kt * 64 + 8 * ach;
-    if constexpr (VEC) {
-      const uint32_t tap = fdiv((uint32_t)kk, a.f_ch);
-      const int ch = kk - (int)(tap * a.f_ch.d);
-      const uint32_t t0 = fdiv(tap, a.f_tw);
-      const int t1 = (int)(tap - t0 * a.f_tw.d);
-      const bool kok = kk < a.K;
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        int off;
-        bool ok;
-        if constexpr (MODE == kModeConv) {
-          const int iy = ay[i] + (int)t0, ix = ax[i] + t1;
-          ok = aok[i] && kok && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-          off = abase[i] + (iy * d.W + ix) * d.C + ch;
-        } else {
-          const int oy = ay[i] - (int)t0, ox = ax[i] - t1;
-          ok = aok[i] && kok && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
-          off = abase[i] + (oy * d.OW + ox) * d.CO + ch;
-        }
-        const bf16x8 v = load_chunk<AT>(Ap + (ok ? off : 0));
-        ra[i] = ok ? v : zero8();
-      }
-    } else {
-      float v[A_CH][8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = kk + j;
-        const uint32_t tap = fdiv((uint32_t)k, a.f_ch);
-        const int ch = k - (int)(tap * a.f_ch.d);
-        const uint32_t ky = fdiv(tap, a.f_tw);
-        const int kx = (int)(tap - ky * a.f_tw.d);
-        const bool kok = k < a.K;
-#pragma unroll
-        for (int i = 0; i < A_CH; ++i) {
-          const int iy = ay[i] + (int)ky, ix = ax[i] + kx;
-          const bool ok = aok[i] && kok && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-          const float x = (float)Ap[ok ? abase[i] + (iy * d.W + ix) * d.C + ch : 0];
-          v[i][j] = ok ? x : 0.f;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ra[i][j] = (__bf16)v[i][j];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      const int col = nt * BN + r;
-      const bool ok = r < BN && col < a.Ncols && kk < a.K;
-      const bf16x8 v = load_chunk<__bf16>(Bc + (ok ? (size_t)col * a.K + kk : 0));
-      rb[i] = ok ? v : zero8();
-    }
-  };
-  auto sstore = [&](int buf) {
-    uint8_t* As = lds + buf * STAGE;
-    uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<bf16x8*>(As + rimg(r, ach)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      if (r < BN) *reinterpret_cast<bf16x8*>(Bs + rimg(r, ach)) = rb[i];
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const uint8_t* As = lds + buf * STAGE;
-    const uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int s = (KWS == 2 ? 0 : 0); s < 2 / KWS; ++s) {
-      const int ks = KWS == 2 ? wk : s;
-      const int ch = ks * 4 + (lane >> 4);
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-        af[fm] = *reinterpret_cast<const bf16x8*>(As + rimg(wm * (BM / WM) + fm * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn)
-        bfr[fn] = *reinterpret_cast<const bf16x8*>(Bs + rimg(wn * (BN / WN) + fn * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
-    }
-  };
-
-  if (kt0 < kt1) {
-    gload(kt0);
-    sstore(0);
-  }
-  __syncthreads();
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int buf = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) gload(kt + 1);
-    compute(buf);
-    if (more) sstore(buf ^ 1);
-    __syncthreads();
-  }
-
-  igemm_epilogue<MODE, TC>(a, acc, lds, mt, nt, kz, cls, oa, ob);
-}
-
-// ---------------------------------------------------------- LDS-DMA helpers ----
-// Zero source for out-of-range chunks of an LDS-DMA tile load (static device
-// memory is zero-initialised): a global_load_lds has no per-lane predicate, so
-// masked lanes fetch 16 zero bytes instead.
-__device__ __attribute__((aligned(64))) uint8_t g_zero16[64];
-
-__device__ __forceinline__ void glds16(const void* src, uint8_t* lds_base) {
-  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
-}
-
-// Counted wait on this wave's outstanding LDS-DMA loads: `n` newer tiles of
-// `NI` instructions each may stay in flight.
-template <int NI, int S>
-__device__ __forceinline__ void wait_tiles(int n) {
-  static_assert(NI * (S - 2) <= 63, "vmcnt range");
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory"); break;
-    case 2: if constexpr (S >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory"); break;
-    case 3: if constexpr (S >= 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NI) : "memory"); break;
-    default: if constexpr (S >= 6) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NI) : "memory"); break;
-  }
-}
-
-// Workgroup barrier that neither drains the LDS-DMA queue (unlike
-// __syncthreads, whose fence waits vmcnt(0)) nor lets this wave's LDS reads
-// of the previous stage still be in flight.
-__device__ __forceinline__ void stage_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// Forward-type GEMM with an S-stage LDS ring filled by global_load_lds
-// (bf16 vector gathers only): S-1 k-tiles are in flight while one is
-// multiplied, with no staging registers. The per-lane global address does
-// the im2col gather AND the XOR swizzle (the LDS side of a DMA is lane-linear).
-template <int MODE, class TC, int S>
-__global__ void __launch_bounds__(256) igemm_glds_k(IgArgs a) {
-  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
-  constexpr int BR = BN < 32 ? 32 : BN;         // staged B rows (>= one DMA row group per wave)
-  constexpr int A_CH = BM / 32, B_CH = BR / 32;  // DMA instructions per wave per tile
-  constexpr int NI = A_CH + B_CH;
-  constexpr int A_BYTES = BM * 128, STAGE = (BM + BR) * 128;
-  static_assert(TC::RED_BYTES + WM * BN * 4 <= S * STAGE, "epilogue scratch exceeds LDS");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[S * STAGE];
-
-  const ConvDesc& d = a.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = tile / a.ntiles, nt = tile - mt * a.ntiles;
-  const int kz = blockIdx.y, cls = blockIdx.z;
-  const int kt0 = kz * a.kt_per_split;
-  const int nk = min(a.ktiles, kt0 + a.kt_per_split) - kt0;
-
-  int ea = 0, eb = 0, oa = 0, ob = 0;
-  if constexpr (MODE == kModeTconv) {
-    const int ca = cls / d.S, cb = cls - ca * d.S;
-    oa = ((ca - d.P) % d.S + d.S) % d.S;
-    ob = ((cb - d.P) % d.S + d.S) % d.S;
-    ea = (oa + d.P - ca) / d.S;
-    eb = (ob + d.P - cb) / d.S;
-  }
-  // lane-linear DMA: lane l of wave w fills row 32i + 8w + (l>>3), slot l&7,
-  // which must hold logical chunk slot ^ (row & 7)
-  const int ach = (tid & 7) ^ ((tid >> 3) & 7);
-  int abase[A_CH], ay[A_CH], ax[A_CH];
-  bool aok[A_CH];
-#pragma unroll
-  for (int i = 0; i < A_CH; ++i) {
-    const int m = mt * BM + (tid >> 3) + 32 * i;
-    aok[i] = m < a.M;
-    const uint32_t mm = aok[i] ? (uint32_t)m : 0u;
-    const uint32_t n = fdiv(mm, a.f_pix);
-    const uint32_t rem = mm - n * a.f_pix.d;
-    const uint32_t yy = fdiv(rem, a.f_w);
-    const uint32_t xx = rem - yy * a.f_w.d;
-    if constexpr (MODE == kModeConv) {
-      abase[i] = (int)n * d.H * d.W * d.C;
-      ay[i] = (int)yy * d.S - d.P;
-      ax[i] = (int)xx * d.S - d.P;
-    } else {
-      abase[i] = (int)n * d.OH * d.OW * d.CO;
-      ay[i] = (int)yy + ea;
-      ax[i] = (int)xx + eb;
-    }
-  }
-  const __bf16* Ap = reinterpret_cast<const __bf16*>(a.A);
-  const __bf16* Bc = a.B + (size_t)cls * a.Ncols * a.K;
-
-  auto issue = [&](int kt, int buf) {
-    uint8_t* As = lds + buf * STAGE;
-    uint8_t* Bs = As + A_BYTES;
-    const int kk = kt * 64 + 8 * ach;
-    const uint32_t tap = fdiv((uint32_t)kk, a.f_ch);
-    const int ch = kk - (int)(tap * a.f_ch.d);
-    const uint32_t t0 = fdiv(tap, a.f_tw);
-    const int t1 = (int)(tap - t0 * a.f_tw.d);
-    const bool kok = kk < a.K;
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      int off;
-      bool ok;
-      if constexpr (MODE == kModeConv) {
-        const int iy = ay[i] + (int)t0, ix = ax[i] + t1;
-        ok = aok[i] && kok && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-        off = abase[i] + (iy * d.W + ix) * d.C + ch;
-      } else {
-        const int oy = ay[i] - (int)t0, ox = ax[i] - t1;
-        ok = aok[i] && kok && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
-        off = abase[i] + (oy * d.OW + ox) * d.CO + ch;
-      }
-      glds16(ok ? (const void*)(Ap + off) : (const void*)g_zero16, As + (32 * i + 8 * w) * 128);
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      const int col = nt * BN + r;
-      const bool ok = r < BN && col < a.Ncols && kk < a.K;
-      glds16(ok ? (const void*)(Bc + (size_t)col * a.K + kk) : (const void*)g_zero16, Bs + (32 * i + 8 * w) * 128);
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const uint8_t* As = lds + buf * STAGE;
-    const uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2 / KWS; ++s) {
-      const int ks = KWS == 2 ? wk : s;
-      const int ch = ks * 4 + (lane >> 4);
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-        af[fm] = *reinterpret_cast<const bf16x8*>(As + rimg(wm * (BM / WM) + fm * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn)
-        bfr[fn] = *reinterpret_cast<const bf16x8*>(Bs + rimg(wn * (BN / WN) + fn * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
-    }
-  };
-
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(kt0 + s, s);
-  for (int it = 0; it < nk; ++it) {
-    const int newer = min(nk - 1 - it, S - 2);
-    wait_tiles<NI, S>(newer);
-    stage_barrier();
-    if (it + S - 1 < nk) issue(kt0 + it + S - 1, (it + S - 1) % S);
-    compute(it % S);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  stage_barrier();
-  igemm_epilogue<MODE, TC>(a, acc, lds, mt, nt, kz, cls, oa, ob);
-}
-
-// ================================================================= wgrad ====
-struct WgArgs {
-  ConvDesc d;
-  const __bf16* G;  // [M][CO]
-  const void* X;    // NHWC conv input
-  float* out;       // [nsplit][CO][K2]
-  int M, K2, cotiles, ktiles, mtiles, mt_per_split;
-  FastDiv f_pix, f_w, f_c, f_kw;
-};
-
-// Epilogue of the weight-gradient kernels: combine k-halves, store the f32
-// partial tile of this m-split.
-template <class TC>
-__device__ __forceinline__ void wgrad_epilogue(const WgArgs& a, f32x4 (&acc)[TC::FM][TC::FN], uint8_t* lds, int ct,
-                                               int nt, int split) {
-  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
-  const ConvDesc& d = a.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
-  if constexpr (KWS == 2) {
-    float* red = reinterpret_cast<float*>(lds);
-    const int slot = w % (WM * WN);
-    if (wk == 1) {
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          *reinterpret_cast<f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4) = acc[fm][fn];
-    }
-    __syncthreads();
-    if (wk == 0) {
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] += *reinterpret_cast<const f32x4*>(red + (((slot * FM + fm) * FN + fn) * 64 + lane) * 4);
-    }
-  }
-  if (KWS == 1 || wk == 0) {
-    float* out = a.out + (size_t)split * d.CO * a.K2;
-#pragma unroll
-    for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int orow = ct * BM + wm * (BM / WM) + fm * 16 + 4 * (lane >> 4) + r;
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int kp = nt * BN + wn * (BN / WN) + fn * 16 + (lane & 15);
-          if (orow < d.CO && kp < a.K2) out[(size_t)orow * a.K2 + kp] = acc[fm][fn][r];
-        }
-      }
-  }
-}
-
-template <typename XT, bool VEC, class TC>
-__global__ void __launch_bounds__(256) wgrad_k(WgArgs a) {
-  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
-  constexpr int CPR_A = BM / 8, A_RPP = 256 / CPR_A, A_CH = 64 / A_RPP;
-  constexpr int CPR_B = BN / 8, B_RPP = 256 / CPR_B, B_CH = (64 + B_RPP - 1) / B_RPP;
-  constexpr int A_BYTES = 64 * BM * 2, B_BYTES = 64 * BN * 2, STAGE = A_BYTES + B_BYTES;
-  static_assert(TC::RED_BYTES <= 2 * STAGE, "reduction scratch exceeds LDS");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
-
-  const ConvDesc& d = a.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
-  // 1-D grid, split-major after the XCD remap: an XCD owns a contiguous
-  // m-range for ALL (co, k') tiles, so its slice of G and X is fetched into
-  // its L2 once instead of once per tile.
-  const int wid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntile = a.cotiles * a.ktiles;
-  const int split = wid / ntile;
-  const int tile = wid - split * ntile;
-  const int ct = tile / a.ktiles, nt = tile - ct * a.ktiles;
-  const int mt0 = split * a.mt_per_split;
-  const int mt1 = min(a.mtiles, mt0 + a.mt_per_split);
-
-  const int cha = tid % CPR_A, ra0 = tid / CPR_A;
-  const int co = ct * BM + 8 * cha;
-  const bool coka = co < d.CO;
-  const int chb = tid % CPR_B, rb0 = tid / CPR_B;
-  const XT* Xp = reinterpret_cast<const XT*>(a.X);
-  const int HWC = d.H * d.W * d.C;
-
-  // B-operand column coordinates (fixed per thread)
-  int kyv[VEC ? 1 : 8], kxv[VEC ? 1 : 8], civ[VEC ? 1 : 8];
-  bool kokv[VEC ? 1 : 8];
-#pragma unroll
-  for (int j = 0; j < (VEC ? 1 : 8); ++j) {
-    const int kp = nt * BN + 8 * chb + j;
-    kokv[j] = kp < a.K2;
-    const uint32_t tap = fdiv((uint32_t)(kokv[j] ? kp : 0), a.f_c);
-    civ[j] = (kokv[j] ? kp : 0) - (int)(tap * a.f_c.d);
-    const uint32_t ky = fdiv(tap, a.f_kw);
-    kyv[j] = (int)ky;
-    kxv[j] = (int)(tap - ky * a.f_kw.d);
-  }
-
-  bf16x8 ra[A_CH], rb[B_CH];
-  auto gload = [&](int mtile) {
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const int m = mtile * 64 + ra0 + A_RPP * i;
-      const bool ok = coka && m < a.M;
-      const bf16x8 v = load_chunk<__bf16>(a.G + (ok ? (size_t)m * d.CO + co : 0));
-      ra[i] = ok ? v : zero8();
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int r = rb0 + B_RPP * i;
-      const int m = mtile * 64 + r;
-      const bool mok = r < 64 && m < a.M;
-      const uint32_t mm = mok ? (uint32_t)m : 0u;
-      const uint32_t n = fdiv(mm, a.f_pix);
-      const uint32_t rem = mm - n * a.f_pix.d;
-      const uint32_t oy = fdiv(rem, a.f_w);
-      const uint32_t ox = rem - oy * a.f_w.d;
-      const int iy0 = (int)oy * d.S - d.P, ix0 = (int)ox * d.S - d.P;
-      if constexpr (VEC) {
-        const int iy = iy0 + kyv[0], ix = ix0 + kxv[0];
-        const bool ok = mok && kokv[0] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-        const bf16x8 v = load_chunk<XT>(Xp + (ok ? (int)n * HWC + (iy * d.W + ix) * d.C + civ[0] : 0));
-        rb[i] = ok ? v : zero8();
-      } else {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int iy = iy0 + kyv[j], ix = ix0 + kxv[j];
-          const bool ok = mok && kokv[j] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-          const float x = (float)Xp[ok ? (int)n * HWC + (iy * d.W + ix) * d.C + civ[j] : 0];
-          v[j] = ok ? x : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) rb[i][j] = (__bf16)v[j];
-      }
-    }
-  };
-  auto sstore = [&](int buf) {
-    uint8_t* As = lds + buf * STAGE;
-    uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const int r = ra0 + A_RPP * i;
-      *reinterpret_cast<bf16x8*>(As + timg<BM>(r, cha)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int r = rb0 + B_RPP * i;
-      if (r < 64) *reinterpret_cast<bf16x8*>(Bs + timg<BN>(r, chb)) = rb[i];
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const uint8_t* As = lds + buf * STAGE;
-    const uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2 / KWS; ++s) {
-      const int kb = 32 * (KWS == 2 ? wk : s);
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm) af[fm] = tr_frag<BM>(As, wm * (BM / WM) + 16 * fm, kb, lane);
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) bfr[fn] = tr_frag<BN>(Bs, wn * (BN / WN) + 16 * fn, kb, lane);
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
-    }
-  };
-
-  if (mt0 < mt1) {
-    gload(mt0);
-    sstore(0);
-  }
-  __syncthreads();
-  for (int mtile = mt0; mtile < mt1; ++mtile) {
-    const int buf = (mtile - mt0) & 1;
-    const bool more = mtile + 1 < mt1;
-    if (more) gload(mtile + 1);
-    compute(buf);
-    if (more) sstore(buf ^ 1);
-    __syncthreads();
-  }
-
-  wgrad_epilogue<TC>(a, acc, lds, ct, nt, split);
-}
-
-// Weight-gradient GEMM with an S-stage LDS-DMA ring (bf16 inputs, C % 8 == 0).
-// Both m-major images are filled lane-linearly; the tr_b16 XOR swizzle is
-// applied on the source side (lane slot p holds logical chunk p ^ trsw(row)).
-template <class TC, int S>
-__global__ void __launch_bounds__(256) wgrad_glds_k(WgArgs a) {
-  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
-  constexpr int CPR_A = BM / 8, A_RPP = 256 / CPR_A, A_CH = 64 / A_RPP;
-  constexpr int CPR_B = BN / 8, B_RPP = 256 / CPR_B, B_CH = (64 + B_RPP - 1) / B_RPP;
-  constexpr int NI = A_CH + B_CH;
-  constexpr int A_BYTES = 64 * BM * 2;
-  constexpr int B_BYTES = (B_RPP * B_CH) * BN * 2;  // rows past 64 only absorb zero DMAs
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  static_assert(TC::RED_BYTES <= S * STAGE, "reduction scratch exceeds LDS");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[S * STAGE];
-
-  const ConvDesc& d = a.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
-  // 1-D grid, split-major after the XCD remap: an XCD owns a contiguous
-  // m-range for ALL (co, k') tiles, so its slice of G and X is fetched into
-  // its L2 once instead of once per tile.
-  const int wid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntile = a.cotiles * a.ktiles;
-  const int split = wid / ntile;
-  const int tile = wid - split * ntile;
-  const int ct = tile / a.ktiles, nt = tile - ct * a.ktiles;
-  const int mt0 = split * a.mt_per_split;
-  const int nk = min(a.mtiles, mt0 + a.mt_per_split) - mt0;
-
-  const int rA0 = tid / CPR_A, rB0 = tid / CPR_B;
-  const int cA = (tid % CPR_A) ^ trsw<BM>(rA0);
-  const int cB = (tid % CPR_B) ^ trsw<BN>(rB0);
-  const int co = ct * BM + 8 * cA;
-  const bool coka = co < d.CO;
-  const int kp = nt * BN + 8 * cB;
-  const bool kokb = kp < a.K2;
-  const uint32_t tap = fdiv((uint32_t)(kokb ? kp : 0), a.f_c);
-  const int ci = (kokb ? kp : 0) - (int)(tap * a.f_c.d);
-  const uint32_t kyu = fdiv(tap, a.f_kw);
-  const int ky = (int)kyu, kx = (int)(tap - kyu * a.f_kw.d);
-  const __bf16* Xp = reinterpret_cast<const __bf16*>(a.X);
-  const int HWC = d.H * d.W * d.C;
-
-  auto issue = [&](int mtile, int buf) {
-    uint8_t* As = lds + buf * STAGE;
-    uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const int m = mtile * 64 + rA0 + A_RPP * i;
-      const bool ok = coka && m < a.M;
-      glds16(ok ? (const void*)(a.G + (size_t)m * d.CO + co) : (const void*)g_zero16,
-             As + (A_RPP * i + w * (64 / CPR_A)) * (BM * 2));
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int r = rB0 + B_RPP * i;
-      const int m = mtile * 64 + r;
-      const bool mok = r < 64 && m < a.M;
-      const uint32_t mm = mok ? (uint32_t)m : 0u;
-      const uint32_t n = fdiv(mm, a.f_pix);
-      const uint32_t rem = mm - n * a.f_pix.d;
-      const uint32_t oy = fdiv(rem, a.f_w);
-      const uint32_t ox = rem - oy * a.f_w.d;
-      const int iy = (int)oy * d.S - d.P + ky, ix = (int)ox * d.S - d.P + kx;
-      const bool ok = mok && kokb && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-      glds16(ok ? (const void*)(Xp + (int)n * HWC + (iy * d.W + ix) * d.C + ci) : (const void*)g_zero16,
-             Bs + (B_RPP * i + w * (64 / CPR_B)) * (BN * 2));
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const uint8_t* As = lds + buf * STAGE;
-    const uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2 / KWS; ++s) {
-      const int kb = 32 * (KWS == 2 ? wk : s);
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm) af[fm] = tr_frag<BM>(As, wm * (BM / WM) + 16 * fm, kb, lane);
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) bfr[fn] = tr_frag<BN>(Bs, wn * (BN / WN) + 16 * fn, kb, lane);
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
-    }
-  };
-
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(mt0 + s, s);
-  for (int it = 0; it < nk; ++it) {
-    const int newer = min(nk - 1 - it, S - 2);
-    wait_tiles<NI, S>(newer);
-    stage_barrier();
-    if (it + S - 1 < nk) issue(mt0 + it + S - 1, (it + S - 1) % S);
-    compute(it % S);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  stage_barrier();
-  wgrad_epilogue<TC>(a, acc, lds, ct, nt, split);
-}
-
-// ======================================================= small reductions ====
-// Split-K combine: y = sum_z slab[z] + bias (+relu) -> f32 and/or bf16.
-// `cnt` outputs per block, 256/cnt threads per output summing interleaved
-// z slices (independent loads in flight), then a fixed-order LDS combine.
-__global__ void __launch_bounds__(256) splitk_combine_k(const float* slab, int ksplit, int M, int N, int cnt,
-                                                        const float* bias, int relu, float* y32, __bf16* y16) {
+__global__ void __launch_bounds__(256) splitk_combine_k(CombineArgs c) {
   __shared__ float red[256];
-  const int t = threadIdx.x, rp = 256 / cnt, col = t % cnt, rl = t / cnt;
-  const long long MN = (long long)M * N;
-  const long long e = (long long)blockIdx.x * cnt + col;
-  float v = 0.f;
-  if (rl < rp && e < MN) {
-#pragma unroll 4
-    for (int z = rl; z < ksplit; z += rp) v += slab[(size_t)z * MN + e];
-  }
-  red[t] = v;
-  __syncthreads();
-  if (rl == 0 && e < MN) {
-    float acc = 0.f;
-    for (int r = 0; r < rp; ++r) acc += red[r * cnt + col];
-    if (bias) acc += bias[e % N];
-    if (relu) acc = fmaxf(acc, 0.f);
-    if (y32) y32[e] = acc;
-    if (y16) y16[e] = (__bf16)acc;
-  }
+  splitk_combine_body(c, red, blockIdx.x);
 }
 
-// Column sums of a bf16 [M][N] matrix (N % 8 == 0): partial row blockIdx.y of
-// `slab` ([gridDim.y][N]) sums rows [y*rows_per, (y+1)*rows_per).
-__global__ void __launch_bounds__(256) colsum_k(const __bf16* G, int M, int N, int rows_per, float* slab) {
-  const int c8 = blockIdx.x * 256 + threadIdx.x;
-  if (c8 * 8 >= N) return;
-  const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-  for (int r = r0; r < r1; ++r) {
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(G + (size_t)r * N + 8 * c8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) slab[(size_t)blockIdx.y * N + 8 * c8 + j] = s[j];
-}
+__global__ void __launch_bounds__(256) colsum_k(ColsumArgs c) { colsum_body(c, blockIdx.x); }
 
 }  // namespace mdt
 
@@ -948,26 +38,11 @@ __global__ void __launch_bounds__(256) colsum_k(const __bf16* G, int M, int N, i
 using namespace mdt;
 
 namespace {
-
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+}  // namespace
 
-// forward-type tile configurations
-using F0 = TileCfg<128, 128, 2, 2>;
-using F1 = TileCfg<128, 64, 2, 2>;
-using F2 = TileCfg<128, 32, 4, 1>;
-using F3 = TileCfg<128, 16, 4, 1>;
-using F4 = TileCfg<64, 128, 2, 2>;
-using F5 = TileCfg<64, 64, 2, 2>;
-using F6 = TileCfg<64, 32, 2, 1>;
-using F7 = TileCfg<64, 16, 4, 1>;
-// weight-gradient tile configurations (co x k'), capped at 64x64 so the
-// m-split partial slabs stay small (slab bytes ~ blocks x BM x BN x 4)
-using W0 = TileCfg<64, 64, 2, 2>;
-using W1 = TileCfg<64, 32, 2, 1>;
-using W2 = TileCfg<64, 16, 4, 1>;
-using W3 = TileCfg<32, 64, 2, 2>;
-using W4 = TileCfg<32, 32, 2, 1>;
-using W5 = TileCfg<32, 16, 2, 1>;
+namespace mdt {
+using namespace mdt::tiles;
 
 bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p) {
   FwdPlan q{};
@@ -1045,6 +120,71 @@ bool use_glds() {
   }();
   return v;
 }
+
+int build_igemm(int mode, const void* A, const void* B16, ConvDesc d, const float* bias, int relu, void* y16,
+                float* y32, const void* omask, float* colsum, float* ws, IgArgs* pa, FwdPlan* pq, CombineArgs* pc,
+                int* nc) {
+  FwdPlan q;
+  const bool can_split = ws != nullptr && omask == nullptr && colsum == nullptr;
+  if (!plan_fwd(mode, d, can_split, &q)) return 1;
+  IgArgs a{};
+  a.d = d;
+  a.A = A;
+  a.B = reinterpret_cast<const __bf16*>(B16);
+  a.relu = relu;
+  a.M = q.M; a.Ncols = q.Ncols; a.K = q.K; a.mtiles = q.mtiles; a.ntiles = q.ntiles; a.ktiles = q.ktiles;
+  a.kt_per_split = q.kt_per_split;
+  if (mode == kModeConv) {
+    a.f_pix = make_fastdiv(d.OH * d.OW); a.f_w = make_fastdiv(d.OW);
+    a.f_ch = make_fastdiv(d.C); a.f_tw = make_fastdiv(d.KW);
+  } else {
+    a.f_pix = make_fastdiv((d.H / d.S) * (d.W / d.S)); a.f_w = make_fastdiv(d.W / d.S);
+    a.f_ch = make_fastdiv(d.CO); a.f_tw = make_fastdiv(d.KW / d.S);
+  }
+  *nc = 0;
+  if (q.ksplit > 1) {
+    a.slab = ws;
+    const long long MN = (long long)q.M * q.Ncols;
+    int rp = 1;
+    while (rp < 64 && rp * 4 < q.ksplit) rp *= 2;
+    const int cnt = 256 / rp;
+    *pc = CombineArgs{ws, q.ksplit, q.M, q.Ncols, cnt, bias, relu, y32, reinterpret_cast<__bf16*>(y16)};
+    *nc = cdiv(MN, cnt);
+  } else {
+    a.y16 = reinterpret_cast<__bf16*>(y16); a.y32 = y32; a.bias = bias;
+    a.omask = reinterpret_cast<const __bf16*>(omask); a.colsum = colsum;
+  }
+  *pa = a;
+  *pq = q;
+  return 0;
+}
+
+int build_wgrad(const void* G16, const void* X, ConvDesc d, float* out, WgArgs* pa, WgradPlan* pq) {
+  WgradPlan q;
+  if (!plan_wgrad(d, &q)) return 1;
+  WgArgs a{};
+  a.d = d;
+  a.G = reinterpret_cast<const __bf16*>(G16);
+  a.X = X;
+  a.out = out;
+  a.M = q.M; a.K2 = q.K2; a.cotiles = q.cotiles; a.ktiles = q.ktiles; a.mtiles = q.mtiles;
+  a.mt_per_split = q.mt_per_split;
+  a.f_pix = make_fastdiv(d.OH * d.OW); a.f_w = make_fastdiv(d.OW);
+  a.f_c = make_fastdiv(d.C); a.f_kw = make_fastdiv(d.KW);
+  *pa = a;
+  *pq = q;
+  return 0;
+}
+
+int launch_splitk_combine(const CombineArgs& c, int nblk, hipStream_t s) {
+  hipLaunchKernelGGL(splitk_combine_k, dim3(nblk), dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+
+}  // namespace mdt
+
+namespace {
+using namespace mdt::tiles;
 
 template <int MODE, typename AT, bool VEC, class TC>
 void launch_fwd(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
@@ -1136,29 +276,11 @@ int mdt_wgrad_plan(ConvDesc d, int* info) {
 // pass; omask/colsum are not allowed with split-K).
 int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d, const float* bias, int relu,
               void* y16, float* y32, const void* omask, float* colsum, float* ws, hipStream_t s) {
+  IgArgs a;
   FwdPlan q;
-  const bool can_split = ws != nullptr && omask == nullptr && colsum == nullptr;
-  if (!plan_fwd(mode, d, can_split, &q)) return 1;
-  IgArgs a{};
-  a.d = d;
-  a.A = A;
-  a.B = reinterpret_cast<const __bf16*>(B16);
-  a.relu = relu;
-  a.M = q.M; a.Ncols = q.Ncols; a.K = q.K; a.mtiles = q.mtiles; a.ntiles = q.ntiles; a.ktiles = q.ktiles;
-  a.kt_per_split = q.kt_per_split;
-  if (mode == kModeConv) {
-    a.f_pix = make_fastdiv(d.OH * d.OW); a.f_w = make_fastdiv(d.OW);
-    a.f_ch = make_fastdiv(d.C); a.f_tw = make_fastdiv(d.KW);
-  } else {
-    a.f_pix = make_fastdiv((d.H / d.S) * (d.W / d.S)); a.f_w = make_fastdiv(d.W / d.S);
-    a.f_ch = make_fastdiv(d.CO); a.f_tw = make_fastdiv(d.KW / d.S);
-  }
-  if (q.ksplit > 1) {
-    a.slab = ws;
-  } else {
-    a.y16 = reinterpret_cast<__bf16*>(y16); a.y32 = y32; a.bias = bias;
-    a.omask = reinterpret_cast<const __bf16*>(omask); a.colsum = colsum;
-  }
+  CombineArgs c;
+  int nc = 0;
+  if (build_igemm(mode, A, B16, d, bias, relu, y16, y32, omask, colsum, ws, &a, &q, &c, &nc)) return 1;
   int rc;
   if (mode == kModeConv) {
     if (q.thin) rc = a_is_f32 ? dispatch_thin<float>(a, q, s) : dispatch_thin<__bf16>(a, q, s);
@@ -1171,29 +293,14 @@ int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d
     rc = use_glds() ? dispatch_glds<kModeTconv>(a, q, s) : dispatch_fwd_cfg<kModeTconv, __bf16, true>(a, q, s);
   }
   if (rc) return rc;
-  if (q.ksplit > 1) {
-    const long long MN = (long long)q.M * q.Ncols;
-    int rp = 1;
-    while (rp < 64 && rp * 4 < q.ksplit) rp *= 2;
-    const int cnt = 256 / rp;
-    hipLaunchKernelGGL(splitk_combine_k, dim3(cdiv(MN, cnt)), dim3(256), 0, s, ws, q.ksplit, q.M, q.Ncols, cnt, bias,
-                       relu, y32, reinterpret_cast<__bf16*>(y16));
-  }
+  if (nc > 0) hipLaunchKernelGGL(splitk_combine_k, dim3(nc), dim3(256), 0, s, c);
   return (int)hipGetLastError();
 }
 
 int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* out, hipStream_t s) {
+  WgArgs a;
   WgradPlan q;
-  if (!plan_wgrad(d, &q)) return 1;
-  WgArgs a{};
-  a.d = d;
-  a.G = reinterpret_cast<const __bf16*>(G16);
-  a.X = X;
-  a.out = out;
-  a.M = q.M; a.K2 = q.K2; a.cotiles = q.cotiles; a.ktiles = q.ktiles; a.mtiles = q.mtiles;
-  a.mt_per_split = q.mt_per_split;
-  a.f_pix = make_fastdiv(d.OH * d.OW); a.f_w = make_fastdiv(d.OW);
-  a.f_c = make_fastdiv(d.C); a.f_kw = make_fastdiv(d.KW);
+  if (build_wgrad(G16, X, d, out, &a, &q)) return 1;
   if (!q.thin && !use_glds()) {
     if (x_is_f32) return 3;
     switch (q.cfg) {
@@ -1231,8 +338,9 @@ int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* o
 
 int mdt_colsum(const void* G16, int M, int N, int rows_per, float* slab, hipStream_t s) {
   if (N % 8 || rows_per < 1) return 1;
-  dim3 grid(cdiv(N / 8, 256), cdiv(M, rows_per));
-  hipLaunchKernelGGL(colsum_k, grid, dim3(256), 0, s, reinterpret_cast<const __bf16*>(G16), M, N, rows_per, slab);
+  const int gx = cdiv(N / 8, 256);
+  const ColsumArgs c{reinterpret_cast<const __bf16*>(G16), M, N, rows_per, gx, slab};
+  hipLaunchKernelGGL(colsum_k, dim3(gx * cdiv(M, rows_per)), dim3(256), 0, s, c);
   return (int)hipGetLastError();
 }
 

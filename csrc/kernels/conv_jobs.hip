@@ -1,0 +1,280 @@
+// Horizontally fused conv-VAE launches ("job kernels") for MI355X (gfx950).
+//
+// Why: at the conv-VAE's batch sizes most launches of a training step are
+// latency-bound -- a 28x28 step was 29 launches of which a dozen do < 2 us
+// of work, and a kernel boundary in a replayed hipGraph costs ~1.5 us plus
+// the fill/drain of the grid. Independent pieces of work of the same step
+// (the weight gradient and the backward-data GEMM of one layer, a bias column
+// sum, the loss reduction) therefore share ONE launch: each job owns a
+// contiguous range of workgroups and runs the same device body as its
+// stand-alone kernel (conv_igemm_dev.h, conv_thin.h, conv_small.h), so results
+// are bitwise identical to the unfused sequence. Two streams with graph
+// branches were measured slower on this stack (cross-stream graph edges,
+// models/conv_vae.py::_backward_overlap), which is why the fusion is done
+// inside a launch instead.
+//
+// A launch of jobs (kinds k0 < k1 < k2 after sorting) needs an instantiated
+// jobs_k<J0, J1, J2>; the table below lists the combinations the 28x28 and
+// 128x128 models' backward sweeps use. Any other combination reports "not
+// fused" and the caller launches the jobs' stand-alone kernels instead.
+#include <string.h>
+
+#include <algorithm>
+
+#include "conv_igemm_dev.h"
+#include "conv_small.h"
+#include "conv_thin.h"
+
+namespace mdt {
+using namespace tiles;
+
+struct JobPack {
+  JobBlob j[3];
+  int start1, start2;  // first workgroup of job 1 / job 2
+};
+
+template <class T>
+__device__ __forceinline__ const T& job_args(const JobBlob& j) {
+  return *reinterpret_cast<const T*>(j.args);
+}
+
+struct JNone {
+  static constexpr int ID = 0, LDS = 0;
+  static __device__ __forceinline__ void run(const JobBlob&, uint8_t*, int) {}
+};
+
+// forward-type GEMM (bf16, vector gathers); aux = {tiles per plane, k-splits}
+template <int MODE, int CFG, class TC>
+struct JIg {
+  static constexpr int ID = kJobIgemm + MODE * 100 + CFG, LDS = igemm_lds_bytes<TC>();
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    const int ntb = j.aux[0], ks = j.aux[1];
+    const int r = b / ntb, t = b - r * ntb;
+    const int cls = r / ks, kz = r - cls * ks;
+    igemm_body<MODE, __bf16, true, TC>(job_args<IgArgs>(j), lds, t, ntb, kz, cls);
+  }
+};
+
+template <int CFG, class TC>
+struct JWg {
+  static constexpr int ID = kJobWgrad + CFG, LDS = wgrad_lds_bytes<TC>();
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    wgrad_body<__bf16, true, TC>(job_args<WgArgs>(j), lds, b, j.nblk);
+  }
+};
+
+template <typename XT, int CFG, class TC>
+struct JWgThin {
+  static constexpr int ID = kJobWgradThin + (sizeof(XT) == 4 ? 20 : 0) + CFG, LDS = wgrad_lds_bytes<TC>();
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    wgrad_body<XT, false, TC>(job_args<WgArgs>(j), lds, b, j.nblk);
+  }
+};
+
+template <int CO, typename TIN>
+struct JThinConv {
+  static constexpr int ID = kJobThinConv + CO + (sizeof(TIN) == 4 ? 100 : 0), LDS = thin_conv_lds_bytes<CO, 4>();
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    thin_conv_body<CO, 4, TIN>(job_args<ThinConvArgs>(j), lds, b);
+  }
+};
+
+struct JColsum {
+  static constexpr int ID = kJobColsum, LDS = 0;
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t*, int b) { colsum_body(job_args<ColsumArgs>(j), b); }
+};
+
+struct JLoss {
+  static constexpr int ID = kJobLoss, LDS = 64;
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int) {
+    loss_finalize_body(job_args<LossArgs>(j), reinterpret_cast<float*>(lds));
+  }
+};
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+template <class A, class B, class C>
+__global__ void __launch_bounds__(256) jobs_k(JobPack p) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[cmax(cmax(A::LDS, B::LDS), cmax(C::LDS, 16))];
+  const int b = blockIdx.x;
+  if (b < p.start1) A::run(p.j[0], lds, b);
+  else if (b < p.start2) B::run(p.j[1], lds, b - p.start1);
+  else C::run(p.j[2], lds, b - p.start2);
+}
+
+}  // namespace mdt
+
+using namespace mdt;
+
+namespace {
+
+typedef void (*PackLaunch)(const JobPack&, int, hipStream_t);
+
+template <class A, class B, class C>
+void launch_pack(const JobPack& p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((jobs_k<A, B, C>), dim3(grid), dim3(256), 0, s, p);
+}
+
+struct Combo {
+  int k0, k1, k2;
+  PackLaunch fn;
+};
+
+#define COMBO3(A, B, C) {A::ID, B::ID, C::ID, &launch_pack<A, B, C>}
+#define COMBO2(A, B) {A::ID, B::ID, 0, &launch_pack<A, B, JNone>}
+
+using WgT5 = JWgThin<__bf16, 5, W5>;
+using ThinC32 = JThinConv<32, __bf16>;
+using Wg0 = JWg<0, W0>;
+using Wg1 = JWg<1, W1>;
+using IgC1 = JIg<kModeConv, 1, F1>;
+using IgC4 = JIg<kModeConv, 4, F4>;
+using IgC5 = JIg<kModeConv, 5, F5>;
+using IgT1 = JIg<kModeTconv, 1, F1>;
+using IgT2 = JIg<kModeTconv, 2, F2>;
+using IgT4 = JIg<kModeTconv, 4, F4>;
+using IgT5 = JIg<kModeTconv, 5, F5>;
+using IgT6 = JIg<kModeTconv, 6, F6>;
+
+// kinds sorted ascending within each entry
+const Combo kCombos[] = {
+    // last layer: thin weight gradient || thin backward-data || loss reduction
+    COMBO3(WgT5, ThinC32, JLoss),
+    COMBO2(WgT5, ThinC32),
+    // transposed-conv layers: conv-mode backward-data || weight gradient
+    COMBO2(IgC5, Wg0),
+    COMBO2(IgC1, Wg0),
+    COMBO2(IgC4, Wg0),
+    // decoder Linear (split-K backward-data) || weight gradient || its bias column sums
+    COMBO3(IgT6, Wg1, JColsum),
+    COMBO3(IgT5, Wg0, JColsum),
+    // encoder head || weight gradient || head bias column sums
+    COMBO3(IgT4, Wg0, JColsum),
+    // conv layers: parity-mode backward-data || weight gradient
+    COMBO2(IgT6, Wg0),
+    COMBO2(IgT4, Wg0),
+    COMBO2(IgT1, Wg0),
+    COMBO2(IgT2, Wg0),
+    COMBO2(IgT5, Wg0),
+};
+
+#undef COMBO3
+#undef COMBO2
+
+inline int cdivj(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+template <class T>
+void put_args(JobBlob* j, const T& a) {
+  static_assert(sizeof(T) <= kJobArgBytes, "job arguments exceed the blob");
+  memset(j->args, 0, sizeof(j->args));
+  memcpy(j->args, &a, sizeof(T));
+}
+
+}  // namespace
+
+extern "C" {
+
+// Forward-type GEMM as a job (`g`); with split-K the combine pass is a second
+// job (`c`, kind kJobCombine, to run after `g`), else c->kind = 0. g->kind = 0
+// when the GEMM has no job form (f32 / per-element gathers, LDS-DMA path).
+int mdt_job_igemm(JobBlob* g, JobBlob* c, int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d,
+                  const float* bias, int relu, void* y16, float* y32, const void* omask, float* colsum, float* ws) {
+  IgArgs a;
+  FwdPlan q;
+  CombineArgs cb;
+  int nc = 0;
+  if (build_igemm(mode, A, B16, d, bias, relu, y16, y32, omask, colsum, ws, &a, &q, &cb, &nc)) return 1;
+  memset(g, 0, sizeof(*g));
+  memset(c, 0, sizeof(*c));
+  const bool ok = !a_is_f32 && !q.thin && !use_glds();
+  g->kind = ok ? kJobIgemm + mode * 100 + q.cfg : 0;
+  g->nblk = q.mtiles * q.ntiles * q.ksplit * q.classes;
+  g->aux[0] = q.mtiles * q.ntiles;
+  g->aux[1] = q.ksplit;
+  put_args(g, a);
+  if (nc > 0) {
+    c->kind = kJobCombine;
+    c->nblk = nc;
+    put_args(c, cb);
+  }
+  return 0;
+}
+
+int mdt_job_wgrad(JobBlob* j, const void* G16, const void* X, int x_is_f32, ConvDesc d, float* out) {
+  WgArgs a;
+  WgradPlan q;
+  if (build_wgrad(G16, X, d, out, &a, &q)) return 1;
+  memset(j, 0, sizeof(*j));
+  if (!q.thin) j->kind = (x_is_f32 || use_glds()) ? 0 : kJobWgrad + q.cfg;
+  else j->kind = kJobWgradThin + (x_is_f32 ? 20 : 0) + q.cfg;
+  j->nblk = q.cotiles * q.ktiles * q.nsplit;
+  put_args(j, a);
+  return 0;
+}
+
+int mdt_job_thin_conv(JobBlob* j, const void* X, int x_is_f32, const float* Wf, ConvDesc d, const float* bias,
+                      int relu, void* y16, const void* omask, float* colsum) {
+  if (d.C != 1 || d.KH != 4 || d.KW != 4) return 1;
+  memset(j, 0, sizeof(*j));
+  const bool ok = d.CO == 16 || d.CO == 32 || d.CO == 64;
+  j->kind = ok ? kJobThinConv + d.CO + (x_is_f32 ? 100 : 0) : 0;
+  j->nblk = cdivj((long long)d.N * d.OH * d.OW, 256);
+  const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
+                        colsum};
+  put_args(j, ta);
+  return 0;
+}
+
+int mdt_job_colsum(JobBlob* j, const void* G16, int M, int N, int rows_per, float* slab) {
+  if (N % 8 || rows_per < 1) return 1;
+  memset(j, 0, sizeof(*j));
+  const int gx = cdivj(N / 8, 256);
+  j->kind = kJobColsum;
+  j->nblk = gx * cdivj(M, rows_per);
+  put_args(j, ColsumArgs{reinterpret_cast<const __bf16*>(G16), M, N, rows_per, gx, slab});
+  return 0;
+}
+
+int mdt_job_loss(JobBlob* j, const float* bce_part, int nb, const float* kld_part, int nk, void* st, const void* hp,
+                 int advance_cursor) {
+  memset(j, 0, sizeof(*j));
+  j->kind = kJobLoss;
+  j->nblk = 1;
+  put_args(j, LossArgs{bce_part, nb, kld_part, nk, reinterpret_cast<TrainState*>(st),
+                       reinterpret_cast<const HParams*>(hp), advance_cursor});
+  return 0;
+}
+
+// Launch 2-3 jobs as ONE kernel. Returns 0 when launched, 1 when no fused
+// kernel exists for this combination of kinds (nothing launched: the caller
+// falls back to the stand-alone kernels), 2 on bad input.
+int mdt_launch_jobs(const JobBlob* jobs, int n, hipStream_t s) {
+  if (n < 2 || n > 3) return 2;
+  const JobBlob* v[3] = {&jobs[0], &jobs[1], n > 2 ? &jobs[2] : nullptr};
+  for (int i = 0; i < n; ++i)
+    if (v[i]->kind <= 0 || v[i]->nblk <= 0) return 1;
+  std::sort(v, v + n, [](const JobBlob* a, const JobBlob* b) { return a->kind < b->kind; });
+  const int k2 = n > 2 ? v[2]->kind : 0;
+  for (const Combo& c : kCombos) {
+    if (c.k0 != v[0]->kind || c.k1 != v[1]->kind || c.k2 != k2) continue;
+    JobPack p;
+    memset(&p, 0, sizeof(p));
+    p.j[0] = *v[0];
+    p.j[1] = *v[1];
+    if (n > 2) p.j[2] = *v[2];
+    p.start1 = v[0]->nblk;
+    p.start2 = v[0]->nblk + v[1]->nblk;
+    const int grid = p.start2 + (n > 2 ? v[2]->nblk : 0);
+    c.fn(p, grid, s);
+    return (int)hipGetLastError() ? -1 : 0;
+  }
+  return 1;
+}
+
+// Launch one job with its stand-alone kernel form (combine / colsum / loss).
+int mdt_launch_job1(const JobBlob* j, hipStream_t s) {
+  if (j->kind == kJobCombine) return launch_splitk_combine(*reinterpret_cast<const CombineArgs*>(j->args), j->nblk, s);
+  return 1;
+}
+
+}  // extern "C"

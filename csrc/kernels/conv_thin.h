@@ -1,0 +1,225 @@
+// Device bodies of the direct single-channel edge-layer kernels (see
+// conv_thin.hip for the design). Included by conv_thin.hip (stand-alone
+// kernels) and conv_igemm.hip (horizontally fused job kernels).
+#pragma once
+#include "common.h"
+#include "conv_igemm.h"
+
+namespace mdt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <typename T>
+__device__ __forceinline__ float ld1(const T* p) { return (float)*p; }
+
+// Per-block column sums of v[CO] over the block's threads (deterministic):
+// transpose through LDS, then thread c < CO adds its column in order.
+template <int CO>
+__device__ __forceinline__ void block_colsum(const float (&v)[CO], float* red, float* out) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int c = 0; c < CO; ++c) red[t * (CO + 1) + c] = v[c];
+  __syncthreads();
+  if (t < CO) {
+    float s = 0.f;
+    for (int r = 0; r < (int)blockDim.x; ++r) s += red[r * (CO + 1) + t];
+    out[t] = s;
+  }
+}
+
+struct ThinConvArgs {
+  const void* X;       // TIN input (C = 1)
+  const float* Wf;     // f32 master weights [CO][K][K]
+  ConvDesc d;
+  const float* bias;
+  int relu;
+  __bf16* y16;
+  const __bf16* omask;
+  float* colsum;       // per-block column sums [blocks][CO] or null
+};
+
+// LDS: staged weights [TAPS][CO] + the colsum transpose (256 x (CO+1)).
+template <int CO, int K>
+constexpr int thin_conv_lds_bytes() { return (K * K * CO + 256 * (CO + 1)) * 4; }
+
+template <int CO, int K, typename TIN>
+__device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* lds, int bid) {
+  constexpr int TAPS = K * K;
+  const ConvDesc& d = ta.d;
+  const TIN* X = reinterpret_cast<const TIN*>(ta.X);
+  const float* Wf = ta.Wf;
+  const float* bias = ta.bias;
+  float* wl = reinterpret_cast<float*>(lds);
+  float* red = wl + TAPS * CO;
+  const int M = d.N * d.OH * d.OW;
+  const int m = bid * blockDim.x + threadIdx.x;
+  const bool live = m < M;
+  const int mm = live ? m : 0;
+  const int n = mm / (d.OH * d.OW);
+  const int rem = mm - n * d.OH * d.OW;
+  const int oy = rem / d.OW, ox = rem - oy * d.OW;
+  const int iy0 = oy * d.S - d.P, ix0 = ox * d.S - d.P;
+  const TIN* img = X + (size_t)n * d.H * d.W;
+  float xin[TAPS];
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t) {
+    const int iy = iy0 + t / K, ix = ix0 + t % K;
+    const bool ok = live && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+    const float x = ld1(img + (ok ? iy * d.W + ix : 0));
+    xin[t] = ok ? x : 0.f;
+  }
+  // weights staged once per block in LDS as [tap][co]; the FMA loop reads
+  // them with wave-uniform (broadcast) ds_read_b128, 4 channels per read
+  for (int e = threadIdx.x; e < TAPS * CO; e += blockDim.x) {
+    const int c = e / TAPS, t = e - c * TAPS;
+    wl[t * CO + c] = Wf[e];
+  }
+  __syncthreads();
+  float acc[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) acc[c] = bias ? bias[c] : 0.f;
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t) {
+    const float x = xin[t];
+#pragma unroll
+    for (int c4 = 0; c4 < CO / 4; ++c4) {
+      const float4 w = *reinterpret_cast<const float4*>(wl + t * CO + 4 * c4);
+      acc[4 * c4 + 0] = fmaf(x, w.x, acc[4 * c4 + 0]);
+      acc[4 * c4 + 1] = fmaf(x, w.y, acc[4 * c4 + 1]);
+      acc[4 * c4 + 2] = fmaf(x, w.z, acc[4 * c4 + 2]);
+      acc[4 * c4 + 3] = fmaf(x, w.w, acc[4 * c4 + 3]);
+    }
+  }
+  if (ta.relu) {
+#pragma unroll
+    for (int c = 0; c < CO; ++c) acc[c] = fmaxf(acc[c], 0.f);
+  }
+  if (ta.omask) {
+#pragma unroll
+    for (int c8 = 0; c8 < CO / 8; ++c8) {
+      const bf16x8 mk = *reinterpret_cast<const bf16x8*>(ta.omask + (size_t)mm * CO + 8 * c8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[8 * c8 + j] = (float)mk[j] > 0.f ? acc[8 * c8 + j] : 0.f;
+    }
+  }
+  if (live) {
+#pragma unroll
+    for (int c8 = 0; c8 < CO / 8; ++c8) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (__bf16)acc[8 * c8 + j];
+      *reinterpret_cast<bf16x8*>(ta.y16 + (size_t)m * CO + 8 * c8) = o;
+    }
+  }
+  if (ta.colsum) {
+    if (!live) {
+#pragma unroll
+      for (int c = 0; c < CO; ++c) acc[c] = 0.f;
+    }
+    block_colsum<CO>(acc, red, ta.colsum + (size_t)bid * CO);
+  }
+}
+
+// Transposed conv with one output channel, conv view (input C = 1 is the
+// convT output, CO = convT input channels): y[n, iy, ix] = bias +
+// sum over the class taps (ty, tx) and co of G[n, oy, ox, co] * W[co][ky][kx].
+// blockIdx.y = parity class (a, b); threads walk the class's pixels.
+struct ThinTconvArgs {
+  const __bf16* G;
+  const float* Wf;
+  ConvDesc d;
+  const float* bias;
+  float* y32;
+  const float* X;      // target image (BCE) or null
+  __bf16* dlog;
+  float* recon;
+  float* part;         // BCE partials per block
+  float* gpart;        // dlogits partial sums per block (bias gradient)
+  int gx;              // blocks per parity class
+};
+
+template <int CO, int K, int S>
+constexpr int thin_tconv_lds_bytes() { return (16 + (K / S) * (K / S) * CO) * 4; }
+
+// Block `bid` = class * gx + x.
+template <int CO, int K, int S>
+__device__ __forceinline__ void thin_tconv_body(const ThinTconvArgs& ta, uint8_t* lds, int bid) {
+  constexpr int T = K / S;
+  const ConvDesc& d = ta.d;
+  const __bf16* G = ta.G;
+  const float* Wf = ta.Wf;
+  float* scratch = reinterpret_cast<float*>(lds);
+  float* wl = scratch + 16;
+  const int cls = bid / ta.gx, bx = bid - cls * ta.gx;
+  const int ca = cls / S, cb = cls - ca * S;
+  const int oa = ((ca - d.P) % S + S) % S, ob = ((cb - d.P) % S + S) % S;
+  const int ea = (oa + d.P - ca) / S, eb = (ob + d.P - cb) / S;
+  const int HS = d.H / S, WS = d.W / S;
+  const int Mc = d.N * HS * WS;
+  const int m = bx * blockDim.x + threadIdx.x;
+  const bool live = m < Mc;
+  const int mm = live ? m : 0;
+  const int n = mm / (HS * WS);
+  const int rem = mm - n * HS * WS;
+  const int j = rem / WS, i = rem - j * WS;
+  // gather the T*T input rows of CO channels once (16-byte loads)
+  float gv[T * T][CO];
+#pragma unroll
+  for (int ty = 0; ty < T; ++ty)
+#pragma unroll
+    for (int tx = 0; tx < T; ++tx) {
+      const int oy = j + ea - ty, ox = i + eb - tx;
+      const bool ok = live && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
+      const __bf16* g = G + (((size_t)n * d.OH + (ok ? oy : 0)) * d.OW + (ok ? ox : 0)) * CO;
+#pragma unroll
+      for (int c8 = 0; c8 < CO / 8; ++c8) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(g + 8 * c8);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) gv[ty * T + tx][8 * c8 + jj] = ok ? (float)v[jj] : 0.f;
+      }
+    }
+  // this class's T*T taps x CO weights staged in LDS as [tap][co]
+  for (int e = threadIdx.x; e < T * T * CO; e += blockDim.x) {
+    const int tp = e / CO, c = e - tp * CO;
+    const int ky = ca + S * (tp / T), kx = cb + S * (tp % T);
+    wl[e] = Wf[(c * K + ky) * K + kx];
+  }
+  __syncthreads();
+  float acc = ta.bias ? ta.bias[0] : 0.f;
+#pragma unroll
+  for (int tp = 0; tp < T * T; ++tp)
+#pragma unroll
+    for (int c4 = 0; c4 < CO / 4; ++c4) {
+      const float4 w = *reinterpret_cast<const float4*>(wl + tp * CO + 4 * c4);
+      acc = fmaf(gv[tp][4 * c4 + 0], w.x, acc);
+      acc = fmaf(gv[tp][4 * c4 + 1], w.y, acc);
+      acc = fmaf(gv[tp][4 * c4 + 2], w.z, acc);
+      acc = fmaf(gv[tp][4 * c4 + 3], w.w, acc);
+    }
+  const int iy = S * j + oa, ix = S * i + ob;
+  const size_t e = ((size_t)n * d.H + iy) * d.W + ix;
+  if (live && ta.y32) ta.y32[e] = acc;
+  float loss = 0.f, gsum = 0.f;
+  if (ta.X) {
+    if (live) {
+      const float t = acc, x = ta.X[e];
+      const float p = 1.f / (1.f + expf(-t));
+      const float g = p - x;
+      if (ta.dlog) ta.dlog[e] = (__bf16)g;
+      if (ta.recon) ta.recon[e] = p;
+      const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));
+      loss = x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
+      gsum = g;
+    }
+    const int pb = bid;
+    const float s = block_sum(loss, scratch);
+    if (threadIdx.x == 0) ta.part[pb] = s;
+    if (ta.gpart) {
+      __syncthreads();
+      const float gs = block_sum(gsum, scratch);
+      if (threadIdx.x == 0) ta.gpart[pb] = gs;
+    }
+  }
+}
+
+}  // namespace mdt

@@ -41,9 +41,30 @@ int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, mdt::ConvDesc d,
 int mdt_thin_blocks(int tconv, mdt::ConvDesc d);
 int mdt_thin_tconv(const void* G16, const float* Wf, mdt::ConvDesc d, const float* bias, float* y32, const float* X,
                    void* dlog16, float* recon, float* part, float* gpart, hipStream_t s);
+int mdt_job_igemm(mdt::JobBlob* g, mdt::JobBlob* c, int mode, const void* A, int a_is_f32, const void* B16,
+                  mdt::ConvDesc d, const float* bias, int relu, void* y16, float* y32, const void* omask,
+                  float* colsum, float* ws);
+int mdt_job_wgrad(mdt::JobBlob* j, const void* G16, const void* X, int x_is_f32, mdt::ConvDesc d, float* out);
+int mdt_job_thin_conv(mdt::JobBlob* j, const void* X, int x_is_f32, const float* Wf, mdt::ConvDesc d,
+                      const float* bias, int relu, void* y16, const void* omask, float* colsum);
+int mdt_job_colsum(mdt::JobBlob* j, const void* G16, int M, int N, int rows_per, float* slab);
+int mdt_job_loss(mdt::JobBlob* j, const float* bce_part, int nb, const float* kld_part, int nk, void* st,
+                 const void* hp, int advance_cursor);
+int mdt_launch_jobs(const mdt::JobBlob* jobs, int n, hipStream_t s);
+int mdt_launch_job1(const mdt::JobBlob* j, hipStream_t s);
 }
 
 namespace mdt {
+
+// A recorded launch for the horizontally fused job kernels (conv_jobs.hip):
+// the op bindings below take an optional Job; when given, they validate and
+// RECORD the launch into it instead of issuing it. `post` is the dependent
+// follow-up (split-K combine) to launch after the job's own kernel.
+struct Job {
+  JobBlob main{}, post{};
+  int kind() const { return main.kind; }
+  bool has_post() const { return post.kind != 0; }
+};
 
 static hipStream_t cur() { return c10::hip::getCurrentHIPStream().stream(); }
 static void rc(int r, const char* w) { TORCH_CHECK(r == 0, "mdt: ", w, " failed (", r, ")"); }
@@ -87,7 +108,7 @@ std::vector<int64_t> wgrad_plan(const std::vector<int64_t>& dv) {
 void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::vector<int64_t>& dv,
            const c10::optional<at::Tensor>& bias, bool relu, const c10::optional<at::Tensor>& y16,
            const c10::optional<at::Tensor>& y32, const c10::optional<at::Tensor>& omask,
-           const c10::optional<at::Tensor>& colsum, const c10::optional<at::Tensor>& ws) {
+           const c10::optional<at::Tensor>& colsum, const c10::optional<at::Tensor>& ws, Job* job) {
   const ConvDesc d = desc(dv);
   TORCH_CHECK(A.is_cuda() && A.is_contiguous(), "A must be contiguous CUDA");
   const bool f32 = A.scalar_type() == torch::kFloat32;
@@ -106,13 +127,20 @@ void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::
   check_min(bias, Ncols, "bias");
   check_min(colsum, (int64_t)info[11] * Ncols, "colsum");
   if (ksplit > 1) check_min(ws, ksplit * M * Ncols, "ws");
+  if (job) {
+    rc(mdt_job_igemm(&job->main, &job->post, (int)mode, A.data_ptr(), f32, B16.data_ptr(), d,
+                     (const float*)opt_ptr(bias), relu, const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32),
+                     opt_ptr(omask), (float*)opt_ptr(colsum), (float*)opt_ptr(ws)),
+       "job_igemm");
+    return;
+  }
   rc(mdt_igemm((int)mode, A.data_ptr(), f32, B16.data_ptr(), d, (const float*)opt_ptr(bias), relu,
                const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32), opt_ptr(omask), (float*)opt_ptr(colsum),
                (float*)opt_ptr(ws), cur()),
      "igemm");
 }
 
-void wgrad(const at::Tensor& G16, const at::Tensor& X, const std::vector<int64_t>& dv, at::Tensor out) {
+void wgrad(const at::Tensor& G16, const at::Tensor& X, const std::vector<int64_t>& dv, at::Tensor out, Job* job) {
   const ConvDesc d = desc(dv);
   check_bf16(G16, "G16");
   check_f32(out, "out");
@@ -124,6 +152,10 @@ void wgrad(const at::Tensor& G16, const at::Tensor& X, const std::vector<int64_t
   TORCH_CHECK(X.numel() >= (int64_t)d.N * d.H * d.W * d.C, "X too small");
   TORCH_CHECK(out.numel() >= (int64_t)info[6] * d.CO * d.KH * d.KW * d.C, "wgrad out too small for ", info[6],
               " partial slabs");
+  if (job) {
+    rc(mdt_job_wgrad(&job->main, G16.data_ptr(), X.data_ptr(), f32, d, out.data_ptr<float>()), "job_wgrad");
+    return;
+  }
   rc(mdt_wgrad(G16.data_ptr(), X.data_ptr(), f32, d, out.data_ptr<float>(), cur()), "wgrad");
 }
 
@@ -131,7 +163,7 @@ void wgrad(const at::Tensor& G16, const at::Tensor& X, const std::vector<int64_t
 // [CO][KH][KW][1] (read with wave-uniform scalar loads).
 void thin_conv(const at::Tensor& X, const at::Tensor& Wf, const std::vector<int64_t>& dv,
                const c10::optional<at::Tensor>& bias, bool relu, at::Tensor y16,
-               const c10::optional<at::Tensor>& omask, const c10::optional<at::Tensor>& colsum) {
+               const c10::optional<at::Tensor>& omask, const c10::optional<at::Tensor>& colsum, Job* job) {
   const ConvDesc d = desc(dv);
   const bool f32 = X.scalar_type() == torch::kFloat32;
   TORCH_CHECK(X.is_cuda() && X.is_contiguous() && (f32 || X.scalar_type() == torch::kBFloat16), "X dtype/layout");
@@ -144,6 +176,12 @@ void thin_conv(const at::Tensor& X, const at::Tensor& Wf, const std::vector<int6
   check_min(omask, M * d.CO, "omask");
   check_min(colsum, (int64_t)mdt_thin_blocks(0, d) * d.CO, "colsum");
   check_min(bias, d.CO, "bias");
+  if (job) {
+    rc(mdt_job_thin_conv(&job->main, X.data_ptr(), f32, Wf.data_ptr<float>(), d, (const float*)opt_ptr(bias), relu,
+                         y16.data_ptr(), opt_ptr(omask), (float*)opt_ptr(colsum)),
+       "job_thin_conv");
+    return;
+  }
   rc(mdt_thin_conv(X.data_ptr(), f32, Wf.data_ptr<float>(), d, (const float*)opt_ptr(bias), relu, y16.data_ptr(),
                    opt_ptr(omask), (float*)opt_ptr(colsum), cur()),
      "thin_conv");
@@ -175,11 +213,15 @@ void thin_tconv(const at::Tensor& G16, const at::Tensor& Wf, const std::vector<i
      "thin_tconv");
 }
 
-void colsum(const at::Tensor& G16, int64_t M, int64_t N, int64_t rows_per, at::Tensor slab) {
+void colsum(const at::Tensor& G16, int64_t M, int64_t N, int64_t rows_per, at::Tensor slab, Job* job) {
   check_bf16(G16, "G16");
   check_f32(slab, "slab");
   TORCH_CHECK(G16.numel() >= M * N, "G16 too small");
   TORCH_CHECK(slab.numel() >= ((M + rows_per - 1) / rows_per) * N, "colsum slab too small");
+  if (job) {
+    rc(mdt_job_colsum(&job->main, G16.data_ptr(), (int)M, (int)N, (int)rows_per, slab.data_ptr<float>()), "job_colsum");
+    return;
+  }
   rc(mdt_colsum(G16.data_ptr(), (int)M, (int)N, (int)rows_per, slab.data_ptr<float>(), cur()), "colsum");
 }
 
@@ -215,10 +257,34 @@ void bce_logits(const at::Tensor& logits, const at::Tensor& X, const c10::option
 }
 
 void loss_finalize2(const at::Tensor& bce_part, int64_t nb, const at::Tensor& kld_part, int64_t nk, at::Tensor state,
-                    const at::Tensor& hparams, bool advance_cursor) {
+                    const at::Tensor& hparams, bool advance_cursor, Job* job) {
+  if (job) {
+    rc(mdt_job_loss(&job->main, bce_part.data_ptr<float>(), (int)nb, kld_part.data_ptr<float>(), (int)nk,
+                    state.data_ptr(), hparams.data_ptr(), advance_cursor ? 1 : 0),
+       "job_loss");
+    return;
+  }
   rc(mdt_conv_loss_finalize(bce_part.data_ptr<float>(), (int)nb, kld_part.data_ptr<float>(), (int)nk,
                             state.data_ptr(), hparams.data_ptr(), advance_cursor ? 1 : 0, cur()),
      "loss_finalize");
+}
+
+// Launch recorded jobs as ONE fused kernel when an instantiation exists for
+// their kinds (returns true), else launch nothing and return false (the caller
+// then issues the ops' own kernels). Follow-up combines run right after.
+bool launch_jobs(const std::vector<Job*>& jobs) {
+  TORCH_CHECK(jobs.size() >= 2 && jobs.size() <= 3, "launch_jobs takes 2 or 3 jobs");
+  JobBlob v[3];
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    TORCH_CHECK(jobs[i] != nullptr, "null job");
+    v[i] = jobs[i]->main;
+  }
+  const int r = mdt_launch_jobs(v, (int)jobs.size(), cur());
+  TORCH_CHECK(r >= 0 && r != 2, "mdt: launch_jobs failed (", r, ")");
+  if (r != 0) return false;
+  for (auto* j : jobs)
+    if (j->has_post()) rc(mdt_launch_job1(&j->post, cur()), "job follow-up");
+  return true;
 }
 
 void step_begin(at::Tensor state, const at::Tensor& hparams) {
@@ -359,13 +425,19 @@ void bind_conv(pybind11::module& m) {
   namespace py = pybind11;
   m.def("igemm_plan", &igemm_plan);
   m.def("wgrad_plan", &wgrad_plan);
+  py::class_<Job>(m, "Job")
+      .def(py::init<>())
+      .def_property_readonly("kind", &Job::kind)
+      .def_property_readonly("has_post", &Job::has_post);
+  m.def("launch_jobs", &launch_jobs);
   m.def("igemm", &igemm, py::arg("mode"), py::arg("A"), py::arg("B16"), py::arg("desc"), py::arg("bias"),
         py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),
-        py::arg("colsum") = py::none(), py::arg("ws") = py::none());
-  m.def("wgrad", &wgrad);
-  m.def("colsum", &colsum);
+        py::arg("colsum") = py::none(), py::arg("ws") = py::none(), py::arg("job") = py::none());
+  m.def("wgrad", &wgrad, py::arg("G16"), py::arg("X"), py::arg("desc"), py::arg("out"), py::arg("job") = py::none());
+  m.def("colsum", &colsum, py::arg("G16"), py::arg("M"), py::arg("N"), py::arg("rows_per"), py::arg("slab"),
+        py::arg("job") = py::none());
   m.def("thin_conv", &thin_conv, py::arg("X"), py::arg("Wf"), py::arg("desc"), py::arg("bias"), py::arg("relu"),
-        py::arg("y16"), py::arg("omask") = py::none(), py::arg("colsum") = py::none());
+        py::arg("y16"), py::arg("omask") = py::none(), py::arg("colsum") = py::none(), py::arg("job") = py::none());
   m.def("thin_blocks", &thin_blocks);
   m.def("thin_tconv", &thin_tconv, py::arg("G16"), py::arg("Wf"), py::arg("desc"), py::arg("bias"),
         py::arg("y32") = py::none(), py::arg("X") = py::none(), py::arg("dlog16") = py::none(),
@@ -375,7 +447,8 @@ void bind_conv(pybind11::module& m) {
   m.def("reparam_bwd", &reparam_bwd);
   m.def("bce_logits", &bce_logits, py::arg("logits"), py::arg("X"), py::arg("rows"), py::arg("B"), py::arg("P"),
         py::arg("dlog16"), py::arg("recon"), py::arg("part"), py::arg("gpart") = py::none());
-  m.def("loss_finalize2", &loss_finalize2);
+  m.def("loss_finalize2", &loss_finalize2, py::arg("bce_part"), py::arg("nb"), py::arg("kld_part"), py::arg("nk"),
+        py::arg("state"), py::arg("hparams"), py::arg("advance_cursor"), py::arg("job") = py::none());
   m.def("step_begin", &step_begin);
   m.def("make_grad_segs", &make_grad_segs);
   m.def("make_grad_units", &make_grad_units);

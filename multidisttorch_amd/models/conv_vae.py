@@ -26,6 +26,7 @@ backend and the numerical oracle of the GPU tests.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -223,6 +224,14 @@ class ConvVaeTrainer:
         self.graph_steps = max(1, graph_steps)
         self._graphs = {}
         self.reducer = None
+        # two-stream backward (see _backward_overlap), opt-in with MDT_CONV_OVERLAP=1: measured
+        # slower on MI355X (conv28 0.180 -> 0.277 ms/step) -- cross-stream graph edges cost more
+        # than the overlap recovers
+        self.overlap = self.device.type == "cuda" and os.getenv("MDT_CONV_OVERLAP", "0") == "1"
+        # horizontal fusion of independent backward launches (conv_jobs.hip);
+        # MDT_CONV_JOBS=0 issues every op as its own kernel (A/B, bitwise equal)
+        self.fuse_jobs = os.getenv("MDT_CONV_JOBS", "1") != "0"
+        self._fused_launches = 0
         self._data = None
         torch.manual_seed(self.seed if init_seed is None else init_seed)
         ref = TorchConvVAE(self.spec, image, channels, z)
@@ -395,7 +404,10 @@ class ConvVaeTrainer:
         self.segs = self.C.make_grad_segs(rows, dev.index or 0)
         self.nseg = 2 * len(self.spec)
         tr = []
+        self._tr_layer = []  # layer li owns transpose units [_tr_layer[li], _tr_layer[li + 1])
         for si, r in enumerate(rows):
+            if si % 2 == 0:
+                self._tr_layer.append(len(tr))
             if r[8] < 0:
                 continue
             co, k, ci = r[4], r[5], r[7]
@@ -403,6 +415,7 @@ class ConvVaeTrainer:
                 for co0 in range(0, co, 64):
                     for ci0 in range(0, ci, 64):
                         tr.append([si, tap, co0, ci0])
+        self._tr_layer.append(len(tr))
         self.tr_units = self.C.make_tr_units(tr, dev.index or 0)
         self.n_tr = len(tr)
         self.xb = torch.zeros(B, self.D, **f32)
@@ -610,19 +623,42 @@ class ConvVaeTrainer:
         C.bce_logits(self.logits, self.xb, None, M, self.D, self.dlog16 if train else None,
                      self.recon if want_recon else None, self.bce_part, p["gpart"] if train else None)
 
-    def _backward_hip(self, M):
+    def _run_group(self, fns):
+        """Run independent launches ``fns`` (each ``f(job)``): recorded as jobs
+        and issued as ONE fused kernel when conv_jobs.hip has an instantiation
+        for their kinds, else each op's own kernel (same bodies, same results)."""
+        if self.fuse_jobs and 1 < len(fns) <= 3:
+            jobs = [self.C.Job() for _ in fns]
+            for f, j in zip(fns, jobs):
+                f(j)
+            if all(j.kind > 0 for j in jobs) and self.C.launch_jobs(jobs):
+                self._fused_launches += 1
+                return
+        for f in fns:
+            f(None)
+
+    def _backward_hip(self, M, with_loss=False):
         """Reverse sweep: per layer one weight-gradient GEMM (partial slabs) and
         one backward-data GEMM whose epilogue applies the previous layer's ReLU
-        mask and emits its bias-gradient column sums."""
+        mask and emits its bias-gradient column sums. The two (plus any bias
+        column sum or loss reduction that became ready) are independent and
+        share one launch (``_run_group``). ``with_loss`` adds the loss reduction
+        of the forward to the first launch."""
         C = self.C
         p = self._plan(M)
         spec = self.spec
+        st = self.state
         g = self.dlog16
         red = self.reducer
         if red is not None:
             bounds = list(red.bounds())
             starts = {b: i for i, (l, b, e) in enumerate(self.layer_ranges())}
             assert all(b in starts or b == self.numel for b in bounds), "bucket bounds must fall on layer starts"
+        carry = []  # launches that depend on the previous group's outputs
+        if with_loss:
+            carry.append(lambda job: C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part,
+                                                      -(-M * self.Z // 256), st.train_state, st.hparams, True,
+                                                      job=job))
         for i in range(len(spec) - 1, -1, -1):
             if red is not None and i + 1 < len(spec):
                 self._maybe_launch_bucket(red, bounds, starts, i + 1, M)
@@ -637,30 +673,47 @@ class ConvVaeTrainer:
                 a_in = self.acts[prev.name]
             wslab = p["slabs"].get(l.name + ".weight")
             wout = wslab[0] if wslab is not None else self._gw(l)
+            fns, carry, after = carry, [], []
             if l.kind == "convT":  # conv view: output = convT input, input = convT output
-                C.wgrad(a_in, g, d, wout)
+                fns.append(lambda job, a_in=a_in, g=g, d=d, wout=wout: C.wgrad(a_in, g, d, wout, job=job))
             else:
-                C.wgrad(g, a_in, d, wout)
+                fns.append(lambda job, a_in=a_in, g=g, d=d, wout=wout: C.wgrad(g, a_in, d, wout, job=job))
+            gin = None
+            if prev is not None:
+                omask = a_in if prev.relu else None
+                if l.name == "dec_fc":
+                    fns.append(lambda job, g=g, l=l, d=d: C.igemm(1, g, self._wt(l), d, None, False, None, self.dz,
+                                                                  ws=p["ws"], job=job))
+                    after.append(lambda: C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M,
+                                                       self.Z, st.hparams))
+                    cso = p["colsum"][prev.name]
+                    carry.append(lambda job, cso=cso: C.colsum(self.dmulv16, M, 2 * self.Z, p["rows_per"], cso,
+                                                               job=job))
+                    gin = self.dmulv16
+                elif i == len(spec) - 1 and self._thin_last:
+                    gin = self.gacts[prev.name]
+                    cso = p["colsum"][prev.name]
+                    fns.append(lambda job, g=g, l=l, d=d, gin=gin, omask=omask, cso=cso:
+                               C.thin_conv(g, self._wf32(l), d, None, False, gin, omask, cso, job=job))
+                else:
+                    gin = self.gacts[prev.name]
+                    cs = None if prev.name == "dec_fc" else p["colsum"].get(prev.name)
+                    mode = 0 if l.kind == "convT" else 1
+                    w = self._w(l) if l.kind == "convT" else self._wt(l)
+                    fns.append(lambda job, g=g, w=w, d=d, gin=gin, omask=omask, cs=cs, mode=mode:
+                               C.igemm(mode, g, w, d, None, False, gin, None, omask, cs, job=job))
+                    if prev.name == "dec_fc":
+                        cso = p["colsum"][prev.name]
+                        carry.append(lambda job, gin=gin, n=prev.cout, cso=cso:
+                                     C.colsum(gin, M, n, p["rows_per"], cso, job=job))
+            self._run_group(fns)
+            for f in after:
+                f()
             if prev is None:
+                assert not carry
                 if red is not None:
                     self._maybe_launch_bucket(red, bounds, starts, 0, M)
                 break
-            omask = a_in if prev.relu else None
-            if l.name == "dec_fc":
-                C.igemm(1, g, self._wt(l), d, None, False, None, self.dz, ws=p["ws"])
-                C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M, self.Z, self.state.hparams)
-                C.colsum(self.dmulv16, M, 2 * self.Z, p["rows_per"], p["colsum"][prev.name])
-                gin = self.dmulv16
-            elif i == len(spec) - 1 and self._thin_last:
-                gin = self.gacts[prev.name]
-                C.thin_conv(g, self._wf32(l), d, None, False, gin, omask, p["colsum"][prev.name])
-            else:
-                gin = self.gacts[prev.name]
-                cs = None if prev.name == "dec_fc" else p["colsum"].get(prev.name)
-                C.igemm(0 if l.kind == "convT" else 1, g, self._w(l) if l.kind == "convT" else self._wt(l), d,
-                        None, False, gin, None, omask, cs)
-                if prev.name == "dec_fc":
-                    C.colsum(gin, M, prev.cout, p["rows_per"], p["colsum"][prev.name])
             g = gin
 
     def _maybe_launch_bucket(self, red, bounds, starts, i, M):
@@ -687,9 +740,12 @@ class ConvVaeTrainer:
         C.step_begin(st.train_state, st.hparams)
         C.gather_rows(X, idx, st.train_state, self.B, M, self.xb)
         self._forward_hip(M, st.train_state, self.rng_stream)
-        C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, -(-M * self.Z // 256),
-                         st.train_state, st.hparams, True)
-        self._backward_hip(M)  # with a reducer: finalizes + launches each bucket as it completes
+        if self.reducer is None and self.overlap:
+            self._backward_overlap(M)
+            return
+        # loss reduction rides in the backward's first launch; with a reducer the
+        # backward finalizes + launches each bucket as it completes
+        self._backward_hip(M, with_loss=True)
         if self.reducer is not None:
             self.reducer.wait_all()
             C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
@@ -697,6 +753,89 @@ class ConvVaeTrainer:
         else:
             self._finalize_grads(M, True)
         self._transpose_weights()
+
+    # layer groups whose gradients are finalized together (optimizer + bf16
+    # re-cast + transposed copies) on the side stream once the backward-data
+    # sweep has passed them; the last group's launches end the step.
+    FINALIZE_GROUPS = {28: ("dec_fc", "enc2", "enc1"), 128: ("dec2", "dec_fc", "enc3", "enc2", "enc1")}
+
+    def _side_stream(self):
+        s = getattr(self, "_side", None)
+        if s is None:
+            s = self._side = torch.cuda.Stream(self.device)
+        return s
+
+    def _backward_overlap(self, M):
+        """Backward with two streams (both captured into the step graph as
+        parallel branches). The main stream runs only the backward-data chain
+        (the critical path); the side stream runs every weight-gradient GEMM,
+        the bias column sums, the loss reduction and -- per layer group, as soon
+        as the chain no longer reads those weights -- the gradient finalize +
+        fused Adam + bf16 cast and the transposed weight copies. Same kernels,
+        same arithmetic and the same deterministic reduction order as the
+        sequential path; only the launch order across streams changes."""
+        C = self.C
+        p = self._plan(M)
+        spec = self.spec
+        st = self.state
+        main = torch.cuda.current_stream(self.device)
+        side = self._side_stream()
+        names = [l.name for l in spec]
+        cut = {names.index(n) for n in self.FINALIZE_GROUPS.get(self.image, ("enc1",)) if n in names}
+        cut.add(0)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, -(-M * self.Z // 256),
+                             st.train_state, st.hparams, True)
+        g = self.dlog16
+        hi = len(spec)  # layers [i, hi) wait for their finalize
+        for i in range(len(spec) - 1, -1, -1):
+            l = spec[i]
+            prev = spec[i - 1] if i > 0 else None
+            d = self._desc(l, M)
+            a_in = self.xb if i == 0 else (self.z16 if l.name == "dec_fc" else self.acts[prev.name])
+            wslab = p["slabs"].get(l.name + ".weight")
+            wout = wslab[0] if wslab is not None else self._gw(l)
+            with torch.cuda.stream(side):
+                if l.kind == "convT":
+                    C.wgrad(a_in, g, d, wout)
+                else:
+                    C.wgrad(g, a_in, d, wout)
+            side_cs = []
+            if prev is not None:
+                omask = a_in if prev.relu else None
+                if l.name == "dec_fc":
+                    C.igemm(1, g, self._wt(l), d, None, False, None, self.dz, ws=p["ws"])
+                    C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M, self.Z,
+                                  st.hparams)
+                    gin = self.dmulv16
+                    side_cs.append((gin, 2 * self.Z, p["colsum"][prev.name]))
+                elif i == len(spec) - 1 and self._thin_last:
+                    gin = self.gacts[prev.name]
+                    C.thin_conv(g, self._wf32(l), d, None, False, gin, omask, p["colsum"][prev.name])
+                else:
+                    gin = self.gacts[prev.name]
+                    cs = None if prev.name == "dec_fc" else p["colsum"].get(prev.name)
+                    C.igemm(0 if l.kind == "convT" else 1, g, self._w(l) if l.kind == "convT" else self._wt(l), d,
+                            None, False, gin, None, omask, cs)
+                    if prev.name == "dec_fc":
+                        side_cs.append((gin, prev.cout, p["colsum"][prev.name]))
+                g = gin
+            side.wait_stream(main)  # layer i's backward-data is done: its weights are free to update
+            with torch.cuda.stream(side):
+                for t, n, out in side_cs:
+                    C.colsum(t, M, n, p["rows_per"], out)
+                if i in cut:
+                    u0, u1 = p["layer_units"][i], p["layer_units"][hi]
+                    C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"],
+                                    p["units"].narrow(0, u0 * 12, (u1 - u0) * 12), u1 - u0, st.train_state,
+                                    st.hparams, True)
+                    t0, t1 = self._tr_layer[i], self._tr_layer[hi]
+                    if t1 > t0:
+                        C.wtrans(self.w16, self.w16t, self.segs, self.tr_units.narrow(0, t0 * 16, (t1 - t0) * 16),
+                                 t1 - t0)
+                    hi = i
+        main.wait_stream(side)
 
     def _finalize_grads(self, M, do_adam):
         """Reduce the partial slabs into the gradient arena (deterministic order);
