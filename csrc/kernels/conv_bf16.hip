@@ -138,83 +138,25 @@ __global__ void __launch_bounds__(256) adam_cast_k(float* P, const float* G, flo
   }
 }
 
-// One unit = `count` consecutive elements of one segment. Threads t = rl*count
-// + col sum partial rows rl, rl+rp, ... (rp = 512/count) of column col, then
-// row lane 0 adds the rp sums in order: a fixed reduction tree, so results are
-// bitwise reproducible (unlike f32 atomics). With do_adam the same thread
-// applies Adam to the parameter and re-emits its bf16 copy.
-__global__ void __launch_bounds__(512) grad_finalize_k(float* P, float* G, float* Mo, float* Vo, __bf16* w16,
-                                                       const GradSeg* segs, const GradUnit* units,
-                                                       const TrainState* st, const HParams* hp, int do_adam) {
-  __shared__ float red[512];
+__global__ void __launch_bounds__(kFinalizeThreads) grad_finalize_k(FinalizeArgs fa) {
+  __shared__ float red[kFinalizeThreads];
   __shared__ AdamC cs;
-  AdamC c{};
-  if (do_adam) c = adam_consts_block(st, hp, &cs);
-  const GradUnit u = units[blockIdx.x];
-  const GradSeg sg = segs[u.seg];
-  const int t = threadIdx.x, cnt = u.count, rp = 512 / cnt;
-  const int col = t % cnt, rl = t / cnt;
-  float acc = 0.f;
-  if (sg.slab && rl < rp) {
-    const float* p = sg.slab + u.start + col;
-    const long long n = sg.numel;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int s = rl;
-    for (; s + 3 * rp < sg.nsplit; s += 4 * rp) {
-      a0 += p[(long long)s * n];
-      a1 += p[(long long)(s + rp) * n];
-      a2 += p[(long long)(s + 2 * rp) * n];
-      a3 += p[(long long)(s + 3 * rp) * n];
-    }
-    for (; s < sg.nsplit; s += rp) a0 += p[(long long)s * n];
-    acc = (a0 + a1) + (a2 + a3);
-  }
-  red[t] = acc;
-  __syncthreads();
-  if (rl == 0) {
-    const long long o = sg.off + u.start + col;
-    float g;
-    if (sg.slab) {
-      g = 0.f;
-      for (int r = 0; r < rp; ++r) g += red[r * cnt + col];
-      if (!do_adam) G[o] = g;  // the fused-Adam path consumes g in registers only
-    } else {
-      g = G[o];
-    }
-    if (do_adam) {
-      float p = P[o], m = Mo[o], v = Vo[o];
-      adam_update(p, m, v, g, c);
-      P[o] = p; Mo[o] = m; Vo[o] = v;
-      w16[o] = (__bf16)p;
-    }
-  }
+  grad_finalize_body(fa, red, &cs, blockIdx.x);
 }
 
-// bf16 weights [CO][k][k][CI] -> parity-ordered transpose [s][s][CI][k/s][k/s][CO]
-// (class (a, b) holds taps ky = a + s*ty, kx = b + s*tx) for the kModeTconv
-// GEMM. One 64x64 (co, ci) tile of one tap per block, staged through LDS so
-// both the read (ci-contiguous) and the write (co-contiguous) are coalesced.
-__global__ void __launch_bounds__(256) wtrans_k(const __bf16* w16, __bf16* w16t, const GradSeg* segs,
-                                                const TrUnit* units) {
-  __shared__ unsigned short tile[64][66];
-  const TrUnit u = units[blockIdx.x];
-  const GradSeg sg = segs[u.seg];
-  const int k = sg.k, s = sg.s, CI = sg.ci, CO = sg.co, T = k / s;
-  const int ky = u.tap / k, kx = u.tap - ky * k;
-  const int a = ky % s, ty = ky / s, b = kx % s, tx = kx / s;
-  const unsigned short* src = reinterpret_cast<const unsigned short*>(w16) + sg.off;
-  unsigned short* dst = reinterpret_cast<unsigned short*>(w16t) + sg.toff;
-  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
-    const int r = idx >> 6, c = idx & 63;
-    const int co = u.co0 + r, ci = u.ci0 + c;
-    if (co < CO && ci < CI) tile[r][c] = src[((long long)(co * k + ky) * k + kx) * CI + ci];
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
-    const int r = idx >> 6, c = idx & 63;
-    const int ci = u.ci0 + r, co = u.co0 + c;
-    if (co < CO && ci < CI) dst[((((long long)(a * s + b) * CI + ci) * T + ty) * T + tx) * CO + co] = tile[c][r];
-  }
+__global__ void __launch_bounds__(256) wtrans_k(WtransArgs wa) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWtransLds];
+  wtrans_body(wa, lds, blockIdx.x);
+}
+
+__global__ void __launch_bounds__(256) combine_reparam_k(CombineReparamArgs a) {
+  __shared__ float red[2 * 256 + 16];
+  combine_reparam_body(a, red, blockIdx.x);
+}
+
+__global__ void __launch_bounds__(256) combine_reparam_bwd_k(CombineReparamBwdArgs a) {
+  __shared__ float red[256];
+  combine_reparam_bwd_body(a, red, blockIdx.x);
 }
 
 }  // namespace mdt
@@ -285,18 +227,38 @@ int mdt_adam_cast(float* P, const float* G, float* Mo, float* Vo, void* w16, con
 int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs, const void* units,
                       int nunits, const void* st, const void* hp, int do_adam, hipStream_t s) {
   if (nunits <= 0) return 0;
-  hipLaunchKernelGGL(grad_finalize_k, dim3(nunits), dim3(512), 0, s, P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16),
-                     reinterpret_cast<const GradSeg*>(segs), reinterpret_cast<const GradUnit*>(units),
-                     reinterpret_cast<const TrainState*>(st), reinterpret_cast<const HParams*>(hp), do_adam);
+  const FinalizeArgs fa{P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16), reinterpret_cast<const GradSeg*>(segs),
+                        reinterpret_cast<const GradUnit*>(units), reinterpret_cast<const TrainState*>(st),
+                        reinterpret_cast<const HParams*>(hp), do_adam};
+  hipLaunchKernelGGL(grad_finalize_k, dim3(nunits), dim3(kFinalizeThreads), 0, s, fa);
   return (int)hipGetLastError();
 }
 
 int mdt_wtrans(const void* w16, void* w16t, const void* segs, const void* units, int nunits, hipStream_t s) {
   if (nunits <= 0) return 0;
-  hipLaunchKernelGGL(wtrans_k, dim3(nunits), dim3(256), 0, s, reinterpret_cast<const __bf16*>(w16),
-                     reinterpret_cast<__bf16*>(w16t), reinterpret_cast<const GradSeg*>(segs),
-                     reinterpret_cast<const TrUnit*>(units));
+  const WtransArgs wa{reinterpret_cast<const __bf16*>(w16), reinterpret_cast<__bf16*>(w16t),
+                      reinterpret_cast<const GradSeg*>(segs), reinterpret_cast<const TrUnit*>(units)};
+  hipLaunchKernelGGL(wtrans_k, dim3(nunits), dim3(256), 0, s, wa);
   return (int)hipGetLastError();
 }
+
+int mdt_combine_reparam(const float* slab, int ks, const float* bias, float* mulv, float* eps, void* z16, float* z32,
+                        int B, int Z, const void* st, const void* hp, unsigned stream, float* kld_part, hipStream_t s) {
+  const CombineReparamArgs a{slab, ks, splitk_rp(ks), bias, mulv, eps, reinterpret_cast<__bf16*>(z16), z32, B, Z,
+                             reinterpret_cast<const TrainState*>(st), reinterpret_cast<const HParams*>(hp),
+                             (uint32_t)stream, kld_part};
+  hipLaunchKernelGGL(combine_reparam_k, dim3(combine_reparam_blocks(ks, B, Z)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int mdt_combine_reparam_bwd(const float* slab, int ks, const float* mulv, const float* eps, float* dmulv,
+                            void* dmulv16, float* dz, int B, int Z, const void* hp, hipStream_t s) {
+  const CombineReparamBwdArgs a{slab, ks, splitk_rp(ks), mulv, eps, dmulv, reinterpret_cast<__bf16*>(dmulv16), dz, B,
+                                Z, reinterpret_cast<const HParams*>(hp)};
+  hipLaunchKernelGGL(combine_reparam_bwd_k, dim3(combine_reparam_blocks(ks, B, Z)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int mdt_combine_reparam_blocks(int ks, int B, int Z) { return combine_reparam_blocks(ks, B, Z); }
 
 }  // extern "C"

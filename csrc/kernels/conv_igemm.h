@@ -106,6 +106,8 @@ enum JobKindBase : int {
   kJobColsum = 5000,
   kJobLoss = 5001,
   kJobCombine = 5002,
+  kJobFinalize = 5003,
+  kJobWtrans = 5004,
 };
 
 }  // namespace mdt

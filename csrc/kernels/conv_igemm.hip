@@ -70,7 +70,13 @@ bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p) {
   q.mtiles = cdiv(q.M, q.BM);
   const long long blocks = (long long)q.classes * q.mtiles * q.ntiles;
   q.ksplit = 1;
-  if (allow_split && q.classes == 1 && blocks < 256 && q.ktiles >= 8) {
+  // split-K only for deep problems: at 8-15 k-tiles the extra combine launch
+  // costs more than the under-filled grid (conv28 enc2: 98 blocks x 8 k-tiles)
+  static const int min_kt = [] {
+    const char* e = getenv("MDT_CONV_SPLIT_MIN_KT");
+    return e ? atoi(e) : 16;
+  }();
+  if (allow_split && q.classes == 1 && blocks < 256 && q.ktiles >= min_kt) {
     int ks = cdiv(512, blocks);
     if (ks > q.ktiles / 4) ks = q.ktiles / 4;
     if (ks < 1) ks = 1;
@@ -275,7 +281,7 @@ int mdt_wgrad_plan(ConvDesc d, int* info) {
 // for deep, narrow problems (then bias/relu/y16/y32 are applied by a combine
 // pass; omask/colsum are not allowed with split-K).
 int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d, const float* bias, int relu,
-              void* y16, float* y32, const void* omask, float* colsum, float* ws, hipStream_t s) {
+              void* y16, float* y32, const void* omask, float* colsum, float* ws, int skip_combine, hipStream_t s) {
   IgArgs a;
   FwdPlan q;
   CombineArgs c;
@@ -293,7 +299,7 @@ int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d
     rc = use_glds() ? dispatch_glds<kModeTconv>(a, q, s) : dispatch_fwd_cfg<kModeTconv, __bf16, true>(a, q, s);
   }
   if (rc) return rc;
-  if (nc > 0) hipLaunchKernelGGL(splitk_combine_k, dim3(nc), dim3(256), 0, s, c);
+  if (nc > 0 && !skip_combine) hipLaunchKernelGGL(splitk_combine_k, dim3(nc), dim3(256), 0, s, c);
   return (int)hipGetLastError();
 }
 

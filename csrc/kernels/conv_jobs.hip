@@ -91,6 +91,21 @@ struct JLoss {
   }
 };
 
+struct JFinalize {
+  static constexpr int ID = kJobFinalize, LDS = kFinalizeThreads * 4 + 64;
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    grad_finalize_body(job_args<FinalizeArgs>(j), reinterpret_cast<float*>(lds),
+                       reinterpret_cast<AdamC*>(lds + kFinalizeThreads * 4), b);
+  }
+};
+
+struct JWtrans {
+  static constexpr int ID = kJobWtrans, LDS = kWtransLds;
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    wtrans_body(job_args<WtransArgs>(j), lds, b);
+  }
+};
+
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 template <class A, class B, class C>
@@ -124,6 +139,7 @@ struct Combo {
 #define COMBO2(A, B) {A::ID, B::ID, 0, &launch_pack<A, B, JNone>}
 
 using WgT5 = JWgThin<__bf16, 5, W5>;
+using WgT5f = JWgThin<float, 5, W5>;
 using ThinC32 = JThinConv<32, __bf16>;
 using Wg0 = JWg<0, W0>;
 using Wg1 = JWg<1, W1>;
@@ -156,6 +172,10 @@ const Combo kCombos[] = {
     COMBO2(IgT1, Wg0),
     COMBO2(IgT2, Wg0),
     COMBO2(IgT5, Wg0),
+    // optimizer tail: first-layer weight gradient || finalize+Adam of every
+    // other layer; then first-layer finalize || transposed weight copies
+    COMBO2(WgT5f, JFinalize),
+    COMBO2(JFinalize, JWtrans),
 };
 
 #undef COMBO3
@@ -178,7 +198,8 @@ extern "C" {
 // job (`c`, kind kJobCombine, to run after `g`), else c->kind = 0. g->kind = 0
 // when the GEMM has no job form (f32 / per-element gathers, LDS-DMA path).
 int mdt_job_igemm(JobBlob* g, JobBlob* c, int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d,
-                  const float* bias, int relu, void* y16, float* y32, const void* omask, float* colsum, float* ws) {
+                  const float* bias, int relu, void* y16, float* y32, const void* omask, float* colsum, float* ws,
+                  int skip_combine) {
   IgArgs a;
   FwdPlan q;
   CombineArgs cb;
@@ -192,7 +213,7 @@ int mdt_job_igemm(JobBlob* g, JobBlob* c, int mode, const void* A, int a_is_f32,
   g->aux[0] = q.mtiles * q.ntiles;
   g->aux[1] = q.ksplit;
   put_args(g, a);
-  if (nc > 0) {
+  if (nc > 0 && !skip_combine) {
     c->kind = kJobCombine;
     c->nblk = nc;
     put_args(c, cb);
@@ -220,7 +241,7 @@ int mdt_job_thin_conv(JobBlob* j, const void* X, int x_is_f32, const float* Wf, 
   j->kind = ok ? kJobThinConv + d.CO + (x_is_f32 ? 100 : 0) : 0;
   j->nblk = cdivj((long long)d.N * d.OH * d.OW, 256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
-                        colsum};
+                        colsum, nullptr, nullptr, nullptr, 0, nullptr, j->nblk};
   put_args(j, ta);
   return 0;
 }
@@ -242,6 +263,28 @@ int mdt_job_loss(JobBlob* j, const float* bce_part, int nb, const float* kld_par
   j->nblk = 1;
   put_args(j, LossArgs{bce_part, nb, kld_part, nk, reinterpret_cast<TrainState*>(st),
                        reinterpret_cast<const HParams*>(hp), advance_cursor});
+  return 0;
+}
+
+int mdt_job_finalize(JobBlob* j, float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs,
+                     const void* units, int nunits, const void* st, const void* hp, int do_adam) {
+  memset(j, 0, sizeof(*j));
+  if (nunits <= 0) return 1;
+  j->kind = kJobFinalize;
+  j->nblk = nunits;
+  put_args(j, FinalizeArgs{P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16), reinterpret_cast<const GradSeg*>(segs),
+                           reinterpret_cast<const GradUnit*>(units), reinterpret_cast<const TrainState*>(st),
+                           reinterpret_cast<const HParams*>(hp), do_adam});
+  return 0;
+}
+
+int mdt_job_wtrans(JobBlob* j, const void* w16, void* w16t, const void* segs, const void* units, int nunits) {
+  memset(j, 0, sizeof(*j));
+  if (nunits <= 0) return 1;
+  j->kind = kJobWtrans;
+  j->nblk = nunits;
+  put_args(j, WtransArgs{reinterpret_cast<const __bf16*>(w16), reinterpret_cast<__bf16*>(w16t),
+                         reinterpret_cast<const GradSeg*>(segs), reinterpret_cast<const TrUnit*>(units)});
   return 0;
 }
 

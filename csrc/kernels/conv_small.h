@@ -1,7 +1,9 @@
 // Device bodies of the small conv-VAE step kernels that also run as jobs of
 // the horizontally fused launches (conv_igemm.hip, "job kernels").
 #pragma once
+#include "adam_common.h"
 #include "common.h"
+#include "conv_igemm.h"
 #include "vae_mlp.h"
 
 namespace mdt {
@@ -36,6 +38,224 @@ __device__ __forceinline__ void loss_finalize_body(const LossArgs& la, float* sc
       if (st->nbatches > 0 && c >= st->nbatches) c = 0;
       st->cursor = c;
     }
+  }
+}
+
+// Split-K combines fused with the reparameterisation (forward) and its
+// backward. A block owns cnt = 256/rp consecutive latent elements e = i*Z + c;
+// rp threads per element sum the interleaved k-slices z = r, r+rp, ... (loads
+// in flight in parallel), and the element's lane adds the rp partials in order
+// (deterministic, same tree as splitk_combine_body).
+__host__ __device__ inline int splitk_rp(int ks) {
+  int rp = 1;
+  while (rp < 64 && rp * 4 < ks) rp *= 2;
+  return rp;
+}
+__host__ __device__ inline int combine_reparam_blocks(int ks, int B, int Z) {
+  const int cnt = 256 / splitk_rp(ks);
+  return (B * Z + cnt - 1) / cnt;
+}
+
+// Encoder head: mulv = sum_z slab[z] + bias (f32 [B][2Z]); eps ~ N(0,1)
+// (Philox, keyed like the MLP kernels); z = mu + eps * exp(lv/2) -> bf16
+// (+f32); one KLD partial per block (combine_reparam_blocks of them).
+struct CombineReparamArgs {
+  const float* slab;
+  int ks, rp;
+  const float* bias;
+  float* mulv;
+  float* eps;
+  __bf16* z16;
+  float* z32;
+  int B, Z;
+  const TrainState* st;
+  const HParams* hp;
+  uint32_t stream;
+  float* kld_part;
+};
+
+// `red` >= 2*256 + 16 floats
+__device__ __forceinline__ void combine_reparam_body(const CombineReparamArgs& a, float* red, int bid) {
+  const int t = threadIdx.x, cnt = 256 / a.rp, col = t % cnt, rl = t / cnt;
+  const int e = bid * cnt + col;
+  const bool live = e < a.B * a.Z;
+  const int i = live ? e / a.Z : 0, c = live ? e - i * a.Z : 0;
+  const long long MN = (long long)a.B * 2 * a.Z;
+  const long long em = (long long)i * 2 * a.Z + c, el = em + a.Z;
+  float vm = 0.f, vl = 0.f;
+  if (live) {
+    for (int z = rl; z < a.ks; z += a.rp) {
+      vm += a.slab[(size_t)z * MN + em];
+      vl += a.slab[(size_t)z * MN + el];
+    }
+  }
+  red[t] = vm;
+  red[256 + t] = vl;
+  __syncthreads();
+  float kl = 0.f;
+  if (rl == 0 && live) {
+    float mu = 0.f, lv = 0.f;
+    for (int r = 0; r < a.rp; ++r) {
+      mu += red[r * cnt + col];
+      lv += red[256 + r * cnt + col];
+    }
+    if (a.bias) {
+      mu += a.bias[c];
+      lv += a.bias[a.Z + c];
+    }
+    a.mulv[em] = mu;
+    a.mulv[el] = lv;
+    const long long stp = a.st->step - 1;
+    const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(i * a.Z + c), a.stream, (uint32_t)((unsigned long long)stp & 0xffffffffu),
+                                           (uint32_t)((unsigned long long)stp >> 32)},
+                                     a.hp->seed_lo, a.hp->seed_hi);
+    const float ep = normal_from_bits(bits.x, bits.y);
+    const float sd = expf(0.5f * lv);
+    const float zz = mu + ep * sd;
+    a.eps[e] = ep;
+    a.z16[e] = (__bf16)zz;
+    if (a.z32) a.z32[e] = zz;
+    kl = 1.f + lv - mu * mu - sd * sd;
+  }
+  const float s = block_sum(kl, red + 512);
+  if (threadIdx.x == 0) a.kld_part[bid] = -0.5f * s;
+}
+
+// Decoder Linear backward-data: dz = sum_z slab[z] -> d[mu|lv] (+bf16 copy).
+struct CombineReparamBwdArgs {
+  const float* slab;
+  int ks, rp;
+  const float* mulv;
+  const float* eps;
+  float* dmulv;
+  __bf16* dmulv16;
+  float* dz;
+  int B, Z;
+  const HParams* hp;
+};
+
+// `red` >= 256 floats
+__device__ __forceinline__ void combine_reparam_bwd_body(const CombineReparamBwdArgs& a, float* red, int bid) {
+  const int t = threadIdx.x, cnt = 256 / a.rp, col = t % cnt, rl = t / cnt;
+  const int e = bid * cnt + col;
+  const bool live = e < a.B * a.Z;
+  const long long MN = (long long)a.B * a.Z;
+  float v = 0.f;
+  if (live)
+    for (int z = rl; z < a.ks; z += a.rp) v += a.slab[(size_t)z * MN + e];
+  red[t] = v;
+  __syncthreads();
+  if (rl != 0 || !live) return;
+  float g = 0.f;
+  for (int r = 0; r < a.rp; ++r) g += red[r * cnt + col];
+  const int i = e / a.Z, c = e - i * a.Z;
+  if (a.dz) a.dz[e] = g;
+  const float beta = a.hp->kl_beta;
+  const float mu = a.mulv[(size_t)i * 2 * a.Z + c], lv = a.mulv[(size_t)i * 2 * a.Z + a.Z + c];
+  const float sd = expf(0.5f * lv);
+  const float dm = g + beta * mu;
+  const float dl = 0.5f * g * a.eps[e] * sd + 0.5f * beta * (sd * sd - 1.f);
+  a.dmulv[(size_t)i * 2 * a.Z + c] = dm;
+  a.dmulv[(size_t)i * 2 * a.Z + a.Z + c] = dl;
+  if (a.dmulv16) {
+    a.dmulv16[(size_t)i * 2 * a.Z + c] = (__bf16)dm;
+    a.dmulv16[(size_t)i * 2 * a.Z + a.Z + c] = (__bf16)dl;
+  }
+}
+
+// Gradient finalisation (256-thread blocks). One unit = `count` consecutive
+// elements of one segment. Threads t = rl*count + col sum partial rows rl,
+// rl+rp, ... (rp = 256/count) of column col, then row lane 0 adds the rp sums
+// in order: a fixed reduction tree, so results are bitwise reproducible
+// (unlike f32 atomics). With do_adam the same thread applies Adam to the
+// parameter and re-emits its bf16 copy.
+struct FinalizeArgs {
+  float *P, *G, *Mo, *Vo;
+  __bf16* w16;
+  const GradSeg* segs;
+  const GradUnit* units;
+  const TrainState* st;
+  const HParams* hp;
+  int do_adam;
+};
+
+constexpr int kFinalizeThreads = 256;
+
+__device__ __forceinline__ void grad_finalize_body(const FinalizeArgs& a, float* red, AdamC* cs, int bid) {
+  AdamC c{};
+  if (a.do_adam) c = adam_consts_block(a.st, a.hp, cs);
+  const GradUnit u = a.units[bid];
+  const GradSeg sg = a.segs[u.seg];
+  const int t = threadIdx.x, cnt = u.count, rp = kFinalizeThreads / cnt;
+  const int col = t % cnt, rl = t / cnt;
+  float acc = 0.f;
+  if (sg.slab && rl < rp) {
+    const float* p = sg.slab + u.start + col;
+    const long long n = sg.numel;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int s = rl;
+    for (; s + 3 * rp < sg.nsplit; s += 4 * rp) {
+      a0 += p[(long long)s * n];
+      a1 += p[(long long)(s + rp) * n];
+      a2 += p[(long long)(s + 2 * rp) * n];
+      a3 += p[(long long)(s + 3 * rp) * n];
+    }
+    for (; s < sg.nsplit; s += rp) a0 += p[(long long)s * n];
+    acc = (a0 + a1) + (a2 + a3);
+  }
+  red[t] = acc;
+  __syncthreads();
+  if (rl == 0) {
+    const long long o = sg.off + u.start + col;
+    float g;
+    if (sg.slab) {
+      g = 0.f;
+      for (int r = 0; r < rp; ++r) g += red[r * cnt + col];
+      if (!a.do_adam) a.G[o] = g;  // the fused-Adam path consumes g in registers only
+    } else {
+      g = a.G[o];
+    }
+    if (a.do_adam) {
+      float p = a.P[o], m = a.Mo[o], v = a.Vo[o];
+      adam_update(p, m, v, g, c);
+      a.P[o] = p; a.Mo[o] = m; a.Vo[o] = v;
+      a.w16[o] = (__bf16)p;
+    }
+  }
+}
+
+// bf16 weights [CO][k][k][CI] -> parity-ordered transpose [s][s][CI][k/s][k/s][CO]
+// (class (a, b) holds taps ky = a + s*ty, kx = b + s*tx) for the kModeTconv
+// GEMM. One 64x64 (co, ci) tile of one tap per block, staged through LDS so
+// both the read (ci-contiguous) and the write (co-contiguous) are coalesced.
+struct WtransArgs {
+  const __bf16* w16;
+  __bf16* w16t;
+  const GradSeg* segs;
+  const TrUnit* units;
+};
+
+constexpr int kWtransLds = 64 * 66 * 2;
+
+__device__ __forceinline__ void wtrans_body(const WtransArgs& wa, uint8_t* lds, int bid) {
+  unsigned short (*tile)[66] = reinterpret_cast<unsigned short (*)[66]>(lds);
+  const TrUnit u = wa.units[bid];
+  const GradSeg sg = wa.segs[u.seg];
+  const int k = sg.k, s = sg.s, CI = sg.ci, CO = sg.co, T = k / s;
+  const int ky = u.tap / k, kx = u.tap - ky * k;
+  const int a = ky % s, ty = ky / s, b = kx % s, tx = kx / s;
+  const unsigned short* src = reinterpret_cast<const unsigned short*>(wa.w16) + sg.off;
+  unsigned short* dst = reinterpret_cast<unsigned short*>(wa.w16t) + sg.toff;
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int r = idx >> 6, c = idx & 63;
+    const int co = u.co0 + r, ci = u.ci0 + c;
+    if (co < CO && ci < CI) tile[r][c] = src[((long long)(co * k + ky) * k + kx) * CI + ci];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int r = idx >> 6, c = idx & 63;
+    const int ci = u.ci0 + r, co = u.co0 + c;
+    if (co < CO && ci < CI) dst[((((long long)(a * s + b) * CI + ci) * T + ty) * T + tx) * CO + co] = tile[c][r];
   }
 }
 

@@ -4,6 +4,7 @@
 #pragma once
 #include "common.h"
 #include "conv_igemm.h"
+#include "vae_mlp.h"
 
 namespace mdt {
 
@@ -36,6 +37,16 @@ struct ThinConvArgs {
   __bf16* y16;
   const __bf16* omask;
   float* colsum;       // per-block column sums [blocks][CO] or null
+  // optional batch gather (first layer of a step): image n is X row
+  // idx[st->cursor * B + n]; the gathered f32 rows are also written to xb
+  // (the BCE target and wgrad input); with hp, block 0 also begins the step
+  // (step++, Adam beta^t products) -- nothing else in this launch reads them.
+  const int* idx;
+  TrainState* st;
+  const HParams* hp;
+  int B;
+  float* xb;
+  int nblk;
 };
 
 // LDS: staged weights [TAPS][CO] + the colsum transpose (256 x (CO+1)).
@@ -59,7 +70,23 @@ __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* 
   const int rem = mm - n * d.OH * d.OW;
   const int oy = rem / d.OW, ox = rem - oy * d.OW;
   const int iy0 = oy * d.S - d.P, ix0 = ox * d.S - d.P;
-  const TIN* img = X + (size_t)n * d.H * d.W;
+  const int* rows = ta.idx ? ta.idx + (size_t)ta.st->cursor * ta.B : nullptr;
+  const TIN* img = X + (size_t)(rows ? rows[n] : n) * d.H * d.W;
+  if (ta.xb) {
+    const int p4 = (d.H * d.W) >> 2;
+    const long long tot = (long long)d.N * p4;
+    for (long long e = (long long)bid * blockDim.x + threadIdx.x; e < tot; e += (long long)ta.nblk * blockDim.x) {
+      const int i = (int)(e / p4), c = (int)(e - (long long)i * p4);
+      reinterpret_cast<float4*>(ta.xb + (size_t)i * d.H * d.W)[c] =
+          reinterpret_cast<const float4*>(X + (size_t)(rows ? rows[i] : i) * d.H * d.W)[c];
+    }
+  }
+  if (ta.hp && bid == 0 && threadIdx.x == 0) {
+    TrainState* st = ta.st;
+    st->step = st->step + 1;
+    st->b1pow *= ta.hp->beta1_d;
+    st->b2pow *= ta.hp->beta2_d;
+  }
   float xin[TAPS];
 #pragma unroll
   for (int t = 0; t < TAPS; ++t) {

@@ -41,12 +41,15 @@ extern "C" {
 
 // conv with a single input channel; x_is_f32 selects f32 / bf16 input.
 int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, const float* bias, int relu, void* y16,
-                  const void* omask, float* colsum, hipStream_t s) {
+                  const void* omask, float* colsum, const int* idx, void* st, const void* hp, int B, float* xb,
+                  hipStream_t s) {
   if (d.C != 1 || d.KH != 4 || d.KW != 4) return 1;
+  if ((idx || xb || hp) && (!st || !x_is_f32 || (d.H * d.W) % 4)) return 1;
   const long long M = (long long)d.N * d.OH * d.OW;
   dim3 grid(cdiv_t(M, 256)), blk(256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
-                        colsum};
+                        colsum, idx, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), B, xb,
+                        (int)grid.x};
 #define THIN(CO_)                                                                     \
   {                                                                                   \
     if (x_is_f32)                                                                     \

@@ -18,7 +18,7 @@ extern "C" {
 int mdt_igemm_plan(int mode, mdt::ConvDesc d, int allow_split, int* info);
 int mdt_wgrad_plan(mdt::ConvDesc d, int* info);
 int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, mdt::ConvDesc d, const float* bias, int relu,
-              void* y16, float* y32, const void* omask, float* colsum, float* ws, hipStream_t s);
+              void* y16, float* y32, const void* omask, float* colsum, float* ws, int skip_combine, hipStream_t s);
 int mdt_wgrad(const void* G16, const void* X, int x_is_f32, mdt::ConvDesc d, float* out, hipStream_t s);
 int mdt_colsum(const void* G16, int M, int N, int rows_per, float* slab, hipStream_t s);
 int mdt_gather_rows(const float* X, const int* idx, const void* st, int B, int M, int P, float* xb, hipStream_t s);
@@ -37,13 +37,22 @@ int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, const
                       int nunits, const void* st, const void* hp, int do_adam, hipStream_t s);
 int mdt_wtrans(const void* w16, void* w16t, const void* segs, const void* units, int nunits, hipStream_t s);
 int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, mdt::ConvDesc d, const float* bias, int relu, void* y16,
-                  const void* omask, float* colsum, hipStream_t s);
+                  const void* omask, float* colsum, const int* idx, void* st, const void* hp, int B, float* xb,
+                  hipStream_t s);
 int mdt_thin_blocks(int tconv, mdt::ConvDesc d);
 int mdt_thin_tconv(const void* G16, const float* Wf, mdt::ConvDesc d, const float* bias, float* y32, const float* X,
                    void* dlog16, float* recon, float* part, float* gpart, hipStream_t s);
 int mdt_job_igemm(mdt::JobBlob* g, mdt::JobBlob* c, int mode, const void* A, int a_is_f32, const void* B16,
                   mdt::ConvDesc d, const float* bias, int relu, void* y16, float* y32, const void* omask,
-                  float* colsum, float* ws);
+                  float* colsum, float* ws, int skip_combine);
+int mdt_job_finalize(mdt::JobBlob* j, float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs,
+                     const void* units, int nunits, const void* st, const void* hp, int do_adam);
+int mdt_job_wtrans(mdt::JobBlob* j, const void* w16, void* w16t, const void* segs, const void* units, int nunits);
+int mdt_combine_reparam(const float* slab, int ks, const float* bias, float* mulv, float* eps, void* z16, float* z32,
+                        int B, int Z, const void* st, const void* hp, unsigned stream, float* kld_part, hipStream_t s);
+int mdt_combine_reparam_blocks(int ks, int B, int Z);
+int mdt_combine_reparam_bwd(const float* slab, int ks, const float* mulv, const float* eps, float* dmulv,
+                            void* dmulv16, float* dz, int B, int Z, const void* hp, hipStream_t s);
 int mdt_job_wgrad(mdt::JobBlob* j, const void* G16, const void* X, int x_is_f32, mdt::ConvDesc d, float* out);
 int mdt_job_thin_conv(mdt::JobBlob* j, const void* X, int x_is_f32, const float* Wf, mdt::ConvDesc d,
                       const float* bias, int relu, void* y16, const void* omask, float* colsum);
@@ -108,7 +117,7 @@ std::vector<int64_t> wgrad_plan(const std::vector<int64_t>& dv) {
 void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::vector<int64_t>& dv,
            const c10::optional<at::Tensor>& bias, bool relu, const c10::optional<at::Tensor>& y16,
            const c10::optional<at::Tensor>& y32, const c10::optional<at::Tensor>& omask,
-           const c10::optional<at::Tensor>& colsum, const c10::optional<at::Tensor>& ws, Job* job) {
+           const c10::optional<at::Tensor>& colsum, const c10::optional<at::Tensor>& ws, Job* job, bool combine) {
   const ConvDesc d = desc(dv);
   TORCH_CHECK(A.is_cuda() && A.is_contiguous(), "A must be contiguous CUDA");
   const bool f32 = A.scalar_type() == torch::kFloat32;
@@ -130,13 +139,13 @@ void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::
   if (job) {
     rc(mdt_job_igemm(&job->main, &job->post, (int)mode, A.data_ptr(), f32, B16.data_ptr(), d,
                      (const float*)opt_ptr(bias), relu, const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32),
-                     opt_ptr(omask), (float*)opt_ptr(colsum), (float*)opt_ptr(ws)),
+                     opt_ptr(omask), (float*)opt_ptr(colsum), (float*)opt_ptr(ws), combine ? 0 : 1),
        "job_igemm");
     return;
   }
   rc(mdt_igemm((int)mode, A.data_ptr(), f32, B16.data_ptr(), d, (const float*)opt_ptr(bias), relu,
                const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32), opt_ptr(omask), (float*)opt_ptr(colsum),
-               (float*)opt_ptr(ws), cur()),
+               (float*)opt_ptr(ws), combine ? 0 : 1, cur()),
      "igemm");
 }
 
@@ -163,7 +172,9 @@ void wgrad(const at::Tensor& G16, const at::Tensor& X, const std::vector<int64_t
 // [CO][KH][KW][1] (read with wave-uniform scalar loads).
 void thin_conv(const at::Tensor& X, const at::Tensor& Wf, const std::vector<int64_t>& dv,
                const c10::optional<at::Tensor>& bias, bool relu, at::Tensor y16,
-               const c10::optional<at::Tensor>& omask, const c10::optional<at::Tensor>& colsum, Job* job) {
+               const c10::optional<at::Tensor>& omask, const c10::optional<at::Tensor>& colsum, Job* job,
+               const c10::optional<at::Tensor>& idx, const c10::optional<at::Tensor>& state,
+               const c10::optional<at::Tensor>& hparams, int64_t B, const c10::optional<at::Tensor>& xb) {
   const ConvDesc d = desc(dv);
   const bool f32 = X.scalar_type() == torch::kFloat32;
   TORCH_CHECK(X.is_cuda() && X.is_contiguous() && (f32 || X.scalar_type() == torch::kBFloat16), "X dtype/layout");
@@ -182,8 +193,16 @@ void thin_conv(const at::Tensor& X, const at::Tensor& Wf, const std::vector<int6
        "job_thin_conv");
     return;
   }
+  const bool gather = idx.has_value() && idx->defined();
+  if (gather) {
+    TORCH_CHECK(job == nullptr, "thin_conv: the gathering form has no job variant");
+    TORCH_CHECK(idx->scalar_type() == torch::kInt32 && state.has_value() && B >= d.N, "thin_conv gather arguments");
+    TORCH_CHECK(X.dim() == 2 && X.size(1) == (int64_t)d.H * d.W, "thin_conv gather: X must be [rows, H*W]");
+  }
+  check_min(xb, (int64_t)d.N * d.H * d.W, "xb");
   rc(mdt_thin_conv(X.data_ptr(), f32, Wf.data_ptr<float>(), d, (const float*)opt_ptr(bias), relu, y16.data_ptr(),
-                   opt_ptr(omask), (float*)opt_ptr(colsum), cur()),
+                   opt_ptr(omask), (float*)opt_ptr(colsum), (const int*)opt_ptr(idx), const_cast<void*>(opt_ptr(state)),
+                   opt_ptr(hparams), (int)B, (float*)opt_ptr(xb), cur()),
      "thin_conv");
 }
 
@@ -341,17 +360,58 @@ void adam_cast(at::Tensor P, const at::Tensor& G, at::Tensor M, at::Tensor V, at
 
 void grad_finalize(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::Tensor w16, const at::Tensor& segs,
                    const at::Tensor& units, int64_t nunits, const at::Tensor& state, const at::Tensor& hparams,
-                   bool do_adam) {
+                   bool do_adam, Job* job) {
+  TORCH_CHECK(units.numel() >= nunits * (int64_t)sizeof(GradUnit), "grad_finalize: unit table too small");
+  if (job) {
+    rc(mdt_job_finalize(&job->main, P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(),
+                        V.data_ptr<float>(), w16.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits,
+                        state.data_ptr(), hparams.data_ptr(), do_adam ? 1 : 0),
+       "job_finalize");
+    return;
+  }
   rc(mdt_grad_finalize(P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(),
                        w16.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits, state.data_ptr(),
                        hparams.data_ptr(), do_adam ? 1 : 0, cur()),
      "grad_finalize");
 }
 
-void wtrans(const at::Tensor& w16, at::Tensor w16t, const at::Tensor& segs, const at::Tensor& units, int64_t nunits) {
+void wtrans(const at::Tensor& w16, at::Tensor w16t, const at::Tensor& segs, const at::Tensor& units, int64_t nunits,
+            Job* job) {
   check_bf16(w16, "w16");
   check_bf16(w16t, "w16t");
+  TORCH_CHECK(units.numel() >= nunits * (int64_t)sizeof(TrUnit), "wtrans: unit table too small");
+  if (job) {
+    rc(mdt_job_wtrans(&job->main, w16.data_ptr(), w16t.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits),
+       "job_wtrans");
+    return;
+  }
   rc(mdt_wtrans(w16.data_ptr(), w16t.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits, cur()), "wtrans");
+}
+
+// Split-K combine of the encoder head fused with the reparameterisation, and
+// of the decoder Linear's backward-data fused with its backward.
+void combine_reparam(const at::Tensor& ws, int64_t ks, const c10::optional<at::Tensor>& bias, at::Tensor mulv,
+                     at::Tensor eps, at::Tensor z16, const c10::optional<at::Tensor>& z32, int64_t B, int64_t Z,
+                     const at::Tensor& state, const at::Tensor& hparams, int64_t stream, at::Tensor kld_part) {
+  check_f32(ws, "ws");
+  TORCH_CHECK(ws.numel() >= ks * B * 2 * Z && mulv.numel() >= B * 2 * Z && eps.numel() >= B * Z &&
+                  z16.numel() >= B * Z && kld_part.numel() >= mdt_combine_reparam_blocks((int)ks, (int)B, (int)Z),
+              "combine_reparam: buffer too small");
+  rc(mdt_combine_reparam(ws.data_ptr<float>(), (int)ks, (const float*)opt_ptr(bias), mulv.data_ptr<float>(),
+                         eps.data_ptr<float>(), z16.data_ptr(), (float*)opt_ptr(z32), (int)B, (int)Z, state.data_ptr(),
+                         hparams.data_ptr(), (unsigned)stream, kld_part.data_ptr<float>(), cur()),
+     "combine_reparam");
+}
+
+void combine_reparam_bwd(const at::Tensor& ws, int64_t ks, const at::Tensor& mulv, const at::Tensor& eps,
+                         at::Tensor dmulv, const c10::optional<at::Tensor>& dmulv16,
+                         const c10::optional<at::Tensor>& dz, int64_t B, int64_t Z, const at::Tensor& hparams) {
+  check_f32(ws, "ws");
+  TORCH_CHECK(ws.numel() >= ks * B * Z && dmulv.numel() >= B * 2 * Z, "combine_reparam_bwd: buffer too small");
+  rc(mdt_combine_reparam_bwd(ws.data_ptr<float>(), (int)ks, mulv.data_ptr<float>(), eps.data_ptr<float>(),
+                             dmulv.data_ptr<float>(), const_cast<void*>(opt_ptr(dmulv16)), (float*)opt_ptr(dz), (int)B,
+                             (int)Z, hparams.data_ptr(), cur()),
+     "combine_reparam_bwd");
 }
 
 // ------------------------------------------------------------------ state ----
@@ -432,12 +492,15 @@ void bind_conv(pybind11::module& m) {
   m.def("launch_jobs", &launch_jobs);
   m.def("igemm", &igemm, py::arg("mode"), py::arg("A"), py::arg("B16"), py::arg("desc"), py::arg("bias"),
         py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),
-        py::arg("colsum") = py::none(), py::arg("ws") = py::none(), py::arg("job") = py::none());
+        py::arg("colsum") = py::none(), py::arg("ws") = py::none(), py::arg("job") = py::none(),
+        py::arg("combine") = true);
   m.def("wgrad", &wgrad, py::arg("G16"), py::arg("X"), py::arg("desc"), py::arg("out"), py::arg("job") = py::none());
   m.def("colsum", &colsum, py::arg("G16"), py::arg("M"), py::arg("N"), py::arg("rows_per"), py::arg("slab"),
         py::arg("job") = py::none());
   m.def("thin_conv", &thin_conv, py::arg("X"), py::arg("Wf"), py::arg("desc"), py::arg("bias"), py::arg("relu"),
-        py::arg("y16"), py::arg("omask") = py::none(), py::arg("colsum") = py::none(), py::arg("job") = py::none());
+        py::arg("y16"), py::arg("omask") = py::none(), py::arg("colsum") = py::none(), py::arg("job") = py::none(),
+        py::arg("idx") = py::none(), py::arg("state") = py::none(), py::arg("hparams") = py::none(),
+        py::arg("B") = 0, py::arg("xb") = py::none());
   m.def("thin_blocks", &thin_blocks);
   m.def("thin_tconv", &thin_tconv, py::arg("G16"), py::arg("Wf"), py::arg("desc"), py::arg("bias"),
         py::arg("y32") = py::none(), py::arg("X") = py::none(), py::arg("dlog16") = py::none(),
@@ -454,8 +517,14 @@ void bind_conv(pybind11::module& m) {
   m.def("make_grad_units", &make_grad_units);
   m.def("make_tr_units", &make_tr_units);
   m.def("adam_cast", &adam_cast);
-  m.def("grad_finalize", &grad_finalize);
-  m.def("wtrans", &wtrans);
+  m.def("grad_finalize", &grad_finalize, py::arg("P"), py::arg("G"), py::arg("M"), py::arg("V"), py::arg("w16"),
+        py::arg("segs"), py::arg("units"), py::arg("nunits"), py::arg("state"), py::arg("hparams"),
+        py::arg("do_adam"), py::arg("job") = py::none());
+  m.def("wtrans", &wtrans, py::arg("w16"), py::arg("w16t"), py::arg("segs"), py::arg("units"), py::arg("nunits"),
+        py::arg("job") = py::none());
+  m.def("combine_reparam", &combine_reparam);
+  m.def("combine_reparam_bwd", &combine_reparam_bwd);
+  m.def("combine_reparam_blocks", &mdt_combine_reparam_blocks);
   py::class_<TrialStateBuf>(m, "TrialState")
       .def(py::init<int64_t>())
       .def("set_hparams", &TrialStateBuf::set_hparams)

@@ -440,7 +440,7 @@ class ConvVaeTrainer:
         self._thin_last = (last.kind == "convT" and last.cout == 1 and last.cin in (16, 32, 64) and last.k % last.s == 0
                            and last.out_hw % last.s == 0)
         self.bce_part = torch.zeros(max(self._n_bce(B), 1), **f32)
-        self.kld_part = torch.zeros(-(-B * zf // 256), **f32)
+        self.kld_part = torch.zeros(B * zf, **f32)  # >= KLD partials of reparam / combine_reparam
         self._plans = {}
         self._cast_weights()
 
@@ -449,6 +449,15 @@ class ConvVaeTrainer:
         if self._thin_last:
             return self.C.thin_blocks(True, self._desc(self.spec[-1], M))
         return -(-M * self.D // 256)
+
+    def _n_kld(self, M):
+        """Number of KLD partials the forward writes for a batch of M (one per
+        block of the reparameterisation kernel that ends the encoder)."""
+        head = [l for l in self.spec if l.name.startswith("enc")][-1]
+        ks = self.C.igemm_plan(0, self._desc(head, M), True)[10]
+        if ks > 1:
+            return self.C.combine_reparam_blocks(ks, M, self.Z)
+        return -(-M * self.Z // 256)
 
     def _wf32(self, l):
         """f32 master weight of a layer (read directly by the thin kernels)."""
@@ -537,11 +546,11 @@ class ConvVaeTrainer:
         for si, (off, numel, ptr, ns, *_rest) in enumerate(segs):
             if si % 2 == 0:
                 layer_units.append(len(units))
-            rp = 1
+            rp = 1  # partial rows per unit column; 256-thread finalize blocks (kFinalizeThreads)
             if ptr:
-                while rp < 512 and rp * 16 < ns:
+                while rp < 256 and rp * 16 < ns:
                     rp *= 2
-            cnt = 512 // rp
+            cnt = 256 // rp
             for st in range(0, numel, cnt):
                 units.append([si, st, min(cnt, numel - st)])
         layer_units.append(len(units))  # layer i owns units [layer_units[i], layer_units[i+1])
@@ -599,17 +608,41 @@ class ConvVaeTrainer:
         else:
             self.C.igemm(0, h, self._w(l), d, self._b(l), l.relu, o16, o32, ws=ws)
 
-    def _forward_hip(self, M, state, stream, want_recon=False, train=True):
+    def _forward_hip(self, M, state, stream, want_recon=False, train=True, src=None):
+        """Forward of one batch. ``src = (X, idx)``: the batch is gathered from
+        the dataset by the step's first kernel (and the step begun there) when
+        the first layer runs on the direct kernel; otherwise by gather_rows."""
         C = self.C
         p = self._plan(M)
+        hp = self.state.hparams
         enc = [l for l in self.spec if l.name.startswith("enc")]
         dec = [l for l in self.spec if l.name.startswith("dec")]
         h = self.xb
-        for l in enc:
+        first = 0
+        if src is not None:
+            X, idx = src
+            l = enc[0]
+            if self.fuse_jobs and self._thin_first and len(enc) > 1:
+                C.thin_conv(X, self._wf32(l), self._desc(l, M), self._b(l), l.relu, self.acts[l.name], idx=idx,
+                            state=state, hparams=hp, B=self.B, xb=self.xb)
+                h, first = self.acts[l.name], 1
+            else:
+                C.step_begin(state, hp)
+                C.gather_rows(X, idx, state, self.B, M, self.xb)
+        for l in enc[first:]:
             last = l is enc[-1]
+            if last:
+                q = C.igemm_plan(0, self._desc(l, M), True)
+                if q[10] > 1:  # split-K head: combine fused with the reparameterisation
+                    C.igemm(0, h, self._w(l), self._desc(l, M), self._b(l), False, None, self.mulv, ws=p["ws"],
+                            combine=False)
+                    C.combine_reparam(p["ws"], q[10], self._b(l), self.mulv, self.eps, self.z16, None, M, self.Z,
+                                      state, hp, stream, self.kld_part)
+                    break
             self._layer_fwd(l, h, M, None if last else self.acts[l.name], self.mulv if last else None, p["ws"])
             h = self.acts[l.name]
-        C.reparam(self.mulv, self.eps, self.z16, None, M, self.Z, state, self.state.hparams, stream, self.kld_part)
+        else:
+            C.reparam(self.mulv, self.eps, self.z16, None, M, self.Z, state, hp, stream, self.kld_part)
         h = self.z16
         for l in dec:
             last = l is dec[-1]
@@ -637,13 +670,15 @@ class ConvVaeTrainer:
         for f in fns:
             f(None)
 
-    def _backward_hip(self, M, with_loss=False):
+    def _backward_hip(self, M, with_loss=False, optimizer=False):
         """Reverse sweep: per layer one weight-gradient GEMM (partial slabs) and
         one backward-data GEMM whose epilogue applies the previous layer's ReLU
         mask and emits its bias-gradient column sums. The two (plus any bias
         column sum or loss reduction that became ready) are independent and
         share one launch (``_run_group``). ``with_loss`` adds the loss reduction
-        of the forward to the first launch."""
+        of the forward to the first launch; ``optimizer`` (no reducer) appends
+        the optimizer tail: first-layer weight gradient || finalize+Adam of the
+        other layers, then first-layer finalize || transposed weight copies."""
         C = self.C
         p = self._plan(M)
         spec = self.spec
@@ -657,7 +692,7 @@ class ConvVaeTrainer:
         carry = []  # launches that depend on the previous group's outputs
         if with_loss:
             carry.append(lambda job: C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part,
-                                                      -(-M * self.Z // 256), st.train_state, st.hparams, True,
+                                                      self._n_kld(M), st.train_state, st.hparams, True,
                                                       job=job))
         for i in range(len(spec) - 1, -1, -1):
             if red is not None and i + 1 < len(spec):
@@ -682,10 +717,17 @@ class ConvVaeTrainer:
             if prev is not None:
                 omask = a_in if prev.relu else None
                 if l.name == "dec_fc":
-                    fns.append(lambda job, g=g, l=l, d=d: C.igemm(1, g, self._wt(l), d, None, False, None, self.dz,
-                                                                  ws=p["ws"], job=job))
-                    after.append(lambda: C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M,
-                                                       self.Z, st.hparams))
+                    ks = C.igemm_plan(1, d, True)[10]
+                    fns.append(lambda job, g=g, l=l, d=d, ks=ks: C.igemm(1, g, self._wt(l), d, None, False, None,
+                                                                         self.dz, ws=p["ws"], job=job,
+                                                                         combine=ks == 1))
+                    if ks > 1:  # split-K combine fused with the reparameterisation backward
+                        after.append(lambda ks=ks: C.combine_reparam_bwd(p["ws"], ks, self.mulv, self.eps, self.dmulv,
+                                                                         self.dmulv16, self.dz, M, self.Z,
+                                                                         st.hparams))
+                    else:
+                        after.append(lambda: C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16,
+                                                           M, self.Z, st.hparams))
                     cso = p["colsum"][prev.name]
                     carry.append(lambda job, cso=cso: C.colsum(self.dmulv16, M, 2 * self.Z, p["rows_per"], cso,
                                                                job=job))
@@ -706,6 +748,13 @@ class ConvVaeTrainer:
                         cso = p["colsum"][prev.name]
                         carry.append(lambda job, gin=gin, n=prev.cout, cso=cso:
                                      C.colsum(gin, M, n, p["rows_per"], cso, job=job))
+            if prev is None and optimizer:
+                L = len(spec)
+                fns.append(lambda job: self._finalize_layers(M, 1, L, job))
+                self._run_group(fns)
+                self._run_group([lambda job: self._finalize_layers(M, 0, 1, job),
+                                 lambda job: self._wtrans_layers(1, L, job)])
+                break
             self._run_group(fns)
             for f in after:
                 f()
@@ -715,6 +764,21 @@ class ConvVaeTrainer:
                     self._maybe_launch_bucket(red, bounds, starts, 0, M)
                 break
             g = gin
+
+    def _finalize_layers(self, M, lo, hi, job=None):
+        """Finalize + Adam + bf16 cast of layers [lo, hi) (their units of the plan)."""
+        p, st = self._plan(M), self.state
+        u0, u1 = p["layer_units"][lo], p["layer_units"][hi]
+        self.C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"],
+                             p["units"].narrow(0, u0 * 12, (u1 - u0) * 12), u1 - u0, st.train_state, st.hparams,
+                             True, job=job)
+
+    def _wtrans_layers(self, lo, hi, job=None):
+        """Parity-ordered transposed copies of layers [lo, hi) (the first layer's
+        copy is never read: it has no backward-data GEMM)."""
+        t0, t1 = self._tr_layer[lo], self._tr_layer[hi]
+        self.C.wtrans(self.w16, self.w16t, self.segs, self.tr_units.narrow(0, t0 * 16, (t1 - t0) * 16), t1 - t0,
+                      job=job)
 
     def _maybe_launch_bucket(self, red, bounds, starts, i, M):
         """Layer i's gradients just became final (all layers >= i are done): if
@@ -737,21 +801,24 @@ class ConvVaeTrainer:
         C = self.C
         X, idx = self._data[0], self._data[1]
         st = self.state
-        C.step_begin(st.train_state, st.hparams)
-        C.gather_rows(X, idx, st.train_state, self.B, M, self.xb)
-        self._forward_hip(M, st.train_state, self.rng_stream)
         if self.reducer is None and self.overlap:
+            C.step_begin(st.train_state, st.hparams)
+            C.gather_rows(X, idx, st.train_state, self.B, M, self.xb)
+            self._forward_hip(M, st.train_state, self.rng_stream)
             self._backward_overlap(M)
             return
-        # loss reduction rides in the backward's first launch; with a reducer the
-        # backward finalizes + launches each bucket as it completes
+        self._forward_hip(M, st.train_state, self.rng_stream, src=(X, idx))
+        if self.reducer is None:
+            # backward + optimizer tail (finalize/Adam/bf16 cast/transposes) in fused launches
+            self._backward_hip(M, with_loss=True, optimizer=True)
+            return
+        # intra-group DDP: the backward finalizes + launches each gradient bucket
+        # as it completes (loss reduction in its first launch); Adam after the
+        # all-reduces
         self._backward_hip(M, with_loss=True)
-        if self.reducer is not None:
-            self.reducer.wait_all()
-            C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
-                        st.train_state, st.hparams, True)
-        else:
-            self._finalize_grads(M, True)
+        self.reducer.wait_all()
+        C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
+                    st.train_state, st.hparams, True)
         self._transpose_weights()
 
     # layer groups whose gradients are finalized together (optimizer + bf16
@@ -785,7 +852,7 @@ class ConvVaeTrainer:
         cut.add(0)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, -(-M * self.Z // 256),
+            C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, self._n_kld(M),
                              st.train_state, st.hparams, True)
         g = self.dlog16
         hi = len(spec)  # layers [i, hi) wait for their finalize
@@ -826,14 +893,9 @@ class ConvVaeTrainer:
                 for t, n, out in side_cs:
                     C.colsum(t, M, n, p["rows_per"], out)
                 if i in cut:
-                    u0, u1 = p["layer_units"][i], p["layer_units"][hi]
-                    C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"],
-                                    p["units"].narrow(0, u0 * 12, (u1 - u0) * 12), u1 - u0, st.train_state,
-                                    st.hparams, True)
-                    t0, t1 = self._tr_layer[i], self._tr_layer[hi]
-                    if t1 > t0:
-                        C.wtrans(self.w16, self.w16t, self.segs, self.tr_units.narrow(0, t0 * 16, (t1 - t0) * 16),
-                                 t1 - t0)
+                    self._finalize_layers(M, i, hi)
+                    if hi > max(i, 1):
+                        self._wtrans_layers(max(i, 1), hi)
                     hi = i
         main.wait_stream(side)
 
@@ -952,11 +1014,10 @@ class ConvVaeTrainer:
             M = min(self.B, n - b * self.B)
             if self.backend == "hip":
                 st = self.state
-                self.C.step_begin(st.eval_state, st.hparams)
-                self.C.gather_rows(X.contiguous(), idx, st.eval_state, self.B, M, self.xb)
                 want = want_first_recon and b == 0
-                self._forward_hip(M, st.eval_state, EVAL_STREAM + self.rng_stream, want_recon=want, train=False)
-                self.C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, -(-M * self.Z // 256),
+                self._forward_hip(M, st.eval_state, EVAL_STREAM + self.rng_stream, want_recon=want, train=False,
+                                  src=(X.contiguous(), idx))
+                self.C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, self._n_kld(M),
                                       st.eval_state, st.hparams, True)
                 if want:
                     first = self.recon[: M * self.D].view(M, self.D).clone()
