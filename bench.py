@@ -3,17 +3,20 @@
 
 Metric / config from BASELINE.json: the global world (one process per MI355X)
 is carved into K trial groups (default K = N: one trial per GPU, BASELINE
-config #3 shape "8 subgroups x 1 GPU"; ``--ngroups`` gives e.g. 4x2 with
-intra-group gradient all-reduce). Every trial trains the reference MLP-VAE
-(784-400-20, /root/reference/vae-hpo.py:19-45, fp32 like the reference) with
-Adam(lr=1e-3) at batch 128 on its DistributedSampler shard of a synthetic
-MNIST-shaped dataset, with its own (lr, beta) hyper-parameters.
+config #3 shape "8 subgroups x 1 GPU"; at N = 1 this is config #2 "1 subgroup
+of 1 MI355X; conv-VAE bf16 on 28x28"). ``--ngroups`` gives e.g. 4x2 with
+intra-group gradient all-reduce (config #4). Every trial trains the conv-VAE
+(bf16 MFMA kernels, fp32 master weights + Adam) at batch 128 on its
+DistributedSampler shard of a synthetic MNIST-shaped dataset, with its own
+(lr, beta) hyper-parameters. ``--model mlp`` runs the reference's own MLP-VAE
+(784-400-20, /root/reference/vae-hpo.py:19-45, fp32); ``--model conv128`` the
+128x128 conv-VAE of config #5.
 
 A step = one full training iteration (fwd + bwd + [all-reduce] + Adam) of every
 trial. Timing: W warm-up steps (also captures the hipGraphs), then a barrier +
 device sync, exactly K steps, barrier + device sync; the max over ranks is
-reported. ``value`` = Σ_trials (batch x steps) / max_time (samples are counted
-once per trial, not per replica — SURVEY.md §6 metric definition).
+reported. ``value`` = sum over trials of (batch x steps) / max_time (samples are
+counted once per trial, not per replica -- SURVEY.md section 6 metric).
 
 Run: python bench.py --gpus N --steps K --warmup W   (N>1 via torch.distributed.run)
 """
@@ -31,11 +34,14 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-# Reference-equivalent step on the SAME MI355X (BASELINE.md, row 2:
-# bench/ref_torch_baseline.py = the reference's DDP + DataLoader + .item() +
-# Adam hot loop in stock PyTorch-ROCm): 93.5k samples/s per trial. Used per
-# trial: baseline(K) = K x 93.5k (generous to the reference: perfect scaling).
-REF_SAMPLES_PER_S_PER_TRIAL = 93465.0
+# Reference-equivalent throughput on the SAME MI355X: the
+# reference's training loop (DDP + DataLoader + loss.item() per step + torch
+# Adam, bench/ref_torch_baseline.py) in stock PyTorch-ROCm eager mode, per
+# trial, for each model. The conv anchors run the reference loop with the
+# conv-VAE swapped in, in fp32 (the reference's dtype; torch's bf16 autocast
+# path faulted inside MIOpen on this stack for the 28x28 model).
+# baseline(K) = K x anchor (generous to the reference: perfect scaling).
+REF_SAMPLES_PER_S_PER_TRIAL = {"mlp": 93465.0, "conv28": 42924.0, "conv128": 18788.0}
 
 
 def main(argv=None):
@@ -45,8 +51,9 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch-size", type=int, default=128)
     ap.add_argument("--ngroups", type=int, default=None, help="trials K (default: world size)")
-    ap.add_argument("--model", default="mlp", choices=["mlp", "conv28", "conv128"],
-                    help="mlp = reference MLP-VAE fp32 (headline); conv28/conv128 = bf16 conv-VAE extension")
+    ap.add_argument("--model", default="conv28", choices=["mlp", "conv28", "conv128"],
+                    help="conv28 = conv-VAE bf16 28x28 (BASELINE configs #2/#3, headline); conv128 = 128x128 "
+                         "(config #5); mlp = the reference's MLP-VAE in fp32")
     ap.add_argument("--graph-steps", type=int, default=10)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--backend", default=None, help="hip|torch (default: hip on GPU)")
@@ -168,7 +175,7 @@ def main(argv=None):
             "ms_per_step": round(dt / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / (REF_SAMPLES_PER_S_PER_TRIAL * K * T), 2),
+            "vs_baseline": round(value / (REF_SAMPLES_PER_S_PER_TRIAL[a.model] * K * T), 2),
             "dtype": "fp32" if a.model == "mlp" else "bf16",
             "data": ("synthetic (MNIST-shaped 60000x1x28x28, random-init weights)" if a.model != "conv128"
                      else "synthetic (1x128x128 images, random-init weights)"),

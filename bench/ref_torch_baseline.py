@@ -86,6 +86,7 @@ def main(argv=None):
     ap.add_argument("--full-epoch", action="store_true", help="also time test pass + sampling like the reference")
     ap.add_argument("--model", default="mlp", choices=["mlp", "conv28", "conv128"])
     ap.add_argument("--max-steps", type=int, default=None, help="cap the timed steps per epoch")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="conv models: autocast bf16 or fp32")
     a = ap.parse_args(argv)
 
     from multidisttorch_amd.runtime import setup_ddp
@@ -118,7 +119,7 @@ def main(argv=None):
 
         z = 32 if img == 28 else 64
         model = ConvRef(TorchConvVAE(conv_vae_spec(img, 1, z), img, 1, z)).to(dev)
-        amp = torch.bfloat16 if dev.type == "cuda" else None
+        amp = torch.bfloat16 if (dev.type == "cuda" and a.dtype == "bf16") else None
     model = torch.nn.parallel.DistributedDataParallel(model, process_group=group)
     opt = optim.Adam(model.parameters(), lr=1e-3)
 

@@ -36,8 +36,8 @@ CONFIGS = {
             args=["--model", "mlp", "--ngroups", "2", "--backend", "torch", "--no-graphs"], env={"DDP_BACKEND": "gloo"}),
     2: dict(desc="1 subgroup x 1 MI355X, conv-VAE 28x28 bf16", nproc=1, gpus=1,
             args=["--model", "conv28", "--ngroups", "1"]),
-    3: dict(desc="8 subgroups x 1 MI355X, MLP-VAE (headline)", nproc=8, gpus=8,
-            args=["--model", "mlp", "--ngroups", "8"]),
+    3: dict(desc="8 subgroups x 1 MI355X, conv-VAE 28x28 (lr, beta) sweep (headline)", nproc=8, gpus=8,
+            args=["--model", "conv28", "--ngroups", "8"]),
     4: dict(desc="4 subgroups x 2 MI355X, conv-VAE 28x28 + intra-group all-reduce", nproc=8, gpus=8,
             args=["--model", "conv28", "--ngroups", "4"]),
     5: dict(desc="2 subgroups x 4 MI355X, conv-VAE 128x128 + per-layer buckets", nproc=8, gpus=8,
@@ -85,6 +85,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--only", default=None, help="comma list of config numbers")
     ap.add_argument("--scaling", action="store_true")
+    ap.add_argument("--model", default="conv28", help="model of the 1/2/4/8-GPU scaling curve")
     a = ap.parse_args(argv)
     ngpu = gpu_count()
     only = {int(x) for x in a.only.split(",")} if a.only else set(CONFIGS)
@@ -105,7 +106,7 @@ def main(argv=None):
             if n > ngpu:
                 curve.append({"n_gpus": n, "skipped": True})
                 continue
-            r = run_bench(n, ["--model", "mlp"], a.steps, a.warmup)
+            r = run_bench(n, ["--model", a.model], a.steps, a.warmup)
             curve.append({"n_gpus": n, "value": r.get("value"), "ms_per_step": r.get("ms_per_step")})
         base = next((c["value"] for c in curve if c.get("n_gpus") == 1 and c.get("value")), None)
         for c in curve:
