@@ -234,6 +234,25 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, f32x4 (&acc)[TC:
   }
 }
 
+// Register-prefetch depth of the k-loops: k-tiles whose global loads are in
+// flight while the MFMAs of the current LDS tile run. Measured on MI355X
+// (profiles/r1_conv_jobs/README.md): a 3-deep ring for small tiles / 2-deep
+// for large ones made every conv GEMM 0.4-1.4 us SLOWER (conv28 step 0.138 ->
+// 0.145 ms, conv128 0.549 -> 0.625 ms; 113-134 VGPRs instead of 64-78), so
+// the default is the single tile in flight; -DMDT_CONV_PF=N keeps the ring
+// for experiments.
+#ifndef MDT_CONV_PF
+#define MDT_CONV_PF 1
+#endif
+template <int STAGE_REGS>
+constexpr int prefetch_depth() {
+  return MDT_CONV_PF > 0 ? MDT_CONV_PF : (STAGE_REGS <= 4 ? 3 : 2);
+}
+template <class TC>
+constexpr int ig_prefetch() { return prefetch_depth<TC::BM / 32 + (TC::BN * 8 + 255) / 256>(); }
+template <int A_CH, int B_CH>
+constexpr int wg_prefetch() { return prefetch_depth<A_CH + B_CH>(); }
+
 template <class TC>
 constexpr int igemm_lds_bytes() { return 2 * (TC::BM * 128 + TC::BN * 128); }
 
@@ -294,8 +313,10 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
   const AT* Ap = reinterpret_cast<const AT*>(a.A);
   const __bf16* Bc = a.B + (size_t)cls * a.Ncols * a.K;
 
-  bf16x8 ra[A_CH], rb[B_CH];
-  auto gload = [&](int kt) {
+  // register prefetch ring: PF k-tiles in flight ahead of the LDS stage
+  constexpr int PF = ig_prefetch<TC>();
+  bf16x8 ra_s[PF][A_CH], rb_s[PF][B_CH];
+  auto gload = [&](int kt, bf16x8 (&ra)[A_CH], bf16x8 (&rb)[B_CH]) {
     const int kk = kt * 64 + 8 * ach;
     if constexpr (VEC) {
       const uint32_t tap = fdiv((uint32_t)kk, a.f_ch);
@@ -352,7 +373,7 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
       rb[i] = ok ? v : zero8();
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const bf16x8 (&ra)[A_CH], const bf16x8 (&rb)[B_CH]) {
     uint8_t* As = lds + buf * STAGE;
     uint8_t* Bs = As + A_BYTES;
 #pragma unroll
@@ -394,18 +415,23 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
     }
   };
 
-  if (kt0 < kt1) {
-    gload(kt0);
-    sstore(0);
-  }
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (kt0 + p < kt1) gload(kt0 + p, ra_s[p], rb_s[p]);
+  if (kt0 < kt1) sstore(0, ra_s[0], rb_s[0]);
   __syncthreads();
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int buf = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) gload(kt + 1);
-    compute(buf);
-    if (more) sstore(buf ^ 1);
-    __syncthreads();
+  for (int kb = kt0; kb < kt1; kb += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int kt = kb + p;
+      if (kt < kt1) {
+        const int buf = (kt - kt0) & 1;
+        if (kt + PF < kt1) gload(kt + PF, ra_s[p], rb_s[p]);  // slot p's tile is already in LDS
+        compute(buf);
+        if (kt + 1 < kt1) sstore(buf ^ 1, ra_s[(p + 1) % PF], rb_s[(p + 1) % PF]);
+        __syncthreads();
+      }
+    }
   }
 
   igemm_epilogue<MODE, TC>(a, acc, lds, mt, nt, kz, cls, oa, ob);
@@ -689,8 +715,9 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, uint8_t* lds, int bi
     kxv[j] = (int)(tap - ky * a.f_kw.d);
   }
 
-  bf16x8 ra[A_CH], rb[B_CH];
-  auto gload = [&](int mtile) {
+  constexpr int PF = wg_prefetch<A_CH, B_CH>();
+  bf16x8 ra_s[PF][A_CH], rb_s[PF][B_CH];
+  auto gload = [&](int mtile, bf16x8 (&ra)[A_CH], bf16x8 (&rb)[B_CH]) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int m = mtile * 64 + ra0 + A_RPP * i;
@@ -728,7 +755,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, uint8_t* lds, int bi
       }
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const bf16x8 (&ra)[A_CH], const bf16x8 (&rb)[B_CH]) {
     uint8_t* As = lds + buf * STAGE;
     uint8_t* Bs = As + A_BYTES;
 #pragma unroll
@@ -767,18 +794,23 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, uint8_t* lds, int bi
     }
   };
 
-  if (mt0 < mt1) {
-    gload(mt0);
-    sstore(0);
-  }
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (mt0 + p < mt1) gload(mt0 + p, ra_s[p], rb_s[p]);
+  if (mt0 < mt1) sstore(0, ra_s[0], rb_s[0]);
   __syncthreads();
-  for (int mtile = mt0; mtile < mt1; ++mtile) {
-    const int buf = (mtile - mt0) & 1;
-    const bool more = mtile + 1 < mt1;
-    if (more) gload(mtile + 1);
-    compute(buf);
-    if (more) sstore(buf ^ 1);
-    __syncthreads();
+  for (int mb = mt0; mb < mt1; mb += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int mtile = mb + p;
+      if (mtile < mt1) {
+        const int buf = (mtile - mt0) & 1;
+        if (mtile + PF < mt1) gload(mtile + PF, ra_s[p], rb_s[p]);
+        compute(buf);
+        if (mtile + 1 < mt1) sstore(buf ^ 1, ra_s[(p + 1) % PF], rb_s[(p + 1) % PF]);
+        __syncthreads();
+      }
+    }
   }
 
   wgrad_epilogue<TC>(a, acc, lds, ct, nt, split);
