@@ -315,9 +315,15 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
 
   // register prefetch ring: PF k-tiles in flight ahead of the LDS stage
   constexpr int PF = ig_prefetch<TC>();
+  // Out-of-range chunks load from a valid address and are zeroed when staged
+  // to LDS (bit i of `okm`: A chunk i, bit 16+i: B chunk i), so the loaded
+  // registers are not consumed until the LDS store: a select on them right
+  // after the load would wait for it and serialise every k-step.
   bf16x8 ra_s[PF][A_CH], rb_s[PF][B_CH];
-  auto gload = [&](int kt, bf16x8 (&ra)[A_CH], bf16x8 (&rb)[B_CH]) {
+  uint32_t okm_s[PF];
+  auto gload = [&](int kt, bf16x8 (&ra)[A_CH], bf16x8 (&rb)[B_CH], uint32_t& okm) {
     const int kk = kt * 64 + 8 * ach;
+    okm = 0u;
     if constexpr (VEC) {
       const uint32_t tap = fdiv((uint32_t)kk, a.f_ch);
       const int ch = kk - (int)(tap * a.f_ch.d);
@@ -337,10 +343,11 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
           ok = aok[i] && kok && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
           off = abase[i] + (oy * d.OW + ox) * d.CO + ch;
         }
-        const bf16x8 v = load_chunk<AT>(Ap + (ok ? off : 0));
-        ra[i] = ok ? v : zero8();
+        ra[i] = load_chunk<AT>(Ap + (ok ? off : 0));
+        okm |= (uint32_t)ok << i;
       }
     } else {
+      okm = (1u << A_CH) - 1u;  // per-element gathers are zeroed in place
       float v[A_CH][8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -369,22 +376,22 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
       const int r = (tid >> 3) + 32 * i;
       const int col = nt * BN + r;
       const bool ok = r < BN && col < a.Ncols && kk < a.K;
-      const bf16x8 v = load_chunk<__bf16>(Bc + (ok ? (size_t)col * a.K + kk : 0));
-      rb[i] = ok ? v : zero8();
+      rb[i] = load_chunk<__bf16>(Bc + (ok ? (size_t)col * a.K + kk : 0));
+      okm |= (uint32_t)ok << (16 + i);
     }
   };
-  auto sstore = [&](int buf, const bf16x8 (&ra)[A_CH], const bf16x8 (&rb)[B_CH]) {
+  auto sstore = [&](int buf, const bf16x8 (&ra)[A_CH], const bf16x8 (&rb)[B_CH], uint32_t okm) {
     uint8_t* As = lds + buf * STAGE;
     uint8_t* Bs = As + A_BYTES;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<bf16x8*>(As + rimg(r, ach)) = ra[i];
+      *reinterpret_cast<bf16x8*>(As + rimg(r, ach)) = ((okm >> i) & 1u) ? ra[i] : zero8();
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int r = (tid >> 3) + 32 * i;
-      if (r < BN) *reinterpret_cast<bf16x8*>(Bs + rimg(r, ach)) = rb[i];
+      if (r < BN) *reinterpret_cast<bf16x8*>(Bs + rimg(r, ach)) = ((okm >> (16 + i)) & 1u) ? rb[i] : zero8();
     }
   };
 
@@ -417,8 +424,8 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
 
 #pragma unroll
   for (int p = 0; p < PF; ++p)
-    if (kt0 + p < kt1) gload(kt0 + p, ra_s[p], rb_s[p]);
-  if (kt0 < kt1) sstore(0, ra_s[0], rb_s[0]);
+    if (kt0 + p < kt1) gload(kt0 + p, ra_s[p], rb_s[p], okm_s[p]);
+  if (kt0 < kt1) sstore(0, ra_s[0], rb_s[0], okm_s[0]);
   __syncthreads();
   for (int kb = kt0; kb < kt1; kb += PF) {
 #pragma unroll
@@ -426,9 +433,9 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
       const int kt = kb + p;
       if (kt < kt1) {
         const int buf = (kt - kt0) & 1;
-        if (kt + PF < kt1) gload(kt + PF, ra_s[p], rb_s[p]);  // slot p's tile is already in LDS
+        if (kt + PF < kt1) gload(kt + PF, ra_s[p], rb_s[p], okm_s[p]);  // slot p's tile is already in LDS
         compute(buf);
-        if (kt + 1 < kt1) sstore(buf ^ 1, ra_s[(p + 1) % PF], rb_s[(p + 1) % PF]);
+        if (kt + 1 < kt1) sstore(buf ^ 1, ra_s[(p + 1) % PF], rb_s[(p + 1) % PF], okm_s[(p + 1) % PF]);
         __syncthreads();
       }
     }
@@ -716,14 +723,17 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, uint8_t* lds, int bi
   }
 
   constexpr int PF = wg_prefetch<A_CH, B_CH>();
+  // masks applied at the LDS store (see igemm_body)
   bf16x8 ra_s[PF][A_CH], rb_s[PF][B_CH];
-  auto gload = [&](int mtile, bf16x8 (&ra)[A_CH], bf16x8 (&rb)[B_CH]) {
+  uint32_t okm_s[PF];
+  auto gload = [&](int mtile, bf16x8 (&ra)[A_CH], bf16x8 (&rb)[B_CH], uint32_t& okm) {
+    okm = 0u;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int m = mtile * 64 + ra0 + A_RPP * i;
       const bool ok = coka && m < a.M;
-      const bf16x8 v = load_chunk<__bf16>(a.G + (ok ? (size_t)m * d.CO + co : 0));
-      ra[i] = ok ? v : zero8();
+      ra[i] = load_chunk<__bf16>(a.G + (ok ? (size_t)m * d.CO + co : 0));
+      okm |= (uint32_t)ok << i;
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
@@ -739,9 +749,10 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, uint8_t* lds, int bi
       if constexpr (VEC) {
         const int iy = iy0 + kyv[0], ix = ix0 + kxv[0];
         const bool ok = mok && kokv[0] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-        const bf16x8 v = load_chunk<XT>(Xp + (ok ? (int)n * HWC + (iy * d.W + ix) * d.C + civ[0] : 0));
-        rb[i] = ok ? v : zero8();
+        rb[i] = load_chunk<XT>(Xp + (ok ? (int)n * HWC + (iy * d.W + ix) * d.C + civ[0] : 0));
+        okm |= (uint32_t)ok << (16 + i);
       } else {
+        okm |= 1u << (16 + i);  // per-element gathers are zeroed in place
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -755,18 +766,18 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, uint8_t* lds, int bi
       }
     }
   };
-  auto sstore = [&](int buf, const bf16x8 (&ra)[A_CH], const bf16x8 (&rb)[B_CH]) {
+  auto sstore = [&](int buf, const bf16x8 (&ra)[A_CH], const bf16x8 (&rb)[B_CH], uint32_t okm) {
     uint8_t* As = lds + buf * STAGE;
     uint8_t* Bs = As + A_BYTES;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int r = ra0 + A_RPP * i;
-      *reinterpret_cast<bf16x8*>(As + timg<BM>(r, cha)) = ra[i];
+      *reinterpret_cast<bf16x8*>(As + timg<BM>(r, cha)) = ((okm >> i) & 1u) ? ra[i] : zero8();
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int r = rb0 + B_RPP * i;
-      if (r < 64) *reinterpret_cast<bf16x8*>(Bs + timg<BN>(r, chb)) = rb[i];
+      if (r < 64) *reinterpret_cast<bf16x8*>(Bs + timg<BN>(r, chb)) = ((okm >> (16 + i)) & 1u) ? rb[i] : zero8();
     }
   };
 
@@ -796,8 +807,8 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, uint8_t* lds, int bi
 
 #pragma unroll
   for (int p = 0; p < PF; ++p)
-    if (mt0 + p < mt1) gload(mt0 + p, ra_s[p], rb_s[p]);
-  if (mt0 < mt1) sstore(0, ra_s[0], rb_s[0]);
+    if (mt0 + p < mt1) gload(mt0 + p, ra_s[p], rb_s[p], okm_s[p]);
+  if (mt0 < mt1) sstore(0, ra_s[0], rb_s[0], okm_s[0]);
   __syncthreads();
   for (int mb = mt0; mb < mt1; mb += PF) {
 #pragma unroll
@@ -805,9 +816,9 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, uint8_t* lds, int bi
       const int mtile = mb + p;
       if (mtile < mt1) {
         const int buf = (mtile - mt0) & 1;
-        if (mtile + PF < mt1) gload(mtile + PF, ra_s[p], rb_s[p]);
+        if (mtile + PF < mt1) gload(mtile + PF, ra_s[p], rb_s[p], okm_s[p]);
         compute(buf);
-        if (mtile + 1 < mt1) sstore(buf ^ 1, ra_s[(p + 1) % PF], rb_s[(p + 1) % PF]);
+        if (mtile + 1 < mt1) sstore(buf ^ 1, ra_s[(p + 1) % PF], rb_s[(p + 1) % PF], okm_s[(p + 1) % PF]);
         __syncthreads();
       }
     }
