@@ -193,3 +193,25 @@ def test_vae_hpo_profile_and_dtype_flags(tmp_path):
     assert {"eval_s", "sample_s", "ckpt_s", "epoch_train_s"} <= set(ep)
     rc, outs = _vae_hpo(tmp_path, 1, "--epochs", "1", "--ngroups", "1", "--dtype", "bf16")
     assert rc != 0 and "computes in fp32" in "\n".join(outs)
+
+
+@pytest.mark.parametrize("n,k", [(2, None), (4, 2)])
+def test_bench_contract_multirank(tmp_path, n, k):
+    """bench.py under torchrun-style env (the driver's N>1 launch): rank 0 prints ONE
+    JSON line with the BASELINE metric, n_gpus = N, trials = K, samples counted once
+    per trial (K x batch x steps / max-rank time)."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "2", "--warmup", "1",
+            "--model", "mlp", "--batch-size", "64"]
+    if k:
+        args += ["--ngroups", str(k)]
+    rc, outs = _run(args, n, "torchrun", timeout=240, cwd=str(tmp_path))
+    text = "\n".join(outs)
+    assert rc == 0, text
+    lines = [l for l in text.splitlines() if l.startswith("{\"metric\"")]
+    assert len(lines) == 1, text
+    out = json.loads(lines[0])
+    K = k or n
+    assert out["n_gpus"] == n and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["trials"] == K and out["config"]["parallelism"] == f"groups{K}x{n // K}"
+    assert out["config"]["valid"] is True
+    assert abs(out["value"] - K * 64 * 2 / (out["ms_per_step"] * 2e-3)) / out["value"] < 0.01
