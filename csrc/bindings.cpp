@@ -12,6 +12,7 @@ void probe_latency(at::Tensor idx, int64_t hops, at::Tensor out);
 void probe_empty(int64_t blocks, int64_t threads);
 void bind_conv(pybind11::module& m);
 void bind_rccl(pybind11::module& m);
+void bind_p2p(pybind11::module& m);
 }  // namespace mdt
 
 PYBIND11_MODULE(_C, m) {
@@ -22,6 +23,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("probe_empty", &mdt::probe_empty);
   mdt::bind_conv(m);
   mdt::bind_rccl(m);
+  mdt::bind_p2p(m);
 
   py::class_<mdt::MlpVaeEngine>(m, "MlpVaeEngine")
       .def(py::init<int64_t, int64_t, int64_t, int64_t, int64_t>(), py::arg("batch"),

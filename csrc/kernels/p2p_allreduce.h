@@ -1,0 +1,31 @@
+// One-shot peer-to-peer all-reduce over xGMI (host/device shared declarations).
+//
+// Included by the HIP kernel (p2p_allreduce.hip) and by the host reducer
+// (csrc/runtime/p2p_comm.cpp); plain data only.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace mdt {
+
+constexpr int kP2PMaxRanks = 8;  // one xGMI hop: a group never spans more than one node
+
+struct P2PArgs {
+  float* data;                          // this rank's bucket, reduced in place
+  long long n;                          // bucket elements
+  float* peer_recv[kP2PMaxRanks];       // every rank's receive region base (device VA in this process)
+  unsigned* peer_flags[kP2PMaxRanks];   // every rank's flag region base
+  float* my_recv;                       // == peer_recv[me]
+  unsigned* my_flags;                   // == peer_flags[me]
+  unsigned* ep;                         // per-block epoch counters of this bucket (local only)
+  int* status;                          // 0 = ok, 1 + bucket = a wait timed out
+  long long recv_off;                   // this bucket's receive slab: [2 parity][s src][n]
+  long long flag_off;                   // this bucket's flags: [s src][grid]
+  int me, s, bucket;
+  float scale;                          // 1/s for averaging
+  long long timeout_ticks;              // s_memrealtime ticks (100 MHz)
+};
+
+}  // namespace mdt
+
+extern "C" int mdt_p2p_allreduce(const mdt::P2PArgs* a, int grid, hipStream_t stream);

@@ -1,0 +1,177 @@
+// XgmiP2PReducer: one-shot peer-to-peer bucket all-reduce over xGMI (hipIpc).
+//
+// on a fully connected 8x MI355X node a group of s GPUs
+// has s-1 direct xGMI links per GPU. RCCL's ring crosses one link per step and
+// pays 2(s-1) hops of latency, which dominates the small (1-4 MB) gradient
+// buckets of the VAE models (/root/reference/vae-hpo.py:130 uses torch DDP's
+// ring all-reduce for them). This reducer pushes each bucket to every peer at
+// once (kernel: csrc/kernels/p2p_allreduce.hip) and needs no communicator:
+//   * each rank allocates ONE uncached device region (receive slabs
+//     [bucket][parity][src][n] + per-(src, block) flags + epoch counters),
+//     exports it with hipIpcGetMemHandle, and maps every peer's region with
+//     hipIpcOpenMemHandle (handles are exchanged by the caller over the gloo
+//     control plane, parallel/ddp.py::make_p2p_reducer);
+//   * launch/wait/readiness semantics, the high-priority stream and the event
+//     fences come from StreamBuckets, so it drops in for RcclBucketReducer and
+//     stays hipGraph-capturable;
+//   * waits are time-bounded in the kernel; `status()` reports a timed-out
+//     bucket instead of hanging the GPU.
+// `connect_local` maps peers that live in the same process (single-GPU tests
+// run s "ranks" on one device, each with its own stream).
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+
+#include "kernels/p2p_allreduce.h"
+#include "runtime/stream_buckets.h"
+
+namespace mdt {
+
+class XgmiP2PReducer : public StreamBuckets {
+ public:
+  XgmiP2PReducer(int64_t rank, int64_t size, at::Tensor flat, std::vector<int64_t> bounds, bool average,
+                 double scale, int64_t max_blocks, double timeout_s)
+      : StreamBuckets(std::move(flat), std::move(bounds)), me_((int)rank), s_((int)size) {
+    TORCH_CHECK(s_ >= 1 && s_ <= kP2PMaxRanks, "XgmiP2PReducer: group size must be 1..", kP2PMaxRanks);
+    TORCH_CHECK(me_ >= 0 && me_ < s_, "XgmiP2PReducer: rank out of range");
+    TORCH_CHECK(flat_.scalar_type() == torch::kFloat32, "XgmiP2PReducer: f32 gradient arena required");
+    scale_ = (float)(scale > 0 ? scale : (average ? 1.0 / s_ : 1.0));
+    timeout_ticks_ = (long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    const int64_t nb = num_buckets();
+    long long roff = 0, foff = 0, eoff = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+      const long long n = bounds_[b + 1] - bounds_[b];
+      long long g = (n + 2047) / 2048;  // >= 2K elements (8 KB) per block
+      g = std::max(1LL, std::min(g, (long long)max_blocks));
+      grid_.push_back((int)g);
+      recv_off_.push_back(roff);
+      flag_off_.push_back(foff);
+      ep_off_.push_back(eoff);
+      roff += 2LL * s_ * ((n + 63) / 64 * 64);
+      foff += (long long)s_ * g;
+      eoff += g;
+    }
+    recv_elems_ = roff;
+    // one region: [recv floats][flags u32][epochs u32][status i32], each part 256-B aligned
+    auto al = [](long long x) { return (x + 255) / 256 * 256; };
+    flags_byte_ = al(recv_elems_ * 4);
+    ep_byte_ = flags_byte_ + al(foff * 4);
+    status_byte_ = ep_byte_ + al(eoff * 4);
+    bytes_ = status_byte_ + 256;
+    DeviceGuard dg(device_);
+    MDT_HIP_CHECK(hipExtMallocWithFlags(&base_, (size_t)bytes_, hipDeviceMallocUncached));
+    MDT_HIP_CHECK(hipMemset((char*)base_ + flags_byte_, 0, (size_t)(bytes_ - flags_byte_)));
+    MDT_HIP_CHECK(hipDeviceSynchronize());
+    for (int p = 0; p < kP2PMaxRanks; ++p) peer_base_[p] = nullptr;
+    peer_base_[me_] = base_;
+  }
+
+  ~XgmiP2PReducer() override {
+    DeviceGuard dg(device_);
+    (void)hipStreamSynchronize(stream_);
+    for (int p = 0; p < s_; ++p)
+      if (p != me_ && peer_base_[p] && opened_[p]) (void)hipIpcCloseMemHandle(peer_base_[p]);
+    if (base_) (void)hipFree(base_);
+  }
+
+  // 64-byte hipIpcMemHandle_t of this rank's region (uint8 CPU tensor)
+  at::Tensor ipc_handle() {
+    DeviceGuard dg(device_);
+    hipIpcMemHandle_t h;
+    MDT_HIP_CHECK(hipIpcGetMemHandle(&h, base_));
+    auto t = torch::empty({(int64_t)sizeof(h)}, torch::kUInt8);
+    std::memcpy(t.data_ptr(), &h, sizeof(h));
+    return t;
+  }
+  int64_t local_base() const { return (int64_t)(uintptr_t)base_; }
+  int64_t region_bytes() const { return bytes_; }
+
+  void connect(std::vector<at::Tensor> handles) {
+    TORCH_CHECK((int)handles.size() == s_, "connect: need one handle per rank");
+    DeviceGuard dg(device_);
+    for (int p = 0; p < s_; ++p) {
+      if (p == me_) continue;
+      TORCH_CHECK(handles[p].numel() == (int64_t)sizeof(hipIpcMemHandle_t), "bad IPC handle size");
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, handles[p].contiguous().data_ptr(), sizeof(h));
+      void* ptr = nullptr;
+      MDT_HIP_CHECK(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
+      peer_base_[p] = ptr;
+      opened_[p] = true;
+    }
+    connected_ = true;
+  }
+  void connect_local(std::vector<int64_t> bases) {
+    TORCH_CHECK((int)bases.size() == s_, "connect_local: need one base per rank");
+    for (int p = 0; p < s_; ++p)
+      if (p != me_) peer_base_[p] = (void*)(uintptr_t)bases[p];
+    connected_ = true;
+  }
+
+  int64_t status() {
+    DeviceGuard dg(device_);
+    int v = 0;
+    MDT_HIP_CHECK(hipStreamSynchronize(stream_));
+    MDT_HIP_CHECK(hipMemcpy(&v, (char*)base_ + status_byte_, sizeof(int), hipMemcpyDeviceToHost));
+    return v;
+  }
+  double scale() const { return scale_; }
+  std::vector<int64_t> grids() const { return std::vector<int64_t>(grid_.begin(), grid_.end()); }
+
+ protected:
+  void issue(int64_t b, hipStream_t s) override {
+    TORCH_CHECK(connected_ || s_ == 1, "XgmiP2PReducer: connect() before launching");
+    P2PArgs a{};
+    a.data = (float*)flat_.data_ptr() + bounds_[b];
+    a.n = bounds_[b + 1] - bounds_[b];
+    for (int p = 0; p < kP2PMaxRanks; ++p) {
+      a.peer_recv[p] = p < s_ ? (float*)peer_base_[p] : nullptr;
+      a.peer_flags[p] = p < s_ ? (unsigned*)((char*)peer_base_[p] + flags_byte_) : nullptr;
+    }
+    a.my_recv = (float*)base_;
+    a.my_flags = (unsigned*)((char*)base_ + flags_byte_);
+    a.ep = (unsigned*)((char*)base_ + ep_byte_) + ep_off_[b];
+    a.status = (int*)((char*)base_ + status_byte_);
+    a.recv_off = recv_off_[b];
+    a.flag_off = flag_off_[b];
+    a.me = me_;
+    a.s = s_;
+    a.bucket = (int)b;
+    a.scale = scale_;
+    a.timeout_ticks = timeout_ticks_;
+    if (s_ == 1 && scale_ == 1.0f) return;
+    const int rc = mdt_p2p_allreduce(&a, grid_[b], s);
+    TORCH_CHECK(rc == 0, "p2p all-reduce launch failed: ", rc);
+  }
+
+ private:
+  int me_, s_;
+  float scale_ = 1.0f;
+  long long timeout_ticks_ = 0;
+  void* base_ = nullptr;
+  void* peer_base_[kP2PMaxRanks];
+  bool opened_[kP2PMaxRanks] = {};
+  bool connected_ = false;
+  long long recv_elems_ = 0, flags_byte_ = 0, ep_byte_ = 0, status_byte_ = 0, bytes_ = 0;
+  std::vector<int> grid_;
+  std::vector<long long> recv_off_, flag_off_, ep_off_;
+};
+
+void bind_p2p(pybind11::module& m) {
+  namespace py = pybind11;
+  auto c = py::class_<XgmiP2PReducer>(m, "XgmiP2PReducer")
+               .def(py::init<int64_t, int64_t, at::Tensor, std::vector<int64_t>, bool, double, int64_t, double>(),
+                    py::arg("rank"), py::arg("size"), py::arg("flat"), py::arg("bounds"), py::arg("average") = true,
+                    py::arg("scale") = 0.0, py::arg("max_blocks") = 64, py::arg("timeout_s") = 60.0)
+               .def("ipc_handle", &XgmiP2PReducer::ipc_handle)
+               .def("local_base", &XgmiP2PReducer::local_base)
+               .def("region_bytes", &XgmiP2PReducer::region_bytes)
+               .def("connect", &XgmiP2PReducer::connect)
+               .def("connect_local", &XgmiP2PReducer::connect_local)
+               .def("status", &XgmiP2PReducer::status)
+               .def("scale", &XgmiP2PReducer::scale)
+               .def("grids", &XgmiP2PReducer::grids);
+  def_bucket_api(c);
+}
+
+}  // namespace mdt

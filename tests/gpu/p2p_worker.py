@@ -1,0 +1,70 @@
+"""Worker for tests/gpu/test_p2p_reducer.py: s processes share the box's single
+MI355X, exchange hipIpc handles of their receive regions over gloo, and run the
+one-shot p2p all-reduce kernel (eager and graph-replayed). Prints RESULT json."""
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def main():
+    dist.init_process_group("gloo")
+    r, s = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+
+    n = 300_001
+    bounds = [0, 1000, 65_536, n]
+    flat = torch.zeros(n, device=dev)
+    os.environ["MDT_P2P_TIMEOUT_S"] = "10"
+    red = make_arena_reducer(dist.group.WORLD, flat, bounds, kind="p2p")
+    gen = lambda rank, it: torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + rank))
+    errs, iters = [], 5
+    for it in range(iters):
+        flat.copy_(gen(r, it).to(dev))
+        torch.cuda.synchronize()
+        red.launch_all()
+        red.wait_all()
+        torch.cuda.synchronize()
+        ref = sum(gen(p, it).double() for p in range(s)) / s
+        errs.append(float((flat.cpu().double() - ref).abs().max()))
+    st = red.status()
+    # bitwise identical on every replica
+    out = [torch.empty(n) for _ in range(s)]
+    dist.all_gather(out, flat.cpu())
+    same = all(torch.equal(out[0], o) for o in out)
+    # hipGraph: capture launch+wait once, replay with fresh inputs
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cs):
+        red.launch_all()
+        red.wait_all()
+    torch.cuda.synchronize()
+    dist.barrier()
+    gerrs = []
+    for it in range(iters, iters + 3):
+        flat.copy_(gen(r, it).to(dev))
+        torch.cuda.synchronize()
+        dist.barrier()
+        g.replay()
+        torch.cuda.synchronize()
+        ref = sum(gen(p, it).double() for p in range(s)) / s
+        gerrs.append(float((flat.cpu().double() - ref).abs().max()))
+    st2 = red.status()
+    dist.barrier()  # peers stop touching our region before it is freed
+    del g, red
+    torch.cuda.synchronize()
+    dist.barrier()
+    print("RESULT " + json.dumps({"rank": r, "errs": errs, "gerrs": gerrs, "status": [st, st2], "same": same}),
+          flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

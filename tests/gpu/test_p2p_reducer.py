@@ -1,0 +1,121 @@
+"""One-shot peer-to-peer bucket all-reduce (csrc/kernels/p2p_allreduce.hip,
+csrc/runtime/p2p_comm.cpp) vs a float64 torch reference of the mean.
+
+A gpurun box has one MI355X, so the "peers" share it:
+  * in-process: s reducers on one device, each with its own stream, mapped to
+    each other's regions directly (connect_local);
+  * multi-process: s processes on the same device exchange hipIpc handles over
+    gloo (the production path, minus the xGMI hop).
+Every wait in the kernel is time-bounded, so a missing peer shows up as a
+status code, never as a hung GPU (test_missing_peer_times_out).
+"""
+import json
+import sys
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+
+
+def _pair(C, s, n, bounds, timeout=5.0):
+    dev = torch.device("cuda", 0)
+    flats = [torch.zeros(n, device=dev) for _ in range(s)]
+    reds = [C.XgmiP2PReducer(r, s, flats[r], bounds, True, 0.0, 64, timeout) for r in range(s)]
+    bases = [r.local_base() for r in reds]
+    for r in reds:
+        r.connect_local(bases)
+    return flats, reds
+
+
+def _fill(flats, it):
+    g = torch.Generator().manual_seed(it)
+    vals = [torch.randn(f.numel(), generator=g) for f in flats]
+    for f, v in zip(flats, vals):
+        f.copy_(v.to(f.device))
+    return sum(v.double() for v in vals) / len(vals)
+
+
+def test_p2p_in_process_eager_and_graph(native_ext):
+    C = native_ext
+    n = 200_003  # odd size: vector body + scalar tail; tiny first bucket = one block
+    bounds = [0, 100, 4096, 70_000, n]
+    flats, reds = _pair(C, 2, n, bounds)
+    assert reds[0].num_buckets() == 4 and reds[0].grids()[0] == 1 and reds[0].grids()[3] <= 64
+    for it in range(4):  # both epoch parities, twice
+        ref = _fill(flats, it)
+        torch.cuda.synchronize()
+        for r in reds:
+            r.launch_all()
+        for r in reds:
+            r.wait_all()
+        torch.cuda.synchronize()
+        assert [r.status() for r in reds] == [0, 0]
+        assert torch.equal(flats[0], flats[1])  # rank-ordered sum: identical replicas
+        torch.testing.assert_close(flats[0].cpu().double(), ref, rtol=0, atol=1e-6)
+    # readiness counting launches a bucket when its last parameter is marked
+    for r in reds:
+        r.set_param_map([0, 1, 1, 2, 3])
+    ref = _fill(flats, 10)
+    torch.cuda.synchronize()
+    for p in range(5):
+        for r in reds:
+            r.mark_ready(p)
+    assert reds[0].pending() == 4
+    for r in reds:
+        r.wait_all()
+        r.reset_iteration()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(flats[1].cpu().double(), ref, rtol=0, atol=1e-6)
+    # hipGraph capture per "rank", replays on separate streams
+    graphs, streams = [], [torch.cuda.Stream() for _ in reds]
+    for r, st in zip(reds, streams):
+        st.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            r.launch_all()
+            r.wait_all()
+        graphs.append(g)
+    torch.cuda.synchronize()
+    for it in range(20, 23):
+        ref = _fill(flats, it)
+        torch.cuda.synchronize()
+        for g, st in zip(graphs, streams):
+            with torch.cuda.stream(st):
+                g.replay()
+        torch.cuda.synchronize()
+        assert [r.status() for r in reds] == [0, 0]
+        assert torch.equal(flats[0], flats[1])
+        torch.testing.assert_close(flats[0].cpu().double(), ref, rtol=0, atol=1e-6)
+
+
+def test_missing_peer_times_out(native_ext):
+    """Rank 1 never launches: rank 0's blocks give up after the timeout and
+    report the first bucket instead of spinning forever."""
+    C = native_ext
+    flats, reds = _pair(C, 2, 8192, [0, 4096, 8192], timeout=0.2)
+    reds[0].launch_all()
+    reds[0].wait_all()
+    torch.cuda.synchronize()
+    assert reds[0].status() == 1
+
+
+@pytest.mark.parametrize("s", [2, 4])
+def test_p2p_multiprocess_ipc(s):
+    from multidisttorch_amd.launch import launch
+
+    env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2"}
+    rc, outs = launch([sys.executable, os.path.join(HERE, "p2p_worker.py")], s, emulate="torchrun", timeout=100,
+                      extra_env=env, capture=True)
+    text = "\n".join(o or "" for o in outs)
+    assert rc == 0, text[-4000:]
+    res = [json.loads(l[7:]) for l in text.splitlines() if l.startswith("RESULT ")]
+    assert len(res) == s, text[-4000:]
+    for r in res:
+        assert r["status"] == [0, 0], r
+        assert r["same"], r
+        assert max(r["errs"] + r["gerrs"]) < 1e-5, r
