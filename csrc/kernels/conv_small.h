@@ -181,11 +181,91 @@ struct FinalizeArgs {
 
 constexpr int kFinalizeThreads = 256;
 
+// Units of more than 256 elements (planned when a segment has <= 16 partial
+// slabs and 16-B aligned rows): each thread finalizes 4 consecutive elements
+// with 16-B loads/stores -- same per-element summation order as the scalar
+// path (4 interleaved accumulators over the slabs), so results are unchanged.
+// The optimizer tail streams P, m, v (+ slabs) once: 16-B accesses keep
+// 4x the bytes in flight per wave-instruction of the 4-B path.
+__device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const AdamC& c, const GradUnit& u,
+                                                   const GradSeg& sg) {
+  const int e0 = u.start + 4 * (int)threadIdx.x;
+  const int left = u.start + u.count - e0;
+  if (left <= 0) return;
+  const long long o = sg.off + e0;
+  const long long n = sg.numel;
+  if (left >= 4) {
+    f32x4 g;
+    if (sg.slab) {
+      const float* p = sg.slab + e0;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      f32x4 a0 = z, a1 = z, a2 = z, a3 = z;
+      int s = 0;
+      for (; s + 3 < sg.nsplit; s += 4) {
+        a0 += *reinterpret_cast<const f32x4*>(p + (long long)s * n);
+        a1 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 1) * n);
+        a2 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 2) * n);
+        a3 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 3) * n);
+      }
+      for (; s < sg.nsplit; ++s) a0 += *reinterpret_cast<const f32x4*>(p + (long long)s * n);
+      g = z + ((a0 + a1) + (a2 + a3));
+      if (!a.do_adam) *reinterpret_cast<f32x4*>(a.G + o) = g;
+    } else {
+      g = *reinterpret_cast<const f32x4*>(a.G + o);
+    }
+    if (a.do_adam) {
+      f32x4 p = *reinterpret_cast<const f32x4*>(a.P + o);
+      f32x4 m = *reinterpret_cast<const f32x4*>(a.Mo + o);
+      f32x4 v = *reinterpret_cast<const f32x4*>(a.Vo + o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) adam_update(p[j], m[j], v[j], g[j], c);
+      *reinterpret_cast<f32x4*>(a.P + o) = p;
+      *reinterpret_cast<f32x4*>(a.Mo + o) = m;
+      *reinterpret_cast<f32x4*>(a.Vo + o) = v;
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = (__bf16)p[j];
+      *reinterpret_cast<bf16x4*>(a.w16 + o) = w;
+    }
+    return;
+  }
+  for (int j = 0; j < left; ++j) {  // segment tail (< 4 elements)
+    float g;
+    if (sg.slab) {
+      const float* p = sg.slab + e0 + j;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int s = 0;
+      for (; s + 3 < sg.nsplit; s += 4) {
+        a0 += p[(long long)s * n];
+        a1 += p[(long long)(s + 1) * n];
+        a2 += p[(long long)(s + 2) * n];
+        a3 += p[(long long)(s + 3) * n];
+      }
+      for (; s < sg.nsplit; ++s) a0 += p[(long long)s * n];
+      g = 0.f + ((a0 + a1) + (a2 + a3));
+      if (!a.do_adam) a.G[o + j] = g;
+    } else {
+      g = a.G[o + j];
+    }
+    if (a.do_adam) {
+      float p = a.P[o + j], m = a.Mo[o + j], v = a.Vo[o + j];
+      adam_update(p, m, v, g, c);
+      a.P[o + j] = p; a.Mo[o + j] = m; a.Vo[o + j] = v;
+      a.w16[o + j] = (__bf16)p;
+    }
+  }
+}
+
 __device__ __forceinline__ void grad_finalize_body(const FinalizeArgs& a, float* red, AdamC* cs, int bid) {
   AdamC c{};
   if (a.do_adam) c = adam_consts_block(a.st, a.hp, cs);
   const GradUnit u = a.units[bid];
   const GradSeg sg = a.segs[u.seg];
+  if (u.count > kFinalizeThreads) {
+    grad_finalize_vec4(a, c, u, sg);
+    return;
+  }
   const int t = threadIdx.x, cnt = u.count, rp = kFinalizeThreads / cnt;
   const int col = t % cnt, rl = t / cnt;
   float acc = 0.f;

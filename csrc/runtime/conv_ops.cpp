@@ -331,7 +331,8 @@ at::Tensor make_grad_segs(const std::vector<std::vector<int64_t>>& segs, int64_t
 at::Tensor make_grad_units(const std::vector<std::vector<int64_t>>& units, int64_t device_index) {
   std::vector<GradUnit> v;
   for (auto& u : units) {
-    TORCH_CHECK(u.size() == 3 && u[2] >= 1 && u[2] <= 512, "unit = (seg, start, count<=512)");
+    // count <= 256: one element (column) per thread group; 256 < count <= 1024: 4 elements per thread
+    TORCH_CHECK(u.size() == 3 && u[2] >= 1 && u[2] <= 1024, "unit = (seg, start, count<=1024)");
     v.push_back(GradUnit{(int)u[0], (int)u[1], (int)u[2]});
   }
   auto cpu = torch::empty({(int64_t)std::max<size_t>(1, v.size() * sizeof(GradUnit))}, torch::kUInt8);

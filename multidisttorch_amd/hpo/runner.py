@@ -34,7 +34,7 @@ from ..ckpt import checkpoint as ckpt
 from ..data.sampler import shard_indices
 from ..obs.metrics import TrialMetrics
 from ..obs import trace
-from ..parallel.autotune import autotune_buckets
+from ..parallel.autotune import autotune_comm
 from ..parallel.ddp import broadcast_params, make_arena_reducer
 from ..parallel.groups import print0
 from ..runtime.bootstrap import bound_device, global_barrier
@@ -189,12 +189,13 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
         if opts.bucket_mb == "auto":
             idx0 = shard_indices(len(train), K, spec.group_id)
             key = f"{opts.model}-{opts.image_size}-b{opts.batch_size}-n{trainer.numel}-s{gsize}"
-            bounds, timings = autotune_buckets(lambda: _make_trainer(spec, opts, device, grank, D), group,
-                                               train.data, idx0, key=key)
-            print0(f"bucket autotune (group of {gsize}): {timings} -> {bounds}", process_group=group)
+            bounds, kind, timings = autotune_comm(lambda: _make_trainer(spec, opts, device, grank, D), group,
+                                                  train.data, idx0, key=key)
+            print0(f"bucket autotune (group of {gsize}): {timings} -> {kind or 'default'} {bounds}",
+                   process_group=group)
         else:
-            bounds = trainer.bucket_bounds(opts.bucket_mb)
-        trainer.attach_reducer(make_arena_reducer(group, trainer.grads, bounds))
+            bounds, kind = trainer.bucket_bounds(opts.bucket_mb), None
+        trainer.attach_reducer(make_arena_reducer(group, trainer.grads, bounds, kind=kind))
     start_epoch = 1
     if opts.ckpt_dir and opts.resume:
         prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer)

@@ -551,6 +551,8 @@ class ConvVaeTrainer:
                 while rp < 256 and rp * 16 < ns:
                     rp *= 2
             cnt = 256 // rp
+            if rp == 1 and numel % 4 == 0 and off % 4 == 0 and ptr % 16 == 0:
+                cnt = 4 * 256  # grad_finalize_vec4: 4 elements per thread, 16-B accesses
             for st in range(0, numel, cnt):
                 units.append([si, st, min(cnt, numel - st)])
         layer_units.append(len(units))  # layer i owns units [layer_units[i], layer_units[i+1])

@@ -9,12 +9,16 @@ this module *measures*: every candidate layout is timed on a throw-away
 trainer of the same configuration (so the real trial's state is untouched),
 the per-rank times are max-reduced over the group so every member picks the
 same layout, and the winner is cached per (model, group size, batch, arena).
+``autotune_comm`` searches the reducer too: RCCL's ring (``rccl``) against the
+one-shot hipIpc push over all s-1 xGMI links (``p2p``, csrc/runtime/p2p_comm.cpp)
+for every layout, when the group is on GPUs of one node.
 """
 
 from __future__ import annotations
 
 import json
 import os
+import socket
 import time
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -23,7 +27,7 @@ import torch.distributed as dist
 
 from .ddp import make_arena_reducer
 
-__all__ = ["autotune_buckets", "bucket_cache_path", "parse_bucket_mb"]
+__all__ = ["autotune_buckets", "autotune_comm", "bucket_cache_path", "parse_bucket_mb", "comm_kinds"]
 
 
 def bucket_cache_path() -> str:
@@ -61,23 +65,50 @@ def _store_cache(path: str, key: str, entry: dict) -> None:
         pass
 
 
+def comm_kinds(pg, device: torch.device) -> List[Optional[str]]:
+    """Reducer kinds worth timing for this group: RCCL and the hipIpc p2p push
+    when every member drives a GPU of the same node; otherwise the default."""
+    if device.type != "cuda" or not dist.is_initialized() or dist.get_backend(pg) != "nccl":
+        return [None]
+    hosts = [None] * dist.get_world_size(pg)
+    dist.all_gather_object(hosts, socket.gethostname(), group=pg)
+    return ["rccl", "p2p"] if len(set(hosts)) == 1 else ["rccl"]
+
+
 def autotune_buckets(make_trainer: Callable[[], object], pg, X: torch.Tensor, idx: torch.Tensor,
                      candidates: Sequence = (None, 0, 1, 2, 4, 8, 16), steps: int = 6, warmup: int = 2,
                      key: Optional[str] = None, cache: Optional[str] = None,
                      use_cache: bool = True) -> Tuple[List[int], Dict[str, float]]:
-    """Time each candidate bucket layout; return (best bounds, {layout: seconds}).
+    """Time each candidate bucket layout with the default reducer; return
+    (best bounds, {layout: seconds}). See ``autotune_comm``."""
+    bounds, _, timings = autotune_comm(make_trainer, pg, X, idx, candidates, steps, warmup, key, cache,
+                                       use_cache, kinds=[None])
+    return bounds, timings
+
+
+def autotune_comm(make_trainer: Callable[[], object], pg, X: torch.Tensor, idx: torch.Tensor,
+                  candidates: Sequence = (None, 0, 1, 2, 4, 8, 16), steps: int = 6, warmup: int = 2,
+                  key: Optional[str] = None, cache: Optional[str] = None, use_cache: bool = True,
+                  kinds: Optional[Sequence[Optional[str]]] = None
+                  ) -> Tuple[List[int], Optional[str], Dict[str, float]]:
+    """Time every (reducer kind, bucket layout) pair; return (bounds, kind, timings).
 
     ``make_trainer()`` builds a fresh trainer with the real trial's config;
     candidate ``c`` becomes ``trainer.bucket_bounds(c)`` (duplicates collapse).
+    ``kinds`` defaults to ``comm_kinds(pg, device)``; ``None`` = the default reducer.
     Collective: every member of ``pg`` must call with the same arguments.
     """
     tr = make_trainer()
     gsize = dist.get_world_size(pg) if dist.is_initialized() else 1
     cache = cache or bucket_cache_path()
-    if key is not None and use_cache:
-        hit = _load_cache(cache).get(key)
+    if kinds is None:
+        kinds = comm_kinds(pg, tr.device)
+    kinds = list(kinds)
+    ckey = None if key is None else (key if kinds == [None] else f"{key}-{'+'.join(map(str, kinds))}")
+    if ckey is not None and use_cache:
+        hit = _load_cache(cache).get(ckey)
         if hit is not None and hit.get("group_size") == gsize:
-            return list(hit["bounds"]), dict(hit.get("timings", {}))
+            return list(hit["bounds"]), hit.get("kind"), dict(hit.get("timings", {}))
     layouts, seen = [], set()
     for c in candidates:
         b = tuple(int(x) for x in tr.bucket_bounds(c))
@@ -91,29 +122,33 @@ def autotune_buckets(make_trainer: Callable[[], object], pg, X: torch.Tensor, id
     on_gpu = dev.type == "cuda"
     t_dev = dev if (on_gpu and dist.is_initialized() and dist.get_backend(pg) == "nccl") else torch.device("cpu")
     timings: Dict[str, float] = {}
-    best, best_t = layouts[0], float("inf")
-    for bounds in layouts:
-        tr.set_cursor(0, nb)
-        tr.attach_reducer(make_arena_reducer(pg, tr.grads, bounds))
-        tr.train_steps(warmup)
-        if on_gpu:
-            torch.cuda.synchronize(dev)
-        if gsize > 1:
-            dist.barrier(group=pg)
-        t0 = time.perf_counter()
-        tr.train_steps(steps)
-        if on_gpu:
-            torch.cuda.synchronize(dev)
-        dt = time.perf_counter() - t0
-        t = torch.tensor([dt], dtype=torch.float64 if t_dev.type == "cpu" else torch.float32, device=t_dev)
-        if gsize > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=pg)
-        dt = float(t.item()) / steps
-        timings[",".join(map(str, bounds))] = dt
-        if dt < best_t:
-            best, best_t = bounds, dt
+    best, best_kind, best_t = layouts[0], kinds[0], float("inf")
+    for kind in kinds:
+        for bounds in layouts:
+            tr.set_cursor(0, nb)
+            # the previous reducer is dropped here: every member finished its kernels
+            # before the MAX all-reduce below, so no peer still writes into its region
+            tr.attach_reducer(make_arena_reducer(pg, tr.grads, bounds, kind=kind))
+            tr.train_steps(warmup)
+            if on_gpu:
+                torch.cuda.synchronize(dev)
+            if gsize > 1:
+                dist.barrier(group=pg)
+            t0 = time.perf_counter()
+            tr.train_steps(steps)
+            if on_gpu:
+                torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            t = torch.tensor([dt], dtype=torch.float64 if t_dev.type == "cpu" else torch.float32, device=t_dev)
+            if gsize > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=pg)
+            dt = float(t.item()) / steps
+            label = ",".join(map(str, bounds))
+            timings[label if kind is None else f"{kind}:{label}"] = dt
+            if dt < best_t:
+                best, best_kind, best_t = bounds, kind, dt
     tr.attach_reducer(None)
-    if key is not None and (not dist.is_initialized() or dist.get_rank(pg) == 0):
-        _store_cache(cache, key, {"bounds": best, "timings": timings, "group_size": gsize,
-                                  "when": time.strftime("%Y-%m-%dT%H:%M:%S")})
-    return best, timings
+    if ckey is not None and (not dist.is_initialized() or dist.get_rank(pg) == 0):
+        _store_cache(cache, ckey, {"bounds": best, "kind": best_kind, "timings": timings, "group_size": gsize,
+                                   "when": time.strftime("%Y-%m-%dT%H:%M:%S")})
+    return best, best_kind, timings

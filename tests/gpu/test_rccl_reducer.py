@@ -124,3 +124,32 @@ def test_trial_groups_split_from_device_bound_world(nccl_world, native_ext):
     red.wait_all()
     torch.cuda.synchronize()
     torch.testing.assert_close(flat, ref)
+
+
+def test_autotune_comm_times_rccl_and_p2p(nccl_world, native_ext, tmp_path):
+    """The measured autotuner searches (reducer kind x bucket layout) on a GPU
+    group; on one rank both reducers are identities, so training is unchanged."""
+    import numpy as np
+
+    from multidisttorch_amd.models.mlp_trainer import MlpVaeTrainer
+    from multidisttorch_amd.parallel.autotune import autotune_comm
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+
+    dev = torch.device("cuda", 0)
+    X = torch.rand(1024, 784, device=dev)
+    idx = torch.arange(1024, device=dev, dtype=torch.int32)
+    make = lambda: MlpVaeTrainer(batch_size=128, device=dev, backend="hip", seed=3, use_graphs=True, graph_steps=4)
+    bounds, kind, timings = autotune_comm(make, nccl_world, X, idx, candidates=(None, 0), steps=4, warmup=2,
+                                          key="gpu-test", cache=str(tmp_path / "b.json"))
+    assert kind in ("rccl", "p2p")
+    assert any(k.startswith("p2p:") for k in timings) and any(k.startswith("rccl:") for k in timings)
+    hist = []
+    for k in ("rccl", "p2p"):
+        tr = make()
+        tr.attach_reducer(make_arena_reducer(nccl_world, tr.grads, bounds, kind=k))
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 8)
+        tr.train_steps(8)
+        torch.cuda.synchronize()
+        hist.append(tr.loss_history()[:8].copy())
+    np.testing.assert_array_equal(hist[0], hist[1])
