@@ -218,7 +218,11 @@ __device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const 
       f32x4 m = *reinterpret_cast<const f32x4*>(a.Mo + o);
       f32x4 v = *reinterpret_cast<const f32x4*>(a.Vo + o);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) adam_update(p[j], m[j], v[j], g[j], c);
+      for (int j = 0; j < 4; ++j) {
+        float pj = p[j], mj = m[j], vj = v[j];
+        adam_update(pj, mj, vj, g[j], c);
+        p[j] = pj; m[j] = mj; v[j] = vj;
+      }
       *reinterpret_cast<f32x4*>(a.P + o) = p;
       *reinterpret_cast<f32x4*>(a.Mo + o) = m;
       *reinterpret_cast<f32x4*>(a.Vo + o) = v;
