@@ -65,8 +65,14 @@ bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p) {
   if (q.thin) q.BN = 32;
   q.ntiles = cdiv(q.Ncols, q.BN);
   q.ktiles = cdiv(q.K, 64);
+  // 64-row tiles when 128-row tiles would leave the grid under `bm64_below`
+  // blocks (MDT_CONV_BM64_BELOW, default 512 = 2 per CU)
+  static const int bm64_below = [] {
+    const char* e = getenv("MDT_CONV_BM64_BELOW");
+    return e ? atoi(e) : 512;
+  }();
   q.BM = 128;
-  if ((long long)q.classes * cdiv(q.M, 128) * q.ntiles < 512) q.BM = 64;
+  if ((long long)q.classes * cdiv(q.M, 128) * q.ntiles < bm64_below) q.BM = 64;
   q.mtiles = cdiv(q.M, q.BM);
   const long long blocks = (long long)q.classes * q.mtiles * q.ntiles;
   q.ksplit = 1;
@@ -76,9 +82,16 @@ bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p) {
     const char* e = getenv("MDT_CONV_SPLIT_MIN_KT");
     return e ? atoi(e) : 16;
   }();
+  // at least `kt_per` k-tiles per split (MDT_CONV_SPLIT_KT_PER): fewer k-steps
+  // per block against more partial slabs for the combine pass to read
+  static const int kt_per = [] {
+    const char* e = getenv("MDT_CONV_SPLIT_KT_PER");
+    const int v = e ? atoi(e) : 4;
+    return v < 1 ? 1 : v;
+  }();
   if (allow_split && q.classes == 1 && blocks < 256 && q.ktiles >= min_kt) {
     int ks = cdiv(512, blocks);
-    if (ks > q.ktiles / 4) ks = q.ktiles / 4;
+    if (ks > q.ktiles / kt_per) ks = q.ktiles / kt_per;
     if (ks < 1) ks = 1;
     q.ksplit = ks;
   }
@@ -104,7 +117,13 @@ bool plan_wgrad(const ConvDesc& d, WgradPlan* p) {
   q.ktiles = cdiv(q.K2, q.BN);
   q.mtiles = cdiv(q.M, 64);
   const int tiles = q.cotiles * q.ktiles;
-  int ns = cdiv(320, tiles);
+  // m-splits so the grid reaches ~`target` blocks (MDT_CONV_WG_TARGET, default 320)
+  static const int target = [] {
+    const char* e = getenv("MDT_CONV_WG_TARGET");
+    const int v = e ? atoi(e) : 320;
+    return v < 1 ? 1 : v;
+  }();
+  int ns = cdiv(target, tiles);
   if (ns > q.mtiles / 2) ns = q.mtiles / 2;
   if (ns < 1) ns = 1;
   q.mt_per_split = cdiv(q.mtiles, ns);

@@ -10,7 +10,7 @@ timeout -k 10 180 python3 bench.py > $O/bench_conv28.json 2> $O/bench_conv28.err
 timeout -k 10 180 python3 bench.py --model conv128 --batch-size 64 > $O/bench_conv128.json 2> $O/bench_conv128.err || exit 1
 timeout -k 10 180 python3 bench.py --model mlp > $O/bench_mlp.json 2> $O/bench_mlp.err || exit 1
 cat $O/bench_*.json
-OUT=$O/tl
+OUT=$GRAFT_REPO_ROOT/$O/tl
 mkdir -p $OUT
 cd /tmp
 for m in conv28 conv128; do
