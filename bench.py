@@ -72,10 +72,13 @@ def main(argv=None):
     from multidisttorch_amd.models.mlp_trainer import MlpVaeTrainer
     from multidisttorch_amd.parallel.ddp import make_arena_reducer
 
-    world, rank = setup_ddp(verbose=False)
-    K = a.ngroups or world
-    handles = setup_ddp_groups(K, verbose=False)
-    ctrl = control_group()
+    from multidisttorch_amd.runtime.bootstrap import _stdout_to_stderr
+
+    with _stdout_to_stderr():  # keep stdout for the single JSON line (gloo prints connect banners)
+        world, rank = setup_ddp(verbose=False)
+        K = a.ngroups or world
+        handles = setup_ddp_groups(K, verbose=False)
+        ctrl = control_group()
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     n_per = world // K
     gid = rank // n_per if rank < K * n_per else None

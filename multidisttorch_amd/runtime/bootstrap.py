@@ -19,7 +19,9 @@ MI355X-first differences:
 from __future__ import annotations
 
 import datetime as _dt
+import contextlib
 import os
+import sys
 from typing import Optional
 
 import torch
@@ -134,6 +136,20 @@ def setup_ddp(backend: Optional[str] = None, verbose: bool = True,
     return world_size, world_rank
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Point fd 1 at fd 2 for the duration (native libraries write to fd 1 directly)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def control_group():
     """World-spanning gloo process group for control-plane barriers.
 
@@ -147,8 +163,11 @@ def control_group():
         if dist.get_backend() == "gloo":
             _STATE["control"] = dist.group.WORLD
         else:
-            _STATE["control"] = dist.new_group(backend="gloo",
-                                               timeout=_dt.timedelta(hours=6))
+            # gloo's C++ connect banner goes to fd 1; keep stdout for the
+            # caller's own output (bench.py's single JSON line)
+            with _stdout_to_stderr():
+                _STATE["control"] = dist.new_group(backend="gloo",
+                                                   timeout=_dt.timedelta(hours=6))
     return _STATE["control"]
 
 

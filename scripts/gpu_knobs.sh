@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 run() {  # name model bs env...
   local name=$1 m=$2 bs=$3; shift 3
   env "$@" timeout -k 10 120 python3 bench.py --model $m --batch-size $bs --steps 300 --warmup 30 > $O/$name.json 2> $O/$name.err || { tail -5 $O/$name.err; return 1; }
-  python3 -c "import json,sys; d=json.load(open('$O/$name.json')); print('$name', d['ms_per_step'], d['config']['valid'])"
+  python3 -c "import json,sys; d=json.loads([l for l in open('$O/$name.json') if l.startswith('{')][-1]); print('$name', d['ms_per_step'], d['config']['valid'])"
 }
 run c28_base conv28 128 MDT_X=0 || exit 1
 run c28_kt1 conv28 128 MDT_CONV_SPLIT_KT_PER=1 || exit 1
