@@ -21,6 +21,8 @@
 // blockIdx remapped so neighbouring tiles share an XCD's L2.
 // Epilogues fuse bias, ReLU, the ReLU-backward mask of the produced gradient
 // and the per-block column sums that become the next layer's bias gradient.
+#include <algorithm>
+
 #include "conv_igemm_dev.h"
 
 namespace mdt {
@@ -66,27 +68,30 @@ bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p) {
   q.ntiles = cdiv(q.Ncols, q.BN);
   q.ktiles = cdiv(q.K, 64);
   // 64-row tiles when 128-row tiles would leave the grid under `bm64_below`
-  // blocks (MDT_CONV_BM64_BELOW, default 512 = 2 per CU)
+  // blocks (MDT_CONV_BM64_BELOW; default 1024 = 4 per CU, measured 3 % faster
+  // than 512 on the 128x128 step and 0.5 % on the 28x28 one, profiles/r1_knobs)
   static const int bm64_below = [] {
     const char* e = getenv("MDT_CONV_BM64_BELOW");
-    return e ? atoi(e) : 512;
+    return e ? atoi(e) : 1024;
   }();
   q.BM = 128;
   if ((long long)q.classes * cdiv(q.M, 128) * q.ntiles < bm64_below) q.BM = 64;
   q.mtiles = cdiv(q.M, q.BM);
   const long long blocks = (long long)q.classes * q.mtiles * q.ntiles;
   q.ksplit = 1;
-  // split-K only for deep problems: at 8-15 k-tiles the extra combine launch
-  // costs more than the under-filled grid (conv28 enc2: 98 blocks x 8 k-tiles)
+  // split-K only for deep problems (>= 8 k-tiles, MDT_CONV_SPLIT_MIN_KT) whose
+  // grid is under-filled; the combine is fused into a following launch where
+  // the model allows it (enc_head -> reparam, dec_fc dgrad -> reparam backward)
   static const int min_kt = [] {
     const char* e = getenv("MDT_CONV_SPLIT_MIN_KT");
-    return e ? atoi(e) : 16;
+    return e ? atoi(e) : 8;
   }();
-  // at least `kt_per` k-tiles per split (MDT_CONV_SPLIT_KT_PER): fewer k-steps
-  // per block against more partial slabs for the combine pass to read
+  // at least `kt_per` k-tiles per split (MDT_CONV_SPLIT_KT_PER, default 1):
+  // fewer k-steps per block against more partial slabs for the combine pass
+  // to read; 1 measured 3 % faster than 4 on the 28x28 step (profiles/r1_knobs)
   static const int kt_per = [] {
     const char* e = getenv("MDT_CONV_SPLIT_KT_PER");
-    const int v = e ? atoi(e) : 4;
+    const int v = e ? atoi(e) : 1;
     return v < 1 ? 1 : v;
   }();
   if (allow_split && q.classes == 1 && blocks < 256 && q.ktiles >= min_kt) {
@@ -117,12 +122,21 @@ bool plan_wgrad(const ConvDesc& d, WgradPlan* p) {
   q.ktiles = cdiv(q.K2, q.BN);
   q.mtiles = cdiv(q.M, 64);
   const int tiles = q.cotiles * q.ktiles;
-  // m-splits so the grid reaches ~`target` blocks (MDT_CONV_WG_TARGET, default 320)
-  static const int target = [] {
+  // m-splits so the grid reaches ~`target` blocks. Default: ~16 m-steps per
+  // block, clamped to [160, 640] blocks -- measured on MI355X (profiles/r1_knobs):
+  // the 28x28 layers (98 m-tiles) want few splits (fewer partial slabs for the
+  // finalize to read), the 128x128 layers (up to 4096 m-tiles) want the grid
+  // wide (a 320-block grid left ~200 serial m-steps per block).
+  // MDT_CONV_WG_TARGET pins the target instead.
+  static const int fixed_target = [] {
     const char* e = getenv("MDT_CONV_WG_TARGET");
-    const int v = e ? atoi(e) : 320;
-    return v < 1 ? 1 : v;
+    return e ? atoi(e) : 0;
   }();
+  int target = fixed_target;
+  if (target <= 0) {
+    const long long work = (long long)q.mtiles * tiles;
+    target = (int)std::min<long long>(640, std::max<long long>(160, work / 16));
+  }
   int ns = cdiv(target, tiles);
   if (ns > q.mtiles / 2) ns = q.mtiles / 2;
   if (ns < 1) ns = 1;
