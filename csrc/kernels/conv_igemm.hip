@@ -65,6 +65,22 @@ bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p) {
   if (q.K % 8 || q.M <= 0) return false;
   q.BN = q.Ncols >= 128 ? 128 : q.Ncols > 32 ? 64 : q.Ncols > 16 ? 32 : 16;
   if (q.thin) q.BN = 32;
+  // narrower column tiles for deep (>= MDT_CONV_BN_SPLIT_MIN_KT = 16 k-tiles)
+  // problems whose grid would stay under MDT_CONV_BN_SPLIT_BELOW = 512 blocks:
+  // more workgroups in flight for the wide-N, short-M 128x128 layers (4 % on
+  // that step); shallow ones (the 28x28 decoder Linear, K = 32) lose from the
+  // extra A re-reads, so they keep their tiles (profiles/r1_knobs)
+  static const int bn_split_below = [] {
+    const char* e = getenv("MDT_CONV_BN_SPLIT_BELOW");
+    return e ? atoi(e) : 512;
+  }();
+  static const int bn_split_min_kt = [] {
+    const char* e = getenv("MDT_CONV_BN_SPLIT_MIN_KT");
+    return e ? atoi(e) : 16;
+  }();
+  while (q.BN > 32 && !q.thin && cdiv(q.K, 64) >= bn_split_min_kt &&
+         (long long)q.classes * cdiv(q.M, 64) * cdiv(q.Ncols, q.BN) < bn_split_below)
+    q.BN /= 2;
   q.ntiles = cdiv(q.Ncols, q.BN);
   q.ktiles = cdiv(q.K, 64);
   // 64-row tiles when 128-row tiles would leave the grid under `bm64_below`

@@ -11,10 +11,7 @@ run() {  # name model bs env...
 }
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-run c28_new conv28 128 MDT_X=0 || exit 1
-run c28_old conv28 128 MDT_CONV_SPLIT_KT_PER=4 MDT_CONV_SPLIT_MIN_KT=16 MDT_CONV_BM64_BELOW=512 MDT_CONV_WG_TARGET=320 || exit 1
-run c28_new2 conv28 128 MDT_X=1 || exit 1
-run c128_new conv128 64 MDT_X=0 || exit 1
-run c128_old conv128 64 MDT_CONV_SPLIT_KT_PER=4 MDT_CONV_SPLIT_MIN_KT=16 MDT_CONV_BM64_BELOW=512 MDT_CONV_WG_TARGET=320 || exit 1
-run c128_new2 conv128 64 MDT_X=1 || exit 1
-run c128_w1024 conv128 64 MDT_CONV_WG_TARGET=1024 || exit 1
+run c28_final conv28 128 MDT_X=0 || exit 1
+run c128_final conv128 64 MDT_X=0 || exit 1
+run c28_final2 conv28 128 MDT_X=1 || exit 1
+run c128_final2 conv128 64 MDT_X=1 || exit 1
