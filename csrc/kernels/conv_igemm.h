@@ -66,6 +66,18 @@ struct WgradPlan {
 // Gradient finalisation: per arena segment, g = sum over `nsplit` partial rows
 // of width `numel` (deterministic order), then either stored to the gradient
 // arena or consumed by a fused Adam + bf16 cast (+ parity-ordered transpose).
+// Optional A-operand prologue: the producing layer ran split-K without a
+// combine pass; A(row, k) = act(bias[c] + sum_s slab[s][off]) is formed while
+// staging (c = off % cin) and written once to `out16` (the producer's output,
+// needed later by the backward), saving the combine launch in between.
+struct APro {
+  const float* slab;  // [ks][A elements] partial sums of the producer (null: plain A)
+  const float* bias;
+  void* out16;        // bf16
+  int ks, relu, cin;
+  long long stride;   // elements per slab
+};
+
 struct GradSeg {
   long long off, numel;
   const float* slab;  // nullptr: the gradient arena already holds g

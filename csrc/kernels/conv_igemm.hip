@@ -241,23 +241,23 @@ int launch_splitk_combine(const CombineArgs& c, int nblk, hipStream_t s) {
 namespace {
 using namespace mdt::tiles;
 
-template <int MODE, typename AT, bool VEC, class TC>
+template <int MODE, typename AT, bool VEC, class TC, bool PRO = false>
 void launch_fwd(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
   dim3 grid(q.mtiles * q.ntiles, q.ksplit, q.classes);
-  hipLaunchKernelGGL((igemm_fwd_k<MODE, AT, VEC, TC>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((igemm_fwd_k<MODE, AT, VEC, TC, PRO>), grid, dim3(256), 0, s, a);
 }
 
-template <int MODE, typename AT, bool VEC>
+template <int MODE, typename AT, bool VEC, bool PRO = false>
 int dispatch_fwd_cfg(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
   switch (q.cfg) {
-    case 0: launch_fwd<MODE, AT, VEC, F0>(a, q, s); return 0;
-    case 1: launch_fwd<MODE, AT, VEC, F1>(a, q, s); return 0;
-    case 2: launch_fwd<MODE, AT, VEC, F2>(a, q, s); return 0;
-    case 3: launch_fwd<MODE, AT, VEC, F3>(a, q, s); return 0;
-    case 4: launch_fwd<MODE, AT, VEC, F4>(a, q, s); return 0;
-    case 5: launch_fwd<MODE, AT, VEC, F5>(a, q, s); return 0;
-    case 6: launch_fwd<MODE, AT, VEC, F6>(a, q, s); return 0;
-    case 7: launch_fwd<MODE, AT, VEC, F7>(a, q, s); return 0;
+    case 0: launch_fwd<MODE, AT, VEC, F0, PRO>(a, q, s); return 0;
+    case 1: launch_fwd<MODE, AT, VEC, F1, PRO>(a, q, s); return 0;
+    case 2: launch_fwd<MODE, AT, VEC, F2, PRO>(a, q, s); return 0;
+    case 3: launch_fwd<MODE, AT, VEC, F3, PRO>(a, q, s); return 0;
+    case 4: launch_fwd<MODE, AT, VEC, F4, PRO>(a, q, s); return 0;
+    case 5: launch_fwd<MODE, AT, VEC, F5, PRO>(a, q, s); return 0;
+    case 6: launch_fwd<MODE, AT, VEC, F6, PRO>(a, q, s); return 0;
+    case 7: launch_fwd<MODE, AT, VEC, F7, PRO>(a, q, s); return 0;
   }
   return 2;
 }
@@ -330,14 +330,20 @@ int mdt_wgrad_plan(ConvDesc d, int* info) {
 // for deep, narrow problems (then bias/relu/y16/y32 are applied by a combine
 // pass; omask/colsum are not allowed with split-K).
 int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d, const float* bias, int relu,
-              void* y16, float* y32, const void* omask, float* colsum, float* ws, int skip_combine, hipStream_t s) {
+              void* y16, float* y32, const void* omask, float* colsum, float* ws, int skip_combine, hipStream_t s,
+              const APro* pro) {
   IgArgs a;
   FwdPlan q;
   CombineArgs c;
   int nc = 0;
   if (build_igemm(mode, A, B16, d, bias, relu, y16, y32, omask, colsum, ws, &a, &q, &c, &nc)) return 1;
   int rc;
-  if (mode == kModeConv) {
+  if (pro && pro->slab) {
+    // A from the producer's split-K slabs: conv-mode, bf16 vector gathers only
+    if (mode != kModeConv || q.thin || a_is_f32 || pro->cin % 8 || pro->ks < 1) return 4;
+    a.pro = *pro;
+    rc = dispatch_fwd_cfg<kModeConv, __bf16, true, true>(a, q, s);
+  } else if (mode == kModeConv) {
     if (q.thin) rc = a_is_f32 ? dispatch_thin<float>(a, q, s) : dispatch_thin<__bf16>(a, q, s);
     else if (a_is_f32) rc = 3;
     else if (use_glds()) rc = dispatch_glds<kModeConv>(a, q, s);

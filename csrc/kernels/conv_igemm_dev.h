@@ -93,6 +93,7 @@ struct TileCfg {
 // ================================================================ forward ====
 struct IgArgs {
   ConvDesc d;
+  APro pro;
   const void* A;
   const __bf16* B;  // [classes][Ncols][K]
   __bf16* y16;
@@ -260,7 +261,7 @@ constexpr int igemm_lds_bytes() { return 2 * (TC::BM * 128 + TC::BN * 128); }
 // (k-split, class) plane), k-split `kz`, parity class `cls`. `lds` holds
 // igemm_lds_bytes<TC>() bytes. Shared by the stand-alone kernel and the
 // horizontally fused job kernels (conv_jobs.h).
-template <int MODE, typename AT, bool VEC, class TC>
+template <int MODE, typename AT, bool VEC, class TC, bool PRO = false>
 __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb, int ntb, int kz, int cls) {
   constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
   constexpr int A_CH = BM / 32;                // 16-B chunks per thread of the BM x 64 A tile
@@ -343,7 +344,28 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
           ok = aok[i] && kok && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
           off = abase[i] + (oy * d.OW + ox) * d.CO + ch;
         }
-        ra[i] = load_chunk<AT>(Ap + (ok ? off : 0));
+        if constexpr (PRO) {
+          // split-K combine of the producing layer (fixed slab order: deterministic)
+          const size_t o = ok ? (size_t)off : 0;
+          const int c0 = (int)(o % (size_t)a.pro.cin);
+          f32x4 s0 = *reinterpret_cast<const f32x4*>(a.pro.bias + c0);
+          f32x4 s1 = *reinterpret_cast<const f32x4*>(a.pro.bias + c0 + 4);
+          for (int z = 0; z < a.pro.ks; ++z) {
+            const float* q = a.pro.slab + (size_t)z * a.pro.stride + o;
+            s0 += *reinterpret_cast<const f32x4*>(q);
+            s1 += *reinterpret_cast<const f32x4*>(q + 4);
+          }
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = (__bf16)(a.pro.relu ? fmaxf(s0[j], 0.f) : s0[j]);
+            v[4 + j] = (__bf16)(a.pro.relu ? fmaxf(s1[j], 0.f) : s1[j]);
+          }
+          ra[i] = v;
+          if (ok && nt == 0) *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.pro.out16) + o) = v;
+        } else {
+          ra[i] = load_chunk<AT>(Ap + (ok ? off : 0));
+        }
         okm |= (uint32_t)ok << i;
       }
     } else {
@@ -444,10 +466,10 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
   igemm_epilogue<MODE, TC>(a, acc, lds, mt, nt, kz, cls, oa, ob);
 }
 
-template <int MODE, typename AT, bool VEC, class TC>
+template <int MODE, typename AT, bool VEC, class TC, bool PRO = false>
 __global__ void __launch_bounds__(256) igemm_fwd_k(IgArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[igemm_lds_bytes<TC>()];
-  igemm_body<MODE, AT, VEC, TC>(a, lds, blockIdx.x, gridDim.x, blockIdx.y, blockIdx.z);
+  igemm_body<MODE, AT, VEC, TC, PRO>(a, lds, blockIdx.x, gridDim.x, blockIdx.y, blockIdx.z);
 }
 
 // ---------------------------------------------------------- LDS-DMA helpers ----

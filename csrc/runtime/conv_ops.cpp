@@ -18,7 +18,8 @@ extern "C" {
 int mdt_igemm_plan(int mode, mdt::ConvDesc d, int allow_split, int* info);
 int mdt_wgrad_plan(mdt::ConvDesc d, int* info);
 int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, mdt::ConvDesc d, const float* bias, int relu,
-              void* y16, float* y32, const void* omask, float* colsum, float* ws, int skip_combine, hipStream_t s);
+              void* y16, float* y32, const void* omask, float* colsum, float* ws, int skip_combine, hipStream_t s,
+              const mdt::APro* pro);
 int mdt_wgrad(const void* G16, const void* X, int x_is_f32, mdt::ConvDesc d, float* out, hipStream_t s);
 int mdt_colsum(const void* G16, int M, int N, int rows_per, float* slab, hipStream_t s);
 int mdt_gather_rows(const float* X, const int* idx, const void* st, int B, int M, int P, float* xb, hipStream_t s);
@@ -117,7 +118,9 @@ std::vector<int64_t> wgrad_plan(const std::vector<int64_t>& dv) {
 void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::vector<int64_t>& dv,
            const c10::optional<at::Tensor>& bias, bool relu, const c10::optional<at::Tensor>& y16,
            const c10::optional<at::Tensor>& y32, const c10::optional<at::Tensor>& omask,
-           const c10::optional<at::Tensor>& colsum, const c10::optional<at::Tensor>& ws, Job* job, bool combine) {
+           const c10::optional<at::Tensor>& colsum, const c10::optional<at::Tensor>& ws, Job* job, bool combine,
+           const c10::optional<at::Tensor>& a_slab, int64_t a_ks, const c10::optional<at::Tensor>& a_bias,
+           bool a_relu, const c10::optional<at::Tensor>& a_out16) {
   const ConvDesc d = desc(dv);
   TORCH_CHECK(A.is_cuda() && A.is_contiguous(), "A must be contiguous CUDA");
   const bool f32 = A.scalar_type() == torch::kFloat32;
@@ -136,6 +139,21 @@ void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::
   check_min(bias, Ncols, "bias");
   check_min(colsum, (int64_t)info[11] * Ncols, "colsum");
   if (ksplit > 1) check_min(ws, ksplit * M * Ncols, "ws");
+  APro pro{};
+  if (a_slab.has_value() && a_slab->defined()) {
+    // A is formed from the producing layer's split-K partial slabs (see APro)
+    TORCH_CHECK(!job, "igemm: the A prologue has no job form");
+    TORCH_CHECK(a_bias.has_value() && a_bias->defined() && a_out16.has_value() && a_out16->defined(),
+                "igemm: a_slab needs a_bias and a_out16");
+    check_f32(*a_slab, "a_slab");
+    check_bf16(*a_out16, "a_out16");
+    TORCH_CHECK(a_ks >= 1 && a_slab->numel() >= a_ks * a_need, "a_slab too small");
+    TORCH_CHECK(a_out16->numel() >= a_need, "a_out16 too small");
+    const int64_t cin = a_bias->numel();
+    TORCH_CHECK(cin % 8 == 0 && a_need % cin == 0, "a_bias length must divide the A row layout");
+    pro = APro{(const float*)a_slab->data_ptr(), (const float*)a_bias->data_ptr(),
+               a_out16->data_ptr(), (int)a_ks, a_relu ? 1 : 0, (int)cin, (long long)a_need};
+  }
   if (job) {
     rc(mdt_job_igemm(&job->main, &job->post, (int)mode, A.data_ptr(), f32, B16.data_ptr(), d,
                      (const float*)opt_ptr(bias), relu, const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32),
@@ -145,7 +163,7 @@ void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::
   }
   rc(mdt_igemm((int)mode, A.data_ptr(), f32, B16.data_ptr(), d, (const float*)opt_ptr(bias), relu,
                const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32), opt_ptr(omask), (float*)opt_ptr(colsum),
-               (float*)opt_ptr(ws), combine ? 0 : 1, cur()),
+               (float*)opt_ptr(ws), combine ? 0 : 1, cur(), pro.slab ? &pro : nullptr),
      "igemm");
 }
 
@@ -494,7 +512,8 @@ void bind_conv(pybind11::module& m) {
   m.def("igemm", &igemm, py::arg("mode"), py::arg("A"), py::arg("B16"), py::arg("desc"), py::arg("bias"),
         py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),
         py::arg("colsum") = py::none(), py::arg("ws") = py::none(), py::arg("job") = py::none(),
-        py::arg("combine") = true);
+        py::arg("combine") = true, py::arg("a_slab") = py::none(), py::arg("a_ks") = 0,
+        py::arg("a_bias") = py::none(), py::arg("a_relu") = false, py::arg("a_out16") = py::none());
   m.def("wgrad", &wgrad, py::arg("G16"), py::arg("X"), py::arg("desc"), py::arg("out"), py::arg("job") = py::none());
   m.def("colsum", &colsum, py::arg("G16"), py::arg("M"), py::arg("N"), py::arg("rows_per"), py::arg("slab"),
         py::arg("job") = py::none());

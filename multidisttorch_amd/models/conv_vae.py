@@ -527,6 +527,17 @@ class ConvVaeTrainer:
                 q = C.igemm_plan(0, self._desc(l, M), True)
                 if q[10] > 1:
                     ws_need = max(ws_need, q[10] * q[4] * q[5])
+        # the layer feeding the encoder head, when it runs split-K: its combine
+        # is folded into the head GEMM's A staging (APro, conv_igemm_dev.h)
+        ws_a, ks_a = None, 0
+        enc = [l for l in spec if l.name.startswith("enc")]
+        if len(enc) >= 3 and os.getenv("MDT_CONV_APRO", "1") != "0":
+            src = enc[-2]
+            if not (src is spec[0] and self._thin_first) and src.kind == "conv" and src.cout % 8 == 0:
+                q = C.igemm_plan(0, self._desc(src, M), True)
+                if q[10] > 1:
+                    ks_a = q[10]
+                    ws_a = torch.empty(ks_a * q[4] * q[5], **f32)
         rows_per = 8  # colsum kernel partial rows for the per-feature biases
         ncs = -(-M // rows_per)
         for l in spec:
@@ -557,6 +568,7 @@ class ConvVaeTrainer:
                 units.append([si, st, min(cnt, numel - st)])
         layer_units.append(len(units))  # layer i owns units [layer_units[i], layer_units[i+1])
         p = dict(slabs=slabs, colsum=colsum, gpart=gpart, ws=torch.empty(max(ws_need, 1), **f32), rows_per=rows_per,
+                 ws_a=ws_a, ks_a=ks_a,
                  segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
                  nunits=len(units), layer_units=layer_units)
         self._plans[M] = p
@@ -596,7 +608,7 @@ class ConvVaeTrainer:
             return [M, l.out_hw, l.out_hw, l.cout, l.in_hw, l.in_hw, l.cin, l.k, l.k, l.s, l.p]
         return [M, l.in_hw, l.in_hw, l.cin, l.out_hw, l.out_hw, l.cout, l.k, l.k, l.s, l.p]
 
-    def _layer_fwd(self, l, h, M, o16, o32, ws):
+    def _layer_fwd(self, l, h, M, o16, o32, ws, **pro):
         """conv / linear: conv-mode GEMM; convT: parity-class GEMM on the
         transposed weights (no zero-insertion taps); single-channel edge
         layers: direct kernels."""
@@ -608,7 +620,7 @@ class ConvVaeTrainer:
         elif l.kind == "convT":
             self.C.igemm(1, h, self._wt(l), d, self._b(l), l.relu, o16, o32)
         else:
-            self.C.igemm(0, h, self._w(l), d, self._b(l), l.relu, o16, o32, ws=ws)
+            self.C.igemm(0, h, self._w(l), d, self._b(l), l.relu, o16, o32, ws=ws, **pro)
 
     def _forward_hip(self, M, state, stream, want_recon=False, train=True, src=None):
         """Forward of one batch. ``src = (X, idx)``: the batch is gathered from
@@ -631,17 +643,27 @@ class ConvVaeTrainer:
             else:
                 C.step_begin(state, hp)
                 C.gather_rows(X, idx, state, self.B, M, self.xb)
+        pro = {}
         for l in enc[first:]:
             last = l is enc[-1]
+            if not last and p["ws_a"] is not None and l is enc[-2]:
+                # split-K partials only; the head's A staging combines them (+bias, ReLU)
+                # and writes this layer's activations for the backward
+                C.igemm(0, h, self._w(l), self._desc(l, M), None, False, None, None, ws=p["ws_a"], combine=False)
+                pro = dict(a_slab=p["ws_a"], a_ks=p["ks_a"], a_bias=self._b(l), a_relu=l.relu,
+                           a_out16=self.acts[l.name])
+                h = self.acts[l.name]
+                continue
             if last:
                 q = C.igemm_plan(0, self._desc(l, M), True)
                 if q[10] > 1:  # split-K head: combine fused with the reparameterisation
                     C.igemm(0, h, self._w(l), self._desc(l, M), self._b(l), False, None, self.mulv, ws=p["ws"],
-                            combine=False)
+                            combine=False, **pro)
                     C.combine_reparam(p["ws"], q[10], self._b(l), self.mulv, self.eps, self.z16, None, M, self.Z,
                                       state, hp, stream, self.kld_part)
                     break
-            self._layer_fwd(l, h, M, None if last else self.acts[l.name], self.mulv if last else None, p["ws"])
+            self._layer_fwd(l, h, M, None if last else self.acts[l.name], self.mulv if last else None, p["ws"],
+                            **(pro if last else {}))
             h = self.acts[l.name]
         else:
             C.reparam(self.mulv, self.eps, self.z16, None, M, self.Z, state, hp, stream, self.kld_part)

@@ -176,3 +176,31 @@ def test_fused_job_launches_are_bitwise_unfused(image, batch, native_ext):
         bad = [n for n in wt if not torch.equal(wt[n], out[0][2][n])]
         assert not bad, bad
         assert st["cursor"] == out[0][3]["cursor"] and st["step"] == out[0][3]["step"]
+
+
+def test_encoder_head_prologue_matches_combine_launch(native_ext, monkeypatch):
+    """28x28: enc2 runs split-K and its combine (+bias, ReLU) is folded into the
+    encoder head's A staging (APro). Same training as with the separate combine
+    launch (MDT_CONV_APRO=0), up to summation order; enc2's activations written
+    by the head kernel equal the combined ones."""
+    from multidisttorch_amd.data.datasets import synthetic_images
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    dev = torch.device("cuda")
+    X = synthetic_images(1024, device=dev)
+    idx = torch.arange(1024, device=dev, dtype=torch.int32)
+    res, acts = [], []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MDT_CONV_APRO", flag)
+        tr = ConvVaeTrainer(batch_size=128, image=28, device=dev, backend="hip", seed=11, use_graphs=False)
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 8)
+        p = tr._plan(128)
+        assert (p["ws_a"] is not None) == (flag == "1")
+        tr.train_steps(6)
+        torch.cuda.synchronize()
+        res.append(tr.loss_history()[:6].copy())
+        acts.append(tr.acts["enc2"].float().clone())
+    np.testing.assert_allclose(res[0], res[1], rtol=2e-3)
+    d = (acts[0] - acts[1]).abs().max().item()
+    assert d <= 0.02 * acts[0].abs().max().item(), d
