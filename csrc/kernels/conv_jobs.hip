@@ -146,6 +146,7 @@ using Wg1 = JWg<1, W1>;
 using IgC1 = JIg<kModeConv, 1, F1>;
 using IgC4 = JIg<kModeConv, 4, F4>;
 using IgC5 = JIg<kModeConv, 5, F5>;
+using IgC6 = JIg<kModeConv, 6, F6>;
 using IgT1 = JIg<kModeTconv, 1, F1>;
 using IgT2 = JIg<kModeTconv, 2, F2>;
 using IgT4 = JIg<kModeTconv, 4, F4>;
@@ -161,9 +162,12 @@ const Combo kCombos[] = {
     COMBO2(IgC5, Wg0),
     COMBO2(IgC1, Wg0),
     COMBO2(IgC4, Wg0),
+    COMBO2(IgC6, Wg0),  // 128x128: narrow column tiles of deep layers (BN split)
+    COMBO3(IgC6, Wg0, JColsum),
     // decoder Linear (split-K backward-data) || weight gradient || its bias column sums
     COMBO3(IgT6, Wg1, JColsum),
     COMBO3(IgT5, Wg0, JColsum),
+    COMBO3(IgT6, Wg0, JColsum),
     // encoder head || weight gradient || head bias column sums
     COMBO3(IgT4, Wg0, JColsum),
     // conv layers: parity-mode backward-data || weight gradient

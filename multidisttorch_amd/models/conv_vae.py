@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import math
 import os
+import sys
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -691,6 +692,9 @@ class ConvVaeTrainer:
             if all(j.kind > 0 for j in jobs) and self.C.launch_jobs(jobs):
                 self._fused_launches += 1
                 return
+            if os.getenv("MDT_JOBS_DEBUG"):
+                print(f"[jobs] not fused: kinds={sorted(j.kind for j in jobs)} post={[j.has_post for j in jobs]}",
+                      file=sys.stderr, flush=True)
         for f in fns:
             f(None)
 
