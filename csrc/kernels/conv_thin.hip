@@ -14,6 +14,8 @@
 //                   stride-parity class per blockIdx.y so the taps, hence the
 //                   weights, are uniform; fused logit-form BCE (-100 clamp),
 //                   dlogits, reconstruction and loss / bias-gradient partials.
+#include <stdlib.h>
+
 #include "conv_thin.h"
 
 namespace mdt {
@@ -22,6 +24,12 @@ template <int CO, int K, typename TIN>
 __global__ void __launch_bounds__(256) thin_conv_k(ThinConvArgs ta) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[thin_conv_lds_bytes<CO, K>()];
   thin_conv_body<CO, K, TIN>(ta, lds, blockIdx.x);
+}
+
+template <int CO>
+__global__ void __launch_bounds__(256) thin_tconv4_k(ThinTconvArgs ta) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[thin_tconv4_lds_bytes<CO>()];
+  thin_tconv4_body<CO>(ta, lds, blockIdx.x);
 }
 
 template <int CO, int K, int S>
@@ -69,8 +77,17 @@ int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, cons
 
 // blocks of the per-block partial outputs (colsum rows for thin_conv,
 // loss partials for thin_tconv)
+static bool tconv4_ok(const ConvDesc& d) {
+  static const bool on = [] {
+    const char* e = getenv("MDT_THIN_TCONV4");
+    return !(e && e[0] == '0');
+  }();
+  return on && d.KH == 4 && d.KW == 4 && d.S == 2 && d.P == 1;
+}
+
 int mdt_thin_blocks(int tconv, ConvDesc d) {
   if (!tconv) return cdiv_t((long long)d.N * d.OH * d.OW, 256);
+  if (tconv4_ok(d)) return cdiv_t((long long)d.N * (d.H / 2) * (d.W / 2), 256);
   return cdiv_t((long long)d.N * (d.H / d.S) * (d.W / d.S), 256) * d.S * d.S;
 }
 
@@ -80,6 +97,17 @@ int mdt_thin_tconv(const void* G16, const float* Wf, ConvDesc d, const float* bi
   if (X && !part) return 1;
   const long long Mc = (long long)d.N * (d.H / d.S) * (d.W / d.S);
   const int gx = cdiv_t(Mc, 256);
+  if (tconv4_ok(d)) {  // one thread per input position: all four parity classes
+    const ThinTconvArgs t4{reinterpret_cast<const __bf16*>(G16), Wf, d, bias, y32, X,
+                           reinterpret_cast<__bf16*>(dlog16), recon, part, gpart, gx};
+    switch (d.CO) {
+      case 16: hipLaunchKernelGGL((thin_tconv4_k<16>), dim3(gx), dim3(256), 0, s, t4); break;
+      case 32: hipLaunchKernelGGL((thin_tconv4_k<32>), dim3(gx), dim3(256), 0, s, t4); break;
+      case 64: hipLaunchKernelGGL((thin_tconv4_k<64>), dim3(gx), dim3(256), 0, s, t4); break;
+      default: return 2;
+    }
+    return (int)hipGetLastError();
+  }
   dim3 grid(gx * d.S * d.S), blk(256);
   const ThinTconvArgs ta{reinterpret_cast<const __bf16*>(G16), Wf, d, bias, y32, X, reinterpret_cast<__bf16*>(dlog16),
                          recon, part, gpart, gx};
