@@ -77,10 +77,14 @@ int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, cons
 
 // blocks of the per-block partial outputs (colsum rows for thin_conv,
 // loss partials for thin_tconv)
+// Opt-in (MDT_THIN_TCONV4=1): measured SLOWER on MI355X than the per-class
+// kernel (conv28 step +1.7 us, conv128 +10 us): a quarter of the threads, each
+// with a 4x longer dependent FMA chain, hides less load latency than the 4x
+// re-read costs (profiles/r1_knobs/ab7_thin_tconv4.txt).
 static bool tconv4_ok(const ConvDesc& d) {
   static const bool on = [] {
     const char* e = getenv("MDT_THIN_TCONV4");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on && d.KH == 4 && d.KW == 4 && d.S == 2 && d.P == 1;
 }

@@ -11,9 +11,9 @@ run() {  # name model bs env...
 }
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-run c28_t4 conv28 128 MDT_X=0 || exit 1
-run c28_t1 conv28 128 MDT_THIN_TCONV4=0 || exit 1
-run c28_t4b conv28 128 MDT_X=1 || exit 1
-run c128_t4 conv128 64 MDT_X=0 || exit 1
-run c128_t1 conv128 64 MDT_THIN_TCONV4=0 || exit 1
-run c128_t4b conv128 64 MDT_X=1 || exit 1
+run c28_t4 conv28 128 MDT_THIN_TCONV4=1 || exit 1
+run c28_t1 conv28 128 MDT_X=0 || exit 1
+run c28_t4b conv28 128 MDT_THIN_TCONV4=1 || exit 1
+run c128_t4 conv128 64 MDT_THIN_TCONV4=1 || exit 1
+run c128_t1 conv128 64 MDT_X=0 || exit 1
+run c128_t4b conv128 64 MDT_THIN_TCONV4=1 || exit 1
