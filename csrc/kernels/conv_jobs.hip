@@ -117,6 +117,57 @@ __global__ void __launch_bounds__(256) jobs_k(JobPack p) {
   else C::run(p.j[2], lds, b - p.start2);
 }
 
+// The optimizer tail as ONE launch. Blocks [0, start1) compute the first
+// layer's weight-gradient partial slabs (job 0) and then arrive on a device
+// ticket (release). Blocks [start1, start2) finalize + Adam the other layers
+// that are still pending (job 2). Blocks [start2, grid) -- the highest block
+// ids, so the dispatcher places every weight-gradient block before them --
+// each own one of the first layer's finalize units (job 1): one thread waits
+// (acquire, s_sleep back-off, bounded: ticket[2] = 1 flags a timeout instead of
+// hanging) until all weight-gradient blocks have arrived, then the block runs
+// the same finalize body as the stand-alone launch (bitwise identical). The
+// grid (a few hundred blocks) is far below the chip's resident capacity, so
+// the waiting blocks never keep an arriving block from running. The last
+// waiter resets the ticket for the next launch (graph replays included).
+// This replaces "wgrad0 || finalize(1..L)" followed by a separate
+// "finalize(0) || transposes" launch; the transposed weight copies move to
+// the next step's first launch (models/conv_vae.py, `_tail1_active`).
+// ticket: int32 [3] = {arrived, waiters passed, timeout flag}.
+template <class W>
+__global__ void __launch_bounds__(256) tail_k(JobPack p, int* ticket) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[cmax(W::LDS, JFinalize::LDS)];
+  const int b = blockIdx.x;
+  if (b < p.start1) {
+    W::run(p.j[0], lds, b);
+    __threadfence();  // every wave releases its slab stores (agent scope: other XCDs' L2s)
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (b < p.start2) {
+    JFinalize::run(p.j[2], lds, b - p.start1);
+    return;
+  }
+  if (threadIdx.x == 0) {
+    int it = 0;
+    while (__hip_atomic_load(ticket, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < p.start1) {
+      if (++it > (1 << 20)) {  // ~50 ms: never reached unless the ticket protocol is broken
+        __hip_atomic_store(ticket + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    const int waiters = (int)gridDim.x - p.start2;
+    if (__hip_atomic_fetch_add(ticket + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == waiters - 1) {
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ticket + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  __threadfence();  // acquire for every wave: all weight-gradient slabs are visible
+  JFinalize::run(p.j[1], lds, b - p.start2);
+}
+
 }  // namespace mdt
 
 using namespace mdt;
@@ -141,6 +192,7 @@ struct Combo {
 using WgT5 = JWgThin<__bf16, 5, W5>;
 using WgT5f = JWgThin<float, 5, W5>;
 using ThinC32 = JThinConv<32, __bf16>;
+using ThinC32f = JThinConv<32, float>;
 using Wg0 = JWg<0, W0>;
 using Wg1 = JWg<1, W1>;
 using IgC1 = JIg<kModeConv, 1, F1>;
@@ -176,10 +228,22 @@ const Combo kCombos[] = {
     COMBO2(IgT1, Wg0),
     COMBO2(IgT2, Wg0),
     COMBO2(IgT5, Wg0),
+    // backward-data || weight gradient || finalize+Adam of the layers whose
+    // gradients the previous launches completed (spread optimizer, tail1 mode)
+    COMBO3(IgC1, Wg0, JFinalize),
+    COMBO3(IgC4, Wg0, JFinalize),
+    COMBO3(IgC5, Wg0, JFinalize),
+    COMBO3(IgT1, Wg0, JFinalize),
+    COMBO3(IgT2, Wg0, JFinalize),
+    COMBO3(IgT4, Wg0, JFinalize),
+    COMBO3(IgT6, Wg0, JFinalize),
     // optimizer tail: first-layer weight gradient || finalize+Adam of every
     // other layer; then first-layer finalize || transposed weight copies
     COMBO2(WgT5f, JFinalize),
     COMBO2(JFinalize, JWtrans),
+    // step's first launch (batch gather + step begin + first layer) || the
+    // transposed weight copies the previous step's one-launch tail left out
+    COMBO2(ThinC32f, JWtrans),
 };
 
 #undef COMBO3
@@ -238,14 +302,17 @@ int mdt_job_wgrad(JobBlob* j, const void* G16, const void* X, int x_is_f32, Conv
 }
 
 int mdt_job_thin_conv(JobBlob* j, const void* X, int x_is_f32, const float* Wf, ConvDesc d, const float* bias,
-                      int relu, void* y16, const void* omask, float* colsum) {
+                      int relu, void* y16, const void* omask, float* colsum, const int* idx, void* st,
+                      const void* hp, int B, float* xb) {
   if (d.C != 1 || d.KH != 4 || d.KW != 4) return 1;
+  if ((idx || xb || hp) && (!st || !x_is_f32 || (d.H * d.W) % 4)) return 1;
   memset(j, 0, sizeof(*j));
   const bool ok = d.CO == 16 || d.CO == 32 || d.CO == 64;
   j->kind = ok ? kJobThinConv + d.CO + (x_is_f32 ? 100 : 0) : 0;
   j->nblk = cdivj((long long)d.N * d.OH * d.OW, 256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
-                        colsum, nullptr, nullptr, nullptr, 0, nullptr, j->nblk};
+                        colsum, idx, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), B, xb,
+                        j->nblk};
   put_args(j, ta);
   return 0;
 }
@@ -316,6 +383,28 @@ int mdt_launch_jobs(const JobBlob* jobs, int n, hipStream_t s) {
     return (int)hipGetLastError() ? -1 : 0;
   }
   return 1;
+}
+
+// One-launch optimizer tail (tail_k): `wg` = the first layer's weight
+// gradient, `fin0` = its finalize units (run by the last wgrad block),
+// `finr` = finalize of the other layers not finalized yet (may be empty:
+// nblk 0, when the backward sweep finalized them in its own launches). Returns 1 (nothing launched) when
+// the kinds have no instantiation.
+int mdt_launch_tail(const JobBlob* wg, const JobBlob* fin0, const JobBlob* finr, int* ticket, hipStream_t s) {
+  if (!ticket || wg->nblk <= 0 || fin0->nblk <= 0 || finr->nblk < 0) return 2;
+  if (fin0->kind != kJobFinalize || (finr->nblk > 0 && finr->kind != kJobFinalize)) return 1;
+  JobPack p;
+  memset(&p, 0, sizeof(p));
+  p.j[0] = *wg;
+  p.j[1] = *fin0;
+  p.j[2] = *finr;
+  p.start1 = wg->nblk;
+  p.start2 = wg->nblk + finr->nblk;
+  const int grid = p.start2 + fin0->nblk;
+  if (wg->kind == WgT5f::ID) hipLaunchKernelGGL((tail_k<WgT5f>), dim3(grid), dim3(256), 0, s, p, ticket);
+  else if (wg->kind == WgT5::ID) hipLaunchKernelGGL((tail_k<WgT5>), dim3(grid), dim3(256), 0, s, p, ticket);
+  else return 1;
+  return (int)hipGetLastError() ? -1 : 0;
 }
 
 // Launch one job with its stand-alone kernel form (combine / colsum / loss).

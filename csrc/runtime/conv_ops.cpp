@@ -56,12 +56,15 @@ int mdt_combine_reparam_bwd(const float* slab, int ks, const float* mulv, const 
                             void* dmulv16, float* dz, int B, int Z, const void* hp, hipStream_t s);
 int mdt_job_wgrad(mdt::JobBlob* j, const void* G16, const void* X, int x_is_f32, mdt::ConvDesc d, float* out);
 int mdt_job_thin_conv(mdt::JobBlob* j, const void* X, int x_is_f32, const float* Wf, mdt::ConvDesc d,
-                      const float* bias, int relu, void* y16, const void* omask, float* colsum);
+                      const float* bias, int relu, void* y16, const void* omask, float* colsum, const int* idx,
+                      void* st, const void* hp, int B, float* xb);
 int mdt_job_colsum(mdt::JobBlob* j, const void* G16, int M, int N, int rows_per, float* slab);
 int mdt_job_loss(mdt::JobBlob* j, const float* bce_part, int nb, const float* kld_part, int nk, void* st,
                  const void* hp, int advance_cursor);
 int mdt_launch_jobs(const mdt::JobBlob* jobs, int n, hipStream_t s);
 int mdt_launch_job1(const mdt::JobBlob* j, hipStream_t s);
+int mdt_launch_tail(const mdt::JobBlob* wg, const mdt::JobBlob* fin0, const mdt::JobBlob* finr, int* ticket,
+                    hipStream_t s);
 }
 
 namespace mdt {
@@ -205,19 +208,19 @@ void thin_conv(const at::Tensor& X, const at::Tensor& Wf, const std::vector<int6
   check_min(omask, M * d.CO, "omask");
   check_min(colsum, (int64_t)mdt_thin_blocks(0, d) * d.CO, "colsum");
   check_min(bias, d.CO, "bias");
-  if (job) {
-    rc(mdt_job_thin_conv(&job->main, X.data_ptr(), f32, Wf.data_ptr<float>(), d, (const float*)opt_ptr(bias), relu,
-                         y16.data_ptr(), opt_ptr(omask), (float*)opt_ptr(colsum)),
-       "job_thin_conv");
-    return;
-  }
   const bool gather = idx.has_value() && idx->defined();
   if (gather) {
-    TORCH_CHECK(job == nullptr, "thin_conv: the gathering form has no job variant");
     TORCH_CHECK(idx->scalar_type() == torch::kInt32 && state.has_value() && B >= d.N, "thin_conv gather arguments");
     TORCH_CHECK(X.dim() == 2 && X.size(1) == (int64_t)d.H * d.W, "thin_conv gather: X must be [rows, H*W]");
   }
   check_min(xb, (int64_t)d.N * d.H * d.W, "xb");
+  if (job) {
+    rc(mdt_job_thin_conv(&job->main, X.data_ptr(), f32, Wf.data_ptr<float>(), d, (const float*)opt_ptr(bias), relu,
+                         y16.data_ptr(), opt_ptr(omask), (float*)opt_ptr(colsum), (const int*)opt_ptr(idx),
+                         const_cast<void*>(opt_ptr(state)), opt_ptr(hparams), (int)B, (float*)opt_ptr(xb)),
+       "job_thin_conv");
+    return;
+  }
   rc(mdt_thin_conv(X.data_ptr(), f32, Wf.data_ptr<float>(), d, (const float*)opt_ptr(bias), relu, y16.data_ptr(),
                    opt_ptr(omask), (float*)opt_ptr(colsum), (const int*)opt_ptr(idx), const_cast<void*>(opt_ptr(state)),
                    opt_ptr(hparams), (int)B, (float*)opt_ptr(xb), cur()),
@@ -309,6 +312,18 @@ void loss_finalize2(const at::Tensor& bce_part, int64_t nb, const at::Tensor& kl
 // Launch recorded jobs as ONE fused kernel when an instantiation exists for
 // their kinds (returns true), else launch nothing and return false (the caller
 // then issues the ops' own kernels). Follow-up combines run right after.
+// One-launch optimizer tail (conv_jobs.hip::tail_k). `ticket`: int32 [3],
+// zero before the first launch (each launch leaves [0] and [1] at zero; [2]
+// is a sticky timeout flag).
+bool launch_tail(Job* wg, Job* fin0, Job* finr, at::Tensor ticket) {
+  TORCH_CHECK(ticket.is_cuda() && ticket.scalar_type() == torch::kInt32 && ticket.numel() >= 3, "ticket");
+  TORCH_CHECK(!wg->has_post() && !fin0->has_post() && !finr->has_post(), "launch_tail: jobs with a post pass");
+  TORCH_CHECK(finr->main.kind != 0 || finr->main.nblk == 0, "launch_tail: finr");
+  const int r = mdt_launch_tail(&wg->main, &fin0->main, &finr->main, ticket.data_ptr<int>(), cur());
+  TORCH_CHECK(r >= 0 && r != 2, "mdt: launch_tail failed (", r, ")");
+  return r == 0;
+}
+
 bool launch_jobs(const std::vector<Job*>& jobs) {
   TORCH_CHECK(jobs.size() >= 2 && jobs.size() <= 3, "launch_jobs takes 2 or 3 jobs");
   JobBlob v[3];
@@ -509,6 +524,7 @@ void bind_conv(pybind11::module& m) {
       .def_property_readonly("kind", &Job::kind)
       .def_property_readonly("has_post", &Job::has_post);
   m.def("launch_jobs", &launch_jobs);
+  m.def("launch_tail", &launch_tail);
   m.def("igemm", &igemm, py::arg("mode"), py::arg("A"), py::arg("B16"), py::arg("desc"), py::arg("bias"),
         py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),
         py::arg("colsum") = py::none(), py::arg("ws") = py::none(), py::arg("job") = py::none(),

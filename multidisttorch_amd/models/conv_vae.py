@@ -232,6 +232,19 @@ class ConvVaeTrainer:
         # horizontal fusion of independent backward launches (conv_jobs.hip);
         # MDT_CONV_JOBS=0 issues every op as its own kernel (A/B, bitwise equal)
         self.fuse_jobs = os.getenv("MDT_CONV_JOBS", "1") != "0"
+        # finalize+Adam of each layer spread over the backward launches (third
+        # job of the launch after its gradients completed) instead of all in
+        # the optimizer tail. Opt-in (MDT_CONV_SPREAD_FIN=1, bitwise equal):
+        # measured neutral at 28x28 (the tail shrinks, the hosting launches
+        # grow by as much) and 0.7 % slower at 128x128 (profiles/r1_tail)
+        self.spread_fin = os.getenv("MDT_CONV_SPREAD_FIN", "0") == "1"
+        # one-launch optimizer tail (conv_jobs.hip::tail_k, device ticket) with
+        # the transposed weight copies moved into the next step's first launch.
+        # Opt-in (MDT_CONV_TAIL1=1): measured slower on MI355X -- the per-wave
+        # agent-scope release fences (L2 write-back, buffer_wbl2) of ~200
+        # weight-gradient blocks cost more than the launch they save
+        # (profiles/r1_tail/README.md)
+        self.tail1 = os.getenv("MDT_CONV_TAIL1", "0") == "1"
         self._fused_launches = 0
         self._data = None
         torch.manual_seed(self.seed if init_seed is None else init_seed)
@@ -252,6 +265,7 @@ class ConvVaeTrainer:
         else:
             self.C = native.require()
             self.state = self.C.TrialState(self.device.index or 0)
+            self._ticket = torch.zeros(3, dtype=torch.int32, device=self.device)  # tail_k: arrived, passed, timeout
             self._alloc_hip()
         self._push_hparams()
 
@@ -634,16 +648,26 @@ class ConvVaeTrainer:
         dec = [l for l in self.spec if l.name.startswith("dec")]
         h = self.xb
         first = 0
+        wt = self._tail1_active()  # w16t of the previous step's update still to be written
         if src is not None:
             X, idx = src
             l = enc[0]
             if self.fuse_jobs and self._thin_first and len(enc) > 1:
-                C.thin_conv(X, self._wf32(l), self._desc(l, M), self._b(l), l.relu, self.acts[l.name], idx=idx,
-                            state=state, hparams=hp, B=self.B, xb=self.xb)
+                first_conv = (lambda job, l=l: C.thin_conv(X, self._wf32(l), self._desc(l, M), self._b(l), l.relu,
+                                                           self.acts[l.name], job=job, idx=idx, state=state,
+                                                           hparams=hp, B=self.B, xb=self.xb))
+                if wt:
+                    # the transposed copies share the step's first launch (nothing in it reads them)
+                    self._run_group([first_conv, lambda job: self._wtrans_layers(1, len(self.spec), job)])
+                    wt = False
+                else:
+                    first_conv(None)
                 h, first = self.acts[l.name], 1
             else:
                 C.step_begin(state, hp)
                 C.gather_rows(X, idx, state, self.B, M, self.xb)
+        if wt:
+            self._wtrans_layers(1, len(self.spec))
         pro = {}
         for l in enc[first:]:
             last = l is enc[-1]
@@ -718,6 +742,11 @@ class ConvVaeTrainer:
             starts = {b: i for i, (l, b, e) in enumerate(self.layer_ranges())}
             assert all(b in starts or b == self.numel for b in bounds), "bucket bounds must fall on layer starts"
         carry = []  # launches that depend on the previous group's outputs
+        # spread mode: layers [fin_hi, L) already finalized (+Adam) as the third
+        # job of a backward launch -- layer j's gradients are complete once the
+        # launch of layer j ran, and nothing later in the step reads its weights
+        spread = (optimizer and self.spread_fin and self.fuse_jobs and self.reducer is None and not self.overlap)
+        fin_hi = len(spec)
         if with_loss:
             carry.append(lambda job: C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part,
                                                       self._n_kld(M), st.train_state, st.hparams, True,
@@ -778,12 +807,25 @@ class ConvVaeTrainer:
                                      C.colsum(gin, M, n, p["rows_per"], cso, job=job))
             if prev is None and optimizer:
                 L = len(spec)
-                fns.append(lambda job: self._finalize_layers(M, 1, L, job))
+                if self._tail1_active() and len(fns) == 1:
+                    jobs = [C.Job() for _ in range(3)]
+                    fns[0](jobs[0])
+                    self._finalize_layers(M, 0, 1, jobs[1])
+                    if fin_hi > 1:
+                        self._finalize_layers(M, 1, fin_hi, jobs[2])
+                    if jobs[0].kind > 0 and C.launch_tail(jobs[0], jobs[1], jobs[2], self._ticket):
+                        self._fused_launches += 1
+                        break
+                if fin_hi > 1:
+                    fns.append(lambda job, hi=fin_hi: self._finalize_layers(M, 1, hi, job))
                 self._run_group(fns)
                 self._run_group([lambda job: self._finalize_layers(M, 0, 1, job),
                                  lambda job: self._wtrans_layers(1, L, job)])
                 break
-            self._run_group(fns)
+            if spread and len(fns) == 2 and i + 1 < fin_hi and self._run_with_finalize(fns, M, i + 1, fin_hi):
+                fin_hi = i + 1
+            else:
+                self._run_group(fns)
             for f in after:
                 f()
             if prev is None:
@@ -792,6 +834,30 @@ class ConvVaeTrainer:
                     self._maybe_launch_bucket(red, bounds, starts, 0, M)
                 break
             g = gin
+
+    def _run_with_finalize(self, fns, M, lo, hi):
+        """Launch the two jobs ``fns`` plus finalize+Adam of layers [lo, hi) as
+        ONE kernel; False (nothing launched) when that combination has no
+        instantiation."""
+        if not self.fuse_jobs:
+            return False
+        jobs = [self.C.Job() for _ in range(3)]
+        for f, j in zip(fns, jobs):
+            f(j)
+        self._finalize_layers(M, lo, hi, jobs[2])
+        if all(j.kind > 0 for j in jobs) and self.C.launch_jobs(jobs):
+            self._fused_launches += 1
+            return True
+        if os.getenv("MDT_JOBS_DEBUG"):
+            print(f"[jobs] no finalize fusion: kinds={sorted(j.kind for j in jobs)}", file=sys.stderr, flush=True)
+        return False
+
+    def _tail1_active(self):
+        """One-launch optimizer tail in use: the backward ends with tail_k and
+        leaves the transposed weight copies (w16t) to the next forward, which
+        writes them before any launch reads them (``_forward_hip``)."""
+        return (self.tail1 and self.fuse_jobs and self._thin_first and self.reducer is None
+                and not self.overlap and len(self.spec) > 1)
 
     def _finalize_layers(self, M, lo, hi, job=None):
         """Finalize + Adam + bf16 cast of layers [lo, hi) (their units of the plan)."""
@@ -976,13 +1042,17 @@ class ConvVaeTrainer:
         if not self.use_graphs:
             for _ in range(n):
                 self._step_hip(M)
-            return
-        S = self.graph_steps
-        while n >= S:
-            self._replay(S, M)
-            n -= S
-        for _ in range(n):
-            self._replay(1, M)
+        else:
+            S = self.graph_steps
+            while n >= S:
+                self._replay(S, M)
+                n -= S
+            for _ in range(n):
+                self._replay(1, M)
+        if self._tail1_active():
+            # the last step's transposed weight copies (deferred to the next
+            # step's first launch): written here so w16t is current between calls
+            self._wtrans_layers(1, len(self.spec))
 
     def prepare(self, batch_sizes, eval_rows=None):
         """Set-up work done once before timing starts: capture the step graphs
