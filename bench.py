@@ -44,6 +44,27 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 REF_SAMPLES_PER_S_PER_TRIAL = {"mlp": 93465.0, "conv28": 42924.0, "conv128": 18788.0}
 
 
+def _timing_barrier(world, dev):
+    """Barrier that brackets the timed steps. With one GPU per local rank on an
+    RCCL world it is a one-element all-reduce over xGMI (tens of microseconds),
+    so the bracket does not add the ~1 ms of a gloo TCP barrier across 8 ranks
+    (measured on loopback) to a 25 ms timed window; otherwise (CPU, or ranks
+    sharing a GPU, which RCCL rejects) the gloo control-plane barrier."""
+    from multidisttorch_amd.runtime import global_barrier
+
+    if world == 1:
+        return (lambda: None), "none"
+    local_n = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    if dev.type == "cuda" and dist.get_backend() == "nccl" and torch.cuda.device_count() >= local_n:
+        flag = torch.ones(1, device=dev)
+
+        def bar():
+            dist.all_reduce(flag)
+
+        return bar, "rccl"
+    return global_barrier, "gloo"
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -140,14 +161,19 @@ def main(argv=None):
 
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    global_barrier()
+    global_barrier()  # coarse: every rank has finished set-up and warm-up
+    tbar, tbar_kind = _timing_barrier(world, dev)
+    tbar()  # opens the RCCL world communicator (lazy init) outside the timer
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    tbar()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     run_all(a.steps)
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    global_barrier()
+    tbar()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -194,6 +220,7 @@ def main(argv=None):
                 "trials": K * T,
                 "backend": trainer.backend if trainer is not None else None,
                 "graphs": (not a.no_graphs),
+                "timing_barrier": tbar_kind,
                 "valid": bool(flag.item() > 0),
             },
         }

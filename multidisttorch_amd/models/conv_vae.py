@@ -1021,7 +1021,7 @@ class ConvVaeTrainer:
             reference_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, st["step"] + 1, h["lr"],
                             h["beta1"], h["beta2"], h["eps"], h["weight_decay"], h["grad_scale"], self.decoupled_wd)
             self.model.from_arena(self.named_parameters())
-        lv = float(loss)
+        lv = float(loss.detach())
         self._hist[st["step"] % 4096] = lv
         st["epoch_loss"] += lv
         st["epoch_count"] += 1
@@ -1128,7 +1128,7 @@ class ConvVaeTrainer:
                 loss, t, _, _ = self.model.loss(x, eps, self.hp["kl_beta"])
                 if want_first_recon and b == 0:
                     first = torch.sigmoid(t).permute(0, 2, 3, 1).reshape(M, self.D).clone()
-                lv = float(loss)
+                lv = float(loss.detach())
                 self._hist_eval[st["step"] % 4096] = lv
                 st["epoch_loss"] += lv
                 st["epoch_count"] += 1
