@@ -148,7 +148,13 @@ bool plan_wgrad(const ConvDesc& d, WgradPlan* p) {
     const char* e = getenv("MDT_CONV_WG_TARGET");
     return e ? atoi(e) : 0;
   }();
-  int target = fixed_target;
+  // MDT_CONV_WG_TARGET_THIN pins the target of the single-channel-input
+  // (thin) layers only: their finalize sits on the optimizer tail
+  static const int thin_target = [] {
+    const char* e = getenv("MDT_CONV_WG_TARGET_THIN");
+    return e ? atoi(e) : 0;
+  }();
+  int target = q.thin && thin_target > 0 ? thin_target : fixed_target;
   if (target <= 0) {
     const long long work = (long long)q.mtiles * tiles;
     target = (int)std::min<long long>(640, std::max<long long>(160, work / 16));

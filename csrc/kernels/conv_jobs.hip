@@ -244,6 +244,11 @@ const Combo kCombos[] = {
     // step's first launch (batch gather + step begin + first layer) || the
     // transposed weight copies the previous step's one-launch tail left out
     COMBO2(ThinC32f, JWtrans),
+    // ... or the first decoder GEMM (MDT_CONV_DEFER_WT=2)
+    COMBO2(IgC1, JWtrans),
+    COMBO2(IgC4, JWtrans),
+    COMBO2(IgC5, JWtrans),
+    COMBO2(IgC6, JWtrans),
 };
 
 #undef COMBO3

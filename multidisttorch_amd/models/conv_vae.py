@@ -245,6 +245,17 @@ class ConvVaeTrainer:
         # weight-gradient blocks cost more than the launch they save
         # (profiles/r1_tail/README.md)
         self.tail1 = os.getenv("MDT_CONV_TAIL1", "0") == "1"
+        # two-launch tail without the transposes (MDT_CONV_DEFER_WT=1|2, no
+        # ticket, no fences): the tail's second launch is the first layer's
+        # finalize alone, and the transposed weight copies ride in the next
+        # step's first launch (=1) or in the decoder Linear's launch (=2: a
+        # 50-block GEMM at 28x28 that leaves most CUs free for the copies).
+        # Measured (profiles/r1_defer): 28x28 0.1249 -> 0.1232 (=1) -> 0.1209
+        # ms/step (=2); 128x128 B=64 0.4517 -> 0.460 (=1) / 0.4545 (=2), so
+        # the default is 2 up to 64x64 images and 0 above
+        mode = os.getenv("MDT_CONV_DEFER_WT", "2" if image <= 64 else "0")
+        self.defer_wt = mode in ("1", "2")
+        self.wt_in_dec = mode == "2"
         self._fused_launches = 0
         self._data = None
         torch.manual_seed(self.seed if init_seed is None else init_seed)
@@ -648,7 +659,7 @@ class ConvVaeTrainer:
         dec = [l for l in self.spec if l.name.startswith("dec")]
         h = self.xb
         first = 0
-        wt = self._tail1_active()  # w16t of the previous step's update still to be written
+        wt = self._wt_deferred()  # w16t of the previous step's update still to be written
         if src is not None:
             X, idx = src
             l = enc[0]
@@ -656,7 +667,7 @@ class ConvVaeTrainer:
                 first_conv = (lambda job, l=l: C.thin_conv(X, self._wf32(l), self._desc(l, M), self._b(l), l.relu,
                                                            self.acts[l.name], job=job, idx=idx, state=state,
                                                            hparams=hp, B=self.B, xb=self.xb))
-                if wt:
+                if wt and not (self.wt_in_dec and not self.tail1):
                     # the transposed copies share the step's first launch (nothing in it reads them)
                     self._run_group([first_conv, lambda job: self._wtrans_layers(1, len(self.spec), job)])
                     wt = False
@@ -666,8 +677,9 @@ class ConvVaeTrainer:
             else:
                 C.step_begin(state, hp)
                 C.gather_rows(X, idx, state, self.B, M, self.xb)
-        if wt:
+        if wt and not (self.wt_in_dec and not self.tail1 and self.fuse_jobs):
             self._wtrans_layers(1, len(self.spec))
+            wt = False
         pro = {}
         for l in enc[first:]:
             last = l is enc[-1]
@@ -695,6 +707,18 @@ class ConvVaeTrainer:
         h = self.z16
         for l in dec:
             last = l is dec[-1]
+            if wt:
+                # the transposed copies share the first decoder launch: nothing
+                # before it reads them, the parity-mode layers after it do
+                wt = False
+                d = self._desc(l, M)
+                if (l.kind != "convT" and not last and C.igemm_plan(0, d, p["ws"] is not None)[10] == 1):
+                    self._run_group([lambda job, l=l, d=d, h=h: C.igemm(0, h, self._w(l), d, self._b(l), l.relu,
+                                                                        self.acts[l.name], None, job=job),
+                                     lambda job: self._wtrans_layers(1, len(self.spec), job)])
+                    h = self.acts[l.name]
+                    continue
+                self._wtrans_layers(1, len(self.spec))
             if last and self._thin_last:  # last layer + BCE + dlogits + bias-grad partials, one launch
                 C.thin_tconv(h, self._wf32(l), self._desc(l, M), self._b(l), X=self.xb,
                              dlog16=self.dlog16 if train else None, recon=self.recon if want_recon else None,
@@ -819,8 +843,11 @@ class ConvVaeTrainer:
                 if fin_hi > 1:
                     fns.append(lambda job, hi=fin_hi: self._finalize_layers(M, 1, hi, job))
                 self._run_group(fns)
-                self._run_group([lambda job: self._finalize_layers(M, 0, 1, job),
-                                 lambda job: self._wtrans_layers(1, L, job)])
+                if self._wt_deferred():
+                    self._finalize_layers(M, 0, 1)
+                else:
+                    self._run_group([lambda job: self._finalize_layers(M, 0, 1, job),
+                                     lambda job: self._wtrans_layers(1, L, job)])
                 break
             if spread and len(fns) == 2 and i + 1 < fin_hi and self._run_with_finalize(fns, M, i + 1, fin_hi):
                 fin_hi = i + 1
@@ -857,6 +884,12 @@ class ConvVaeTrainer:
         leaves the transposed weight copies (w16t) to the next forward, which
         writes them before any launch reads them (``_forward_hip``)."""
         return (self.tail1 and self.fuse_jobs and self._thin_first and self.reducer is None
+                and not self.overlap and len(self.spec) > 1)
+
+    def _wt_deferred(self):
+        """The transposed weight copies (w16t) of a step's update are written by
+        the next step's first launch (one-launch tail, or MDT_CONV_DEFER_WT)."""
+        return ((self.tail1 or self.defer_wt) and self.fuse_jobs and self._thin_first and self.reducer is None
                 and not self.overlap and len(self.spec) > 1)
 
     def _finalize_layers(self, M, lo, hi, job=None):
@@ -1049,7 +1082,7 @@ class ConvVaeTrainer:
                 n -= S
             for _ in range(n):
                 self._replay(1, M)
-        if self._tail1_active():
+        if self._wt_deferred():
             # the last step's transposed weight copies (deferred to the next
             # step's first launch): written here so w16t is current between calls
             self._wtrans_layers(1, len(self.spec))

@@ -242,6 +242,42 @@ def test_one_launch_optimizer_tail_is_bitwise_two_launch(image, batch, native_ex
 
 
 @pytest.mark.parametrize("image,batch", [(28, 128), (128, 32)])
+def test_deferred_transposes_are_bitwise_two_launch(image, batch, native_ext):
+    """MDT_CONV_DEFER_WT: the tail's second launch finalizes only the first
+    layer and the transposed copies are written by the next step's first launch
+    (=1) or by the first decoder GEMM's launch (=2), and at the end of
+    train_steps. Same losses, master weights, Adam moments
+    and transposed weights as the default tail, eager and graph-replayed."""
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    dev = torch.device("cuda")
+    D = image * image
+    X = torch.rand(6 * batch, D, device=dev)
+    idx = torch.arange(6 * batch, device=dev, dtype=torch.int32)
+    out = []
+    for defer, in_dec, graphs in ((False, False, False), (True, False, False), (True, False, True),
+                                  (True, True, False), (True, True, True)):
+        tr = ConvVaeTrainer(batch_size=batch, image=image, device=dev, backend="hip", seed=11,
+                            use_graphs=graphs, graph_steps=2)
+        tr.tail1 = False
+        tr.defer_wt = defer
+        tr.wt_in_dec = in_dec
+        tr.spread_fin = False
+        assert tr._wt_deferred() == defer
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 6)
+        tr.train_steps(5)
+        torch.cuda.synchronize()
+        out.append((tr.loss_history()[:5].copy(), tr.params.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone(),
+                    _wt_layers(tr)))
+    for h, p, m, v, wt in out[1:]:
+        np.testing.assert_array_equal(h, out[0][0])
+        assert torch.equal(p, out[0][1]) and torch.equal(m, out[0][2]) and torch.equal(v, out[0][3])
+        bad = [n for n in wt if not torch.equal(wt[n], out[0][4][n])]
+        assert not bad, bad
+
+
+@pytest.mark.parametrize("image,batch", [(28, 128), (128, 32)])
 def test_spread_finalize_is_bitwise_tail_finalize(image, batch, native_ext):
     """Finalize+Adam of layer j as the third job of the backward launch after
     layer j's gradients completed (MDT_CONV_SPREAD_FIN, default) gives the same
