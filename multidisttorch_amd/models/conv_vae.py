@@ -234,10 +234,12 @@ class ConvVaeTrainer:
         self.fuse_jobs = os.getenv("MDT_CONV_JOBS", "1") != "0"
         # finalize+Adam of each layer spread over the backward launches (third
         # job of the launch after its gradients completed) instead of all in
-        # the optimizer tail. Opt-in (MDT_CONV_SPREAD_FIN=1, bitwise equal):
-        # measured neutral at 28x28 (the tail shrinks, the hosting launches
-        # grow by as much) and 0.7 % slower at 128x128 (profiles/r1_tail)
-        self.spread_fin = os.getenv("MDT_CONV_SPREAD_FIN", "0") == "1"
+        # the optimizer tail (MDT_CONV_SPREAD_FIN, bitwise equal). Measured
+        # neutral at 28x28 with the transposes in the tail (the tail shrinks,
+        # the hosting launches grow by as much) and 0.7 % slower at 128x128
+        # (profiles/r1_tail); with the transposes deferred (below) 1 % faster
+        # at 28x28 (0.1208 -> 0.1196 ms, profiles/r1_defer): on up to 64x64
+        self.spread_fin = os.getenv("MDT_CONV_SPREAD_FIN", "1" if image <= 64 else "0") == "1"
         # one-launch optimizer tail (conv_jobs.hip::tail_k, device ticket) with
         # the transposed weight copies moved into the next step's first launch.
         # Opt-in (MDT_CONV_TAIL1=1): measured slower on MI355X -- the per-wave

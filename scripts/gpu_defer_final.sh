@@ -1,7 +1,7 @@
 # Deferred transposes as the 28x28 default: full GPU suite, smoke, bench (conv28 x2, conv128 B=64, MLP)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/defer_final
+O=gpurun_out/${OUT:-defer_final}
 mkdir -p $O
 export MASTER_ADDR=127.0.0.1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
