@@ -78,8 +78,17 @@ bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p) {
     const char* e = getenv("MDT_CONV_BN_SPLIT_MIN_KT");
     return e ? atoi(e) : 16;
   }();
-  while (q.BN > 32 && !q.thin && cdiv(q.K, 64) >= bn_split_min_kt &&
-         (long long)q.classes * cdiv(q.M, 64) * cdiv(q.Ncols, q.BN) < bn_split_below)
+  // ... and, at any depth, while the grid would stay under
+  // MDT_CONV_BN_SPLIT_TINY = 64 blocks: the 28x28 decoder Linear and encoder
+  // head backward-data GEMMs (M = 128 rows, 50 blocks of 64x128) spread over
+  // twice the CUs (0.1199 -> 0.1152 ms/step, profiles/r1_defer/bn_tiny)
+  static const int bn_split_tiny = [] {
+    const char* e = getenv("MDT_CONV_BN_SPLIT_TINY");
+    return e ? atoi(e) : 64;
+  }();
+  auto grid64 = [&] { return (long long)q.classes * cdiv(q.M, 64) * cdiv(q.Ncols, q.BN); };
+  while (q.BN > 32 && !q.thin &&
+         ((cdiv(q.K, 64) >= bn_split_min_kt && grid64() < bn_split_below) || grid64() < bn_split_tiny))
     q.BN /= 2;
   q.ntiles = cdiv(q.Ncols, q.BN);
   q.ktiles = cdiv(q.K, 64);

@@ -233,6 +233,7 @@ const Combo kCombos[] = {
     COMBO3(IgC1, Wg0, JFinalize),
     COMBO3(IgC4, Wg0, JFinalize),
     COMBO3(IgC5, Wg0, JFinalize),
+    COMBO3(IgC6, Wg0, JFinalize),
     COMBO3(IgT1, Wg0, JFinalize),
     COMBO3(IgT2, Wg0, JFinalize),
     COMBO3(IgT4, Wg0, JFinalize),
