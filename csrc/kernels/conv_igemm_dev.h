@@ -157,9 +157,15 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, f32x4 (&acc)[TC:
     }
     return;
   }
+  // Epilogue order: mask loads, values and column sums in registers, the
+  // column-sum exchange (LDS + barrier), THEN the global stores. A barrier
+  // after the stores would wait for their acknowledgements (vmcnt counts
+  // stores on CDNA) before the column sums could be combined.
   float cs[FN];
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) cs[fn] = 0.f;
+  int grow[FM][4];
+  bool rok[FM][4];
   if (epi) {
     float bv[FN];
 #pragma unroll
@@ -169,69 +175,82 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, f32x4 (&acc)[TC:
     }
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
-      int grow[4];
-      bool rok[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = rbase + fm * 16 + r;
-        rok[r] = m < a.M;
+        rok[fm][r] = m < a.M;
         if constexpr (MODE == kModeConv) {
-          grow[r] = m;
+          grow[fm][r] = m;
         } else {
-          const uint32_t mm = rok[r] ? (uint32_t)m : 0u;
+          const uint32_t mm = rok[fm][r] ? (uint32_t)m : 0u;
           const uint32_t n = fdiv(mm, a.f_pix);
           const uint32_t rem = mm - n * a.f_pix.d;
           const uint32_t yy = fdiv(rem, a.f_w);
           const uint32_t xx = rem - yy * a.f_w.d;
-          grow[r] = ((int)n * d.H + (int)yy * d.S + oa) * d.W + (int)xx * d.S + ob;
+          grow[fm][r] = ((int)n * d.H + (int)yy * d.S + oa) * d.W + (int)xx * d.S + ob;
         }
       }
-      float mk[4][FN];
+    }
+    float mk[FM][4][FN];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) {
           const int col = cbase + fn * 16;
-          const bool ok = rok[r] && col < a.Ncols;
-          mk[r][fn] = (a.omask && ok) ? (float)a.omask[(size_t)grow[r] * a.Ncols + col] : 1.f;
+          const bool ok = rok[fm][r] && col < a.Ncols;
+          mk[fm][r][fn] = (a.omask && ok) ? (float)a.omask[(size_t)grow[fm][r] * a.Ncols + col] : 1.f;
         }
 #pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) {
           const int col = cbase + fn * 16;
-          const bool ok = rok[r] && col < a.Ncols;
+          const bool ok = rok[fm][r] && col < a.Ncols;
           float v = acc[fm][fn][r] + bv[fn];
           if (a.relu) v = fmaxf(v, 0.f);
-          v = mk[r][fn] > 0.f ? v : 0.f;
-          if (ok) {
-            const size_t o = (size_t)grow[r] * a.Ncols + col;
-            if (a.y16) a.y16[o] = (__bf16)v;
-            if (a.y32) a.y32[o] = v;
-          }
+          v = mk[fm][r][fn] > 0.f ? v : 0.f;
+          acc[fm][fn][r] = v;
           cs[fn] += ok ? v : 0.f;
         }
-    }
   }
+  float* sc = reinterpret_cast<float*>(lds + TC::RED_BYTES);
   if (a.colsum) {
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       cs[fn] += __shfl_xor(cs[fn], 16, 64);
       cs[fn] += __shfl_xor(cs[fn], 32, 64);
     }
-    float* sc = reinterpret_cast<float*>(lds + TC::RED_BYTES);
     if (epi && lane < 16) {
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) sc[wm * BN + wn * (BN / WN) + fn * 16 + lane] = cs[fn];
     }
     __syncthreads();
-    if (tid < BN) {
-      float t = 0.f;
+  }
+  if (epi) {
 #pragma unroll
-      for (int q = 0; q < WM; ++q) t += sc[q * BN + tid];
-      const int col = nt * BN + tid;
-      if (col < a.Ncols) a.colsum[(size_t)(cls * a.mtiles + mt) * a.Ncols + col] = t;
-    }
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int col = cbase + fn * 16;
+          if (rok[fm][r] && col < a.Ncols) {
+            const size_t o = (size_t)grow[fm][r] * a.Ncols + col;
+            if (a.y16) a.y16[o] = (__bf16)acc[fm][fn][r];
+            if (a.y32) a.y32[o] = acc[fm][fn][r];
+          }
+        }
+  }
+  if (a.colsum && tid < BN) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < WM; ++q) t += sc[q * BN + tid];
+    const int col = nt * BN + tid;
+    if (col < a.Ncols) a.colsum[(size_t)(cls * a.mtiles + mt) * a.Ncols + col] = t;
   }
 }
 
