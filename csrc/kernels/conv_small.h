@@ -92,9 +92,8 @@ __device__ __forceinline__ void combine_reparam_body(const CombineReparamArgs& a
   red[t] = vm;
   red[256 + t] = vl;
   __syncthreads();
-  float kl = 0.f;
+  float kl = 0.f, mu = 0.f, lv = 0.f, ep = 0.f, zz = 0.f;
   if (rl == 0 && live) {
-    float mu = 0.f, lv = 0.f;
     for (int r = 0; r < a.rp; ++r) {
       mu += red[r * cnt + col];
       lv += red[256 + r * cnt + col];
@@ -103,21 +102,25 @@ __device__ __forceinline__ void combine_reparam_body(const CombineReparamArgs& a
       mu += a.bias[c];
       lv += a.bias[a.Z + c];
     }
-    a.mulv[em] = mu;
-    a.mulv[el] = lv;
     const long long stp = a.st->step - 1;
     const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(i * a.Z + c), a.stream, (uint32_t)((unsigned long long)stp & 0xffffffffu),
                                            (uint32_t)((unsigned long long)stp >> 32)},
                                      a.hp->seed_lo, a.hp->seed_hi);
-    const float ep = normal_from_bits(bits.x, bits.y);
+    ep = normal_from_bits(bits.x, bits.y);
     const float sd = expf(0.5f * lv);
-    const float zz = mu + ep * sd;
+    zz = mu + ep * sd;
+    kl = 1.f + lv - mu * mu - sd * sd;
+  }
+  // the KLD block sum before the stores: its barriers would otherwise wait
+  // for their acknowledgements (vmcnt counts stores on CDNA)
+  const float s = block_sum(kl, red + 512);
+  if (rl == 0 && live) {
+    a.mulv[em] = mu;
+    a.mulv[el] = lv;
     a.eps[e] = ep;
     a.z16[e] = (__bf16)zz;
     if (a.z32) a.z32[e] = zz;
-    kl = 1.f + lv - mu * mu - sd * sd;
   }
-  const float s = block_sum(kl, red + 512);
   if (threadIdx.x == 0) a.kld_part[bid] = -0.5f * s;
 }
 

@@ -225,27 +225,41 @@ __device__ __forceinline__ void thin_tconv_body(const ThinTconvArgs& ta, uint8_t
     }
   const int iy = S * j + oa, ix = S * i + ob;
   const size_t e = ((size_t)n * d.H + iy) * d.W + ix;
-  if (live && ta.y32) ta.y32[e] = acc;
-  float loss = 0.f, gsum = 0.f;
-  if (ta.X) {
-    if (live) {
-      const float t = acc, x = ta.X[e];
-      const float p = 1.f / (1.f + expf(-t));
-      const float g = p - x;
-      if (ta.dlog) ta.dlog[e] = (__bf16)g;
-      if (ta.recon) ta.recon[e] = p;
-      const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));
-      loss = x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
-      gsum = g;
-    }
-    const int pb = bid;
-    const float s = block_sum(loss, scratch);
-    if (threadIdx.x == 0) ta.part[pb] = s;
-    if (ta.gpart) {
-      __syncthreads();
-      const float gs = block_sum(gsum, scratch);
-      if (threadIdx.x == 0) ta.gpart[pb] = gs;
-    }
+  if (!ta.X) {
+    if (live && ta.y32) ta.y32[e] = acc;
+    return;
+  }
+  // BCE, dlogits and both block partial sums first, the global stores last:
+  // a barrier after a store waits for its acknowledgement (vmcnt counts
+  // stores on CDNA). Same summation order as two block_sum calls.
+  float loss = 0.f, gsum = 0.f, p = 0.f;
+  if (live) {
+    const float t = acc, x = ta.X[e];
+    p = 1.f / (1.f + expf(-t));
+    gsum = p - x;
+    const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));
+    loss = x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
+  }
+  const float wl_s = wave_sum(loss), wg_s = ta.gpart ? wave_sum(gsum) : 0.f;
+  const int nw = blockDim.x >> 6;
+  if (lane_id() == 0) {
+    scratch[wave_id()] = wl_s;
+    scratch[8 + wave_id()] = wg_s;
+  }
+  __syncthreads();
+  float sl = 0.f, sg = 0.f;
+  if (threadIdx.x < 64) {
+    sl = wave_sum(threadIdx.x < nw ? scratch[threadIdx.x] : 0.f);
+    if (ta.gpart) sg = wave_sum(threadIdx.x < nw ? scratch[8 + threadIdx.x] : 0.f);
+  }
+  if (live) {
+    if (ta.y32) ta.y32[e] = acc;
+    if (ta.dlog) ta.dlog[e] = (__bf16)gsum;
+    if (ta.recon) ta.recon[e] = p;
+  }
+  if (threadIdx.x == 0) {
+    ta.part[bid] = sl;
+    if (ta.gpart) ta.gpart[bid] = sg;
   }
 }
 

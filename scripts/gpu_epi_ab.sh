@@ -2,7 +2,7 @@
 # prebuilt in-tree copies of _C.so (abtmp/_C_old.so, abtmp/_C_new.so); conv GPU tests on the new one
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/epi
+O=gpurun_out/${OUT:-epi}
 mkdir -p $O
 cp abtmp/_C_new.so multidisttorch_amd/_C.so
 timeout -k 10 400 python -u -m pytest tests/gpu/test_conv_vae_kernels.py tests/gpu/test_conv_igemm.py -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
