@@ -264,6 +264,21 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, f32x4 (&acc)[TC:
 #ifndef MDT_CONV_PF
 #define MDT_CONV_PF 1
 #endif
+// k-loop barrier of the register-staged GEMMs: 0 = __syncthreads (its fence
+// waits vmcnt(0), draining the register prefetches still in flight), 1 =
+// lgkmcnt(0) + s_barrier (LDS writes visible, global prefetches stay in flight)
+#ifndef MDT_CONV_KBAR
+#define MDT_CONV_KBAR 0
+#endif
+__device__ __forceinline__ void kloop_barrier() {
+  if constexpr (MDT_CONV_KBAR == 1) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    __syncthreads();
+  }
+}
 template <int STAGE_REGS>
 constexpr int prefetch_depth() {
   return MDT_CONV_PF > 0 ? MDT_CONV_PF : (STAGE_REGS <= 4 ? 3 : 2);
@@ -477,7 +492,7 @@ __device__ __forceinline__ void igemm_body(const IgArgs& a, uint8_t* lds, int tb
         if (kt + PF < kt1) gload(kt + PF, ra_s[p], rb_s[p], okm_s[p]);  // slot p's tile is already in LDS
         compute(buf);
         if (kt + 1 < kt1) sstore(buf ^ 1, ra_s[(p + 1) % PF], rb_s[(p + 1) % PF], okm_s[(p + 1) % PF]);
-        __syncthreads();
+        kloop_barrier();
       }
     }
   }
@@ -860,7 +875,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, uint8_t* lds, int bi
         if (mtile + PF < mt1) gload(mtile + PF, ra_s[p], rb_s[p], okm_s[p]);
         compute(buf);
         if (mtile + 1 < mt1) sstore(buf ^ 1, ra_s[(p + 1) % PF], rb_s[(p + 1) % PF], okm_s[(p + 1) % PF]);
-        __syncthreads();
+        kloop_barrier();
       }
     }
   }
