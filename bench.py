@@ -13,7 +13,10 @@ DistributedSampler shard of a synthetic MNIST-shaped dataset, with its own
 128x128 conv-VAE of config #5.
 
 A step = one full training iteration (fwd + bwd + [all-reduce] + Adam) of every
-trial. Timing: W warm-up steps (also captures the hipGraphs), then a barrier +
+trial. Timing: ``prepare`` captures the step hipGraphs (S = --graph-steps and the
+S = 1 remainder graph) before anything is timed and the trainers are then
+locked (``strict_graphs``: a missing graph raises rather than being captured
+inside the timer); W warm-up replays, then a barrier +
 device sync, exactly K steps, barrier + device sync; the max over ranks is
 reported. ``value`` = sum over trials of (batch x steps) / max_time (samples are
 counted once per trial, not per replica -- SURVEY.md section 6 metric).
@@ -138,9 +141,15 @@ def main(argv=None):
                 trainer.refresh_weights()
                 mb = None if a.bucket_mb in (None, "") else float(a.bucket_mb)
                 trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, trainer.bucket_bounds(mb)))
-            idx = shard_indices(len(train), K * T, tid)
+            # reference sampler replicas W // group size (vae-hpo.py:146); packing: one shard per trial
+            idx = shard_indices(len(train), (world // n_per) * T, tid)
             trainer.bind_train_data(train.data, idx)
             trainer.set_cursor(0, idx.numel() // a.batch_size)  # full batches only
+            # capture every step graph the timed loop replays (S = graph_steps and
+            # the S = 1 remainder) BEFORE warm-up; afterwards a missing graph is
+            # an error, never a capture inside the timed region
+            trainer.prepare([a.batch_size])
+            trainer.strict_graphs = trainer.use_graphs
             s = torch.cuda.Stream(dev) if (T > 1 and dev.type == "cuda") else None
             if s is not None:
                 with torch.cuda.stream(s):
@@ -222,6 +231,11 @@ def main(argv=None):
                 "graphs": (not a.no_graphs),
                 "timing_barrier": tbar_kind,
                 "valid": bool(flag.item() > 0),
+                # vs_baseline: the reference publishes no numbers (BASELINE.json
+                # "published": {}); the divisor is a builder-measured anchor
+                "baseline": ("NOT a published baseline: builder-measured reference-equivalent torch-eager "
+                             f"loop on one MI355X ({'fp32' if a.model != 'conv128' else 'bf16 autocast'}), "
+                             f"{REF_SAMPLES_PER_S_PER_TRIAL[a.model]:.0f} samples/s per trial x trials"),
             },
         }
         line = json.dumps(out)

@@ -7,6 +7,14 @@ are host C++ against torch's headers. The shared object links torch's bundled
 ``import torch``) so only one HIP runtime ever lives in the process.
 
 Usage: ``python -m multidisttorch_amd._build [-j N] [--force]``.
+
+``MDT_SANITIZE=1`` builds a second, host-sanitized copy
+(``build/san/_C.so``, objects in ``build/native_san``): the C++ runtime
+(reducers, stream/event bookkeeping, planners, bindings) is compiled with
+``-fsanitize=address,undefined``; the gfx950 kernels are unchanged (GPU
+sanitizers are not available on the pool). Load it with
+``MDT_NATIVE_SO=build/san/_C.so`` under ``LD_PRELOAD=<libasan.so>`` on a CPU
+host (``scripts/sanitize_host.sh``).
 """
 
 from __future__ import annotations
@@ -22,8 +30,10 @@ import sysconfig
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "multidisttorch_amd")
 CSRC = os.path.join(ROOT, "csrc")
-BUILD = os.path.join(ROOT, "build", "native")
-OUT = os.path.join(PKG, "_C.so")
+SANITIZE = os.getenv("MDT_SANITIZE", "0") == "1"
+BUILD = os.path.join(ROOT, "build", "native_san" if SANITIZE else "native")
+OUT = os.path.join(ROOT, "build", "san", "_C.so") if SANITIZE else os.path.join(PKG, "_C.so")
+SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
 ARCH = os.environ.get("MDT_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -91,6 +101,8 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
                   "-DHIPBLAS_V2", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C",
                   f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-Wno-deprecated-declarations",
                   "-I" + CSRC, "-I" + pyinc] + ["-I" + p for p in inc] + ["-I" + os.path.join(ROCM, "include")]
+    if SANITIZE:
+        host_flags = ["-O1" if f == "-O2" else f for f in host_flags] + SAN_FLAGS
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     jobsl = []
     for s in kern:
@@ -112,7 +124,8 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
             if verbose and err:
                 print(err, file=sys.stderr)
     if changed or force or not os.path.exists(OUT):
-        link = ["g++", "-shared", "-o", OUT + ".tmp"] + objs + [
+        os.makedirs(os.path.dirname(OUT), exist_ok=True)
+        link = ["g++", "-shared", "-o", OUT + ".tmp"] + (SAN_FLAGS if SANITIZE else []) + objs + [
             "-L" + tlib, "-Wl,-rpath," + tlib,
             "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
             "-lamdhip64", "-lrccl"]  # torch's bundled librccl: the same runtime ProcessGroupNCCL uses

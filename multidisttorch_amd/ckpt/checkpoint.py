@@ -14,6 +14,8 @@ with ``torch.load(weights_only=True)`` (never unpickles code):
   rng          {"seed", "rng_stream"} (Philox is counter-based: the step
                counter + seed fully determine the noise stream)
   layout       [[name, offset, shape...]] of the arena, for validation
+  arch         model kind + dims (mlp: D/H/Z; conv: image/channels/Z + the
+               layer table), validated on load before any tensor is copied
 Only group rank 0 writes (replicas are identical after the all-reduce);
 writes go to a temp file + atomic rename so a crash never leaves a torn file.
 """
@@ -44,7 +46,7 @@ def save_trial(ckpt_dir: str, trainer, spec, epoch: int, extra: Optional[dict] =
         "progress": {"epoch": int(epoch), "step": int(opt["step"])},
         "rng": {"seed": int(trainer.seed), "rng_stream": int(trainer.rng_stream)},
         "layout": [[n, int(o)] + [int(x) for x in s] for n, o, s in trainer.layout],
-        "dims": [int(trainer.D), int(trainer.H), int(trainer.Z)],
+        "arch": trainer.model_meta(),
     }
     if extra:
         payload["extra"] = extra
@@ -78,6 +80,10 @@ def load_latest(ckpt_dir: str, group_id: int, trainer) -> Optional[dict]:
     ck = torch.load(path, map_location="cpu", weights_only=True)
     if ck.get("format") != "multidisttorch_amd.trial.v1":
         raise ValueError(f"{path}: unknown checkpoint format {ck.get('format')!r}")
+    arch = ck.get("arch")
+    if arch is not None and arch != trainer.model_meta():
+        raise ValueError(f"{path}: checkpoint is for {arch.get('kind')} model {arch}, "
+                         f"trainer is {trainer.model_meta()}")
     lay = [[n, int(o)] + [int(x) for x in s] for n, o, s in trainer.layout]
     if ck["layout"] != lay:
         raise ValueError(f"{path}: parameter arena layout mismatch")

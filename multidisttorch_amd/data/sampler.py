@@ -17,7 +17,20 @@ import math
 
 import torch
 
-__all__ = ["shard_indices", "batch_count", "EpochIndexer"]
+__all__ = ["shard_indices", "batch_count", "EpochIndexer", "reference_num_replicas"]
+
+
+def reference_num_replicas(world_size: int, group_size: int) -> int:
+    """``num_replicas`` exactly as /root/reference/vae-hpo.py:146 computes it:
+    ``world_size // local_size`` with ``local_size`` the trial group's size.
+
+    This is NOT always the trial count K: with leftover ranks (W % K != 0) the
+    reference still divides the world by the group size, e.g. W=3, K=2 gives
+    groups of 1 and ``num_replicas = 3`` (three shards of 20000, the third never
+    trained), W=7, K=3 gives groups of 2 and ``num_replicas = 3``."""
+    if group_size < 1 or world_size < group_size:
+        raise ValueError(f"bad world/group sizes {world_size}/{group_size}")
+    return world_size // group_size
 
 
 def shard_indices(n: int, num_replicas: int, rank: int, shuffle: bool = True, seed: int = 0,

@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import math
 import os
+import sys
 import time
 from dataclasses import dataclass, field
 from typing import Optional
@@ -31,14 +32,15 @@ import torch
 import torch.distributed as dist
 
 from ..ckpt import checkpoint as ckpt
-from ..data.sampler import shard_indices
+from ..data.sampler import reference_num_replicas, shard_indices
 from ..obs.metrics import TrialMetrics
 from ..obs import trace
 from ..parallel.autotune import autotune_comm
 from ..parallel.ddp import broadcast_params, make_arena_reducer
 from ..parallel.groups import print0
 from ..runtime.bootstrap import bound_device, global_barrier
-from ..runtime.faults import guarded, maybe_inject
+from ..runtime.faults import (InjectedFault, TrialTimeout, agree_healthy, fault_step, group_timeout_s, guarded,
+                              maybe_inject)
 from ..utils.images import flush_images, save_image_async
 from .trial import TrialSpec
 
@@ -64,7 +66,7 @@ class RunOptions:
     test_samples: Optional[int] = None     # (default 10000)
     image_size: int = 28
     data_dir: str = "data"
-    synthetic: Optional[bool] = True
+    synthetic: Optional[bool] = None       # None: IDX files when present, else synthetic; True/False force
     bucket_mb: Optional[object] = None     # None: model default; 0: one bucket; float: MiB cap; "auto": measured
     profile: bool = False                  # roctx ranges + device-synced phase timings in the metrics JSONL
 
@@ -116,35 +118,94 @@ def _load_data(opts: RunOptions, device):
     return train, test
 
 
-def _launch_epoch(trainer, epoch: int, n_shard: int, opts: RunOptions) -> int:
-    """Enqueue one epoch of steps on the current stream (no host sync); returns
-    the step counter before the epoch."""
+LOSS_RING = 4096  # per-step loss history ring of the trainers (kLossHist, csrc/kernels/vae_mlp.h)
+
+
+def _launch_epoch(trainer, epoch: int, n_shard: int, opts: RunOptions, fault_at: Optional[int] = None):
+    """Enqueue one epoch of steps on the current stream; returns (step counter
+    before the epoch, {batch_idx: loss} of log lines whose ring slots were read
+    early). No host sync unless the epoch is longer than the loss ring: then
+    the ring is read after every LOSS_RING steps, before it wraps (batch sizes
+    below 15 on a 60000-sample shard). ``fault_at`` (MDT_FAULT step=) stops
+    issuing steps at that optimizer step and raises, mid-epoch."""
     B = opts.batch_size
     full, tail = n_shard // B, n_shard % B
     nb = full + (1 if tail else 0)
     trainer.set_cursor(0, nb)
     trainer.reset_loss()
     step0 = trainer.step_count
+    early = {}
+    stop = None if fault_at is None or not step0 <= fault_at < step0 + nb else fault_at - step0
     with trace.range(f"train_epoch_{epoch}"):
-        trainer.train_steps(full, B)
+        c = 0
+        while c < full:
+            n = min(full - c, LOSS_RING) if nb > LOSS_RING else full - c
+            if stop is not None and c + n > stop:
+                trainer.train_steps(stop - c, B)
+                raise InjectedFault(f"injected fault at step {fault_at} (epoch {epoch})")
+            trainer.train_steps(n, B)
+            if nb > LOSS_RING:
+                hist = trainer.loss_history()
+                assert len(hist) == LOSS_RING
+                for bi in range(c - c % opts.log_interval, c + n, opts.log_interval):
+                    if bi >= c:
+                        early[bi] = float(hist[(step0 + bi) % LOSS_RING])
+            c += n
         if tail:
+            if stop is not None and stop == full:
+                raise InjectedFault(f"injected fault at step {fault_at} (epoch {epoch})")
             trainer.train_steps(1, tail)
-    return step0
+    return step0, early
+
+
+def _wait_epoch(trainer, group, device):
+    """Bounded wait for this replica's enqueued epoch (groups > 1 on GPU).
+
+    The bucket collectives run inside replayed graphs, out of sight of
+    ProcessGroupNCCL's watchdog: if a peer died mid-epoch they would never
+    complete. Poll the epoch's completion event; past ``MDT_GROUP_TIMEOUT_S``
+    abort the group's communicator (RCCL kernels observe the abort flag and
+    exit) and fail the trial."""
+    if device.type != "cuda" or group is None or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    ev = torch.cuda.Event()
+    ev.record()
+    deadline = time.monotonic() + group_timeout_s()
+    while not ev.query():
+        if time.monotonic() > deadline:
+            try:
+                be = group._get_backend(device)
+                if hasattr(be, "abort"):
+                    be.abort()
+            except Exception:  # noqa: BLE001 - best effort, we are failing anyway
+                pass
+            raise TrialTimeout(f"epoch did not complete within {group_timeout_s():.0f} s (peer lost?)")
+        time.sleep(0.0005)
+    red = getattr(trainer, "reducer", None)
+    if red is not None and hasattr(red, "status") and int(red.status()) != 0:
+        raise TrialTimeout(f"p2p all-reduce gave up waiting for a peer (status {int(red.status())})")
 
 
 def _train_epoch(trainer, epoch: int, n_shard: int, n_dataset: int, opts: RunOptions, group,
-                 step0: Optional[int] = None, tag: str = "") -> float:
+                 step0: Optional[int] = None, tag: str = "", fault_at: Optional[int] = None) -> float:
     B = opts.batch_size
     full, tail = n_shard // B, n_shard % B
     nb = full + (1 if tail else 0)
+    early = {}
     if step0 is None:
-        step0 = _launch_epoch(trainer, epoch, n_shard, opts)
+        step0, early = _launch_epoch(trainer, epoch, n_shard, opts, fault_at)
+        _wait_epoch(trainer, group, getattr(trainer, "device", torch.device("cpu")))
+    elif nb > LOSS_RING:
+        raise ValueError(f"{nb} batches per epoch exceed the {LOSS_RING}-entry loss ring of a packed trial; "
+                         f"use a larger --batch-size or --trials-per-group 1")
     hist = trainer.loss_history()
     st = trainer.read_state()
     if not opts.quiet_train_log:
         for batch_idx in range(0, nb, opts.log_interval):
             bsz = B if batch_idx < full else tail
-            loss_b = float(hist[(step0 + batch_idx) % len(hist)])
+            loss_b = early.get(batch_idx)
+            if loss_b is None:
+                loss_b = float(hist[(step0 + batch_idx) % len(hist)])
             print0(tag + "Train Epoch: {} [{}/{} ({:.0f}%)]\tLoss: {:.6f}".format(
                 epoch, batch_idx * bsz, n_dataset, 100.0 * batch_idx / nb, loss_b / bsz), process_group=group)
     # The reference divides by the FULL dataset size, not the shard (Q6).
@@ -176,10 +237,15 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
     world_size = dist.get_world_size() if dist.is_initialized() else 1
     grank = dist.get_rank(group) if dist.is_initialized() else 0
     gsize = dist.get_world_size(group) if dist.is_initialized() else 1
-    K = num_trials if num_trials is not None else world_size // gsize
+    # sampler replicas exactly as the reference (vae-hpo.py:146): W // group size,
+    # which differs from the trial count K when W % K != 0 (leftover idle ranks)
+    n_rep = reference_num_replicas(world_size, gsize)
     device = bound_device()
 
     train, test = data if data is not None else _load_data(opts, device)
+    if grank == 0:  # stderr: stdout stays byte-compatible with the reference
+        print(f"[mdt] trial {spec.group_id}: train data {train.name} ({'synthetic' if train.synthetic else 'IDX'}, "
+              f"{len(train)} x {tuple(train.shape)})", file=sys.stderr, flush=True)
     D = int(train.data.shape[1])
     trainer = _make_trainer(spec, opts, device, grank, D)
     if gsize > 1:
@@ -187,7 +253,7 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
         broadcast_params([trainer.params], group)
         trainer.refresh_weights()
         if opts.bucket_mb == "auto":
-            idx0 = shard_indices(len(train), K, spec.group_id)
+            idx0 = shard_indices(len(train), n_rep, spec.group_id)
             key = f"{opts.model}-{opts.image_size}-b{opts.batch_size}-n{trainer.numel}-s{gsize}"
             bounds, kind, timings = autotune_comm(lambda: _make_trainer(spec, opts, device, grank, D), group,
                                                   train.data, idx0, key=key)
@@ -198,16 +264,24 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
         trainer.attach_reducer(make_arena_reducer(group, trainer.grads, bounds, kind=kind))
     start_epoch = 1
     if opts.ckpt_dir and opts.resume:
-        prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer)
+        # only group rank 0 writes checkpoints, so only it reads one; the
+        # replicas receive weights, Adam moments, the step counter and the
+        # epoch to resume from (no shared filesystem needed)
+        prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer) if grank == 0 else None
         if prog is not None:
             start_epoch = prog["epoch"] + 1
             print0(f"resumed trial {spec.group_id} from {prog['path']} (epoch {prog['epoch']})", process_group=group)
         if gsize > 1:
             broadcast_params([trainer.params, trainer.exp_avg, trainer.exp_avg_sq], group)
+            meta = torch.tensor([start_epoch, trainer.step_count], dtype=torch.int64,
+                                device=device if dist.get_backend(group) == "nccl" else "cpu")
+            broadcast_params([meta], group)
+            start_epoch = int(meta[0].item())
+            trainer.set_step(int(meta[1].item()))
             trainer.refresh_weights()
     metrics = TrialMetrics(opts.metrics_dir, spec.group_id, enabled=(grank == 0))
 
-    idx = shard_indices(len(train), K, spec.group_id)
+    idx = shard_indices(len(train), n_rep, spec.group_id)
     trainer.bind_train_data(train.data, idx)
     n_shard = idx.numel()
     # capture the step graphs and load the eval/decode kernels now, like the
@@ -229,12 +303,23 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
         failure["error"] = f"{type(e).__name__}: {e}"
         metrics.log(event="trial_failed", error=failure["error"])
 
+    fault_at = fault_step(trial=spec.group_id, rank=world_rank)
+    checked_in = False  # this member's "not ok" has been delivered to the group
     with guarded(f"trial {spec.group_id} (world rank {world_rank})", group, _fail):
         for epoch in range(start_epoch, spec.epochs + 1):
+            # group members agree on health before every epoch (see faults.py)
+            if not agree_healthy(spec.group_id, True):
+                checked_in = True
+                raise RuntimeError("a replica of this trial failed; stopping the trial on every member")
             maybe_inject(trial=spec.group_id, epoch=epoch, rank=world_rank)
             train_loss, test_loss = _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape,
-                                               gen, device, spec, grank, metrics)
+                                               gen, device, spec, grank, metrics, fault_at=fault_at)
             epochs_done += 1
+        if not agree_healthy(spec.group_id, True):
+            checked_in = True
+            raise RuntimeError("a replica of this trial failed in its last epoch")
+    if failure and not checked_in:
+        agree_healthy(spec.group_id, False)
 
     flush_images()
     global_barrier()  # parity: vae-hpo.py:172 (waits for the slowest trial)
@@ -245,9 +330,10 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
 
 
 def _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape, gen, device, spec, grank, metrics,
-               step0=None, t_train=None, tag=""):
+               step0=None, t_train=None, tag="", fault_at=None):
     te = time.perf_counter()
-    train_loss = _train_epoch(trainer, epoch, n_shard, len(train), opts, group, step0=step0, tag=tag)
+    train_loss = _train_epoch(trainer, epoch, n_shard, len(train), opts, group, step0=step0, tag=tag,
+                              fault_at=fault_at)
     if t_train is None:
         t_train = time.perf_counter() - te
     phases = {}
@@ -310,7 +396,7 @@ def run_packed_trials(specs, group, opts: RunOptions, data=None, num_trials: Opt
             prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer)
             if prog is not None:
                 start = prog["epoch"] + 1
-        idx = shard_indices(len(train), total, spec.group_id)
+        idx = shard_indices(len(train), total, spec.group_id)  # packing extension: one shard per trial
         trainer.bind_train_data(train.data, idx)
         trainer.prepare([opts.batch_size, idx.numel() % opts.batch_size], test.data[: opts.batch_size])
         rdir = (f"results-t{spec.group_id}-0" if opts.results else None)
@@ -331,9 +417,9 @@ def run_packed_trials(specs, group, opts: RunOptions, data=None, num_trials: Opt
                 maybe_inject(trial=t["spec"].group_id, epoch=epoch, rank=world_rank)
                 if t["stream"] is not None:
                     with torch.cuda.stream(t["stream"]):
-                        t["step0"] = _launch_epoch(t["trainer"], epoch, t["n_shard"], opts)
+                        t["step0"], _ = _launch_epoch(t["trainer"], epoch, t["n_shard"], opts)
                 else:
-                    t["step0"] = _launch_epoch(t["trainer"], epoch, t["n_shard"], opts)
+                    t["step0"], _ = _launch_epoch(t["trainer"], epoch, t["n_shard"], opts)
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         t_train = time.perf_counter() - te

@@ -283,6 +283,11 @@ class ConvVaeTrainer:
         self._push_hparams()
 
     # ----------------------------------------------------------- arenas
+    def model_meta(self) -> dict:
+        """Architecture record stored in checkpoints and validated on load."""
+        return {"kind": "conv", "image": int(self.image), "channels": int(self.channels), "Z": int(self.Z),
+                "layers": [[l.name, l.kind, l.cin, l.cout, l.k, l.s, l.p] for l in self.spec]}
+
     def named_parameters(self):
         return {n: self.params.narrow(0, o, math.prod(s)).view(s) for n, o, s in self.layout}
 
@@ -1109,9 +1114,16 @@ class ConvVaeTrainer:
             self.reset_loss(eval=True)
         torch.cuda.synchronize(self.device)
 
+    # strict_graphs: a replay that finds no captured graph raises instead of
+    # capturing lazily (bench.py / autotune set it after ``prepare`` so no
+    # capture ever lands inside a timed region)
+    strict_graphs = False
+
     def _replay(self, S, M):
         g = self._graphs.get((S, M))
         if g is None:
+            if self.strict_graphs:
+                raise RuntimeError(f"no captured step graph for (steps={S}, M={M}); call prepare() first")
             g = self._capture(S, M)
             self._graphs[(S, M)] = g
         g.replay()

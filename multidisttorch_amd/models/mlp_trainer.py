@@ -281,10 +281,19 @@ class MlpVaeTrainer:
             self.reset_loss(eval=True)
         torch.cuda.synchronize(self.device)
 
+    def model_meta(self) -> dict:
+        """Architecture record stored in checkpoints and validated on load."""
+        return {"kind": "mlp", "D": int(self.D), "H": int(self.H), "Z": int(self.Z)}
+
+    # see ConvVaeTrainer.strict_graphs: no lazy capture once set
+    strict_graphs = False
+
     def _replay(self, S: int, M: int):
         key = (S, M)
         g = self._graphs.get(key)
         if g is None:
+            if self.strict_graphs:
+                raise RuntimeError(f"no captured step graph for (steps={S}, M={M}); call prepare() first")
             g = self._capture(S, M)
             self._graphs[key] = g
         g.replay()

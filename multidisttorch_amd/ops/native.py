@@ -9,7 +9,9 @@ are clearly labelled as such (``backend == "torch"``).
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 
 import torch
 
@@ -22,7 +24,14 @@ def _load():
     if _MOD is not None or _ERR is not None:
         return _MOD
     try:
-        _MOD = importlib.import_module("multidisttorch_amd._C")
+        alt = os.getenv("MDT_NATIVE_SO")  # e.g. the host-sanitized build (_build.py, MDT_SANITIZE=1)
+        if alt:
+            spec = importlib.util.spec_from_file_location("multidisttorch_amd._C", alt)
+            _MOD = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_MOD)
+            sys.modules["multidisttorch_amd._C"] = _MOD
+        else:
+            _MOD = importlib.import_module("multidisttorch_amd._C")
     except Exception as e:  # pragma: no cover - exercised when the .so is absent
         _ERR = e
         _MOD = None

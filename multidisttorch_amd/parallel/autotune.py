@@ -129,6 +129,11 @@ def autotune_comm(make_trainer: Callable[[], object], pg, X: torch.Tensor, idx: 
             # the previous reducer is dropped here: every member finished its kernels
             # before the MAX all-reduce below, so no peer still writes into its region
             tr.attach_reducer(make_arena_reducer(pg, tr.grads, bounds, kind=kind))
+            # graphs for this layout are captured here, outside the timer; a
+            # replay that misses one raises instead of capturing while timed
+            if hasattr(tr, "prepare"):
+                tr.prepare([B])
+                tr.strict_graphs = bool(getattr(tr, "use_graphs", False))
             tr.train_steps(warmup)
             if on_gpu:
                 torch.cuda.synchronize(dev)

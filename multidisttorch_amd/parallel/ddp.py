@@ -151,19 +151,34 @@ class PyBucketReducer:
         return self._launched
 
 
+COMM_WARMUPS = [0]  # lazy communicators forced into existence by rccl_comm_ptr (tests assert on it)
+
+
 def rccl_comm_ptr(pg, device: torch.device) -> int:
     """ncclComm_t (as int) of a trial group's ProcessGroupNCCL on `device`.
 
-    torch creates RCCL communicators lazily; one tiny all-reduce forces the
-    communicator into existence so the native reducer can reuse it (one
-    communicator and one RCCL runtime per group, shared with c10d)."""
+    On a device-bound world (the default with one GPU per rank) the group's
+    communicator was created eagerly by ``ncclCommSplit`` in ``new_group``
+    and is used as is. A lazily created group (ranks sharing a GPU, or
+    ``MDT_EAGER_COMM=0``) gets one tiny all-reduce that forces its
+    communicator into existence. Either way the native reducer reuses torch's
+    communicator: one communicator and one RCCL runtime per group."""
     backend = pg._get_backend(device)
     if not hasattr(backend, "_comm_ptr"):
         raise RuntimeError(f"process group backend {type(backend).__name__} is not RCCL")
-    t = torch.zeros(1, device=device)
-    dist.all_reduce(t, group=pg)
-    torch.cuda.current_stream(device).synchronize()
-    return int(backend._comm_ptr())
+    ptr = 0
+    if getattr(pg, "bound_device_id", None) is not None:
+        try:
+            ptr = int(backend._comm_ptr())
+        except RuntimeError:
+            ptr = 0
+    if not ptr:
+        COMM_WARMUPS[0] += 1
+        t = torch.zeros(1, device=device)
+        dist.all_reduce(t, group=pg)
+        torch.cuda.current_stream(device).synchronize()
+        ptr = int(backend._comm_ptr())
+    return ptr
 
 
 def reducer_kind(pg, flat: torch.Tensor) -> str:

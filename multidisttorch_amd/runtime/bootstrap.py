@@ -12,8 +12,9 @@ MI355X-first differences:
     barriers of the HPO driver, so trials of different length never trip the
     RCCL watchdog (10 min) at the final barrier and idle leftover ranks can
     still join it;
-  * optional eager, device-bound world (``MDT_EAGER_COMM=1``) so sub-groups are
-    produced by ``ncclCommSplit`` instead of a fresh bootstrap each.
+  * eager, device-bound RCCL world by default when every local rank has its
+    own GPU (``eager_comm_requested``), so trial groups are produced by
+    ``ncclCommSplit`` instead of a fresh bootstrap each.
 """
 
 from __future__ import annotations
@@ -60,11 +61,23 @@ def get_comm_size_and_rank():
     return 1, 0
 
 
-def eager_comm_requested() -> bool:
-    """MDT_EAGER_COMM=1: bind the world communicator to the local device at
-    init (eager RCCL world) so trial groups are split from it (ncclCommSplit)
-    instead of being bootstrapped from scratch at their first collective."""
-    return os.getenv("MDT_EAGER_COMM", "0") == "1"
+def eager_comm_requested(info: Optional[_envmod.LaunchInfo] = None, ndev: Optional[int] = None) -> bool:
+    """Bind the RCCL world to the local device at init (eager communicator),
+    so trial groups are split from it (``ncclCommSplit``) instead of each
+    bootstrapping a fresh communicator at its first collective.
+
+    ``MDT_EAGER_COMM=1`` forces it, ``=0`` forbids it; by default it is on
+    whenever every rank of this node has its own GPU (the launcher reports a
+    local size no larger than the visible device count) -- the one-process-
+    per-MI355X layout. Ranks sharing a GPU (RCCL rejects duplicate devices in
+    one communicator) or an unknown local size keep the lazy path."""
+    v = os.getenv("MDT_EAGER_COMM", "auto")
+    if v in ("0", "1"):
+        return v == "1"
+    info = info or _STATE.get("launch")
+    if info is None or info.local_size is None or not ndev:
+        return False
+    return info.local_size <= ndev
 
 
 def world_is_device_bound() -> bool:
@@ -129,7 +142,7 @@ def setup_ddp(backend: Optional[str] = None, verbose: bool = True,
         kwargs = {}
         if timeout_s is not None:
             kwargs["timeout"] = _dt.timedelta(seconds=timeout_s)
-        if backend == "nccl" and eager_comm_requested() and _STATE["device"].type == "cuda":
+        if backend == "nccl" and _STATE["device"].type == "cuda" and eager_comm_requested(info, ndev):
             kwargs["device_id"] = _STATE["device"]
         dist.init_process_group(backend=backend, init_method="env://",
                                 world_size=world_size, rank=world_rank, **kwargs)

@@ -71,6 +71,21 @@ def local_rank_from_env(env: Optional[Mapping[str, str]] = None,
     return 0
 
 
+def local_size_from_env(env: Optional[Mapping[str, str]] = None) -> Optional[int]:
+    """Number of ranks on this node, when the launcher says (torchrun
+    ``LOCAL_WORLD_SIZE``, Open MPI ``OMPI_COMM_WORLD_LOCAL_SIZE``, MPICH
+    ``MPI_LOCALNRANKS``, SLURM ``SLURM_NTASKS_PER_NODE``); None if unknown."""
+    e = _env(env)
+    for key in ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "SLURM_NTASKS_PER_NODE"):
+        v = e.get(key)
+        if v not in (None, ""):
+            try:
+                return int(v)
+            except ValueError:  # e.g. SLURM's "8(x2)"
+                continue
+    return None
+
+
 def parse_slurm_nodelist(nodelist: str):
     """Expand a SLURM compressed host list.
 
@@ -158,6 +173,7 @@ class LaunchInfo:
     master_addr: str
     master_port: str
     launcher: str
+    local_size: Optional[int] = None
 
     @property
     def is_distributed(self) -> bool:
@@ -179,4 +195,4 @@ def discover(env: Optional[Mapping[str, str]] = None, ndev: Optional[int] = None
     ws, wr = init_comm_size_and_rank(e)
     addr, port = discover_master(e)
     lr = local_rank_from_env(e, wr, ndev)
-    return LaunchInfo(ws, wr, lr, addr, port, _launcher_name(e))
+    return LaunchInfo(ws, wr, lr, addr, port, _launcher_name(e), local_size_from_env(e))

@@ -1,0 +1,217 @@
+"""Intra-group DDP of the flagship conv-VAE on the HIP path (BASELINE configs
+#4/#5; reference: ``DistributedDataParallel(model, process_group=group)`` at
+/root/reference/vae-hpo.py:129-131 and the per-step all-reduce at :72).
+
+``ConvVaeTrainer`` with a reducer attached runs a different step from the
+single-replica one: per-bucket gradient finalize -> bucket all-reduce launched
+while the rest of the backward is still being issued -> wait -> Adam + bf16
+cast -> transposed copies. These tests run that step on the GPU:
+  * a 1-rank RCCL world (the real RcclBucketReducer on torch's communicator):
+    bucket layouts None / 0 / 0.5 MiB, eager and graph-replayed, 28x28 and
+    128x128; results must equal the reducer-free step (the all-reduce over one
+    rank is an identity) and the bucket launches must interleave with the
+    backward GEMM launches;
+  * s = 2 and 4 processes sharing the GPU through the p2p reducer
+    (conv_ddp_worker.py): replicas bitwise identical, and equal to the
+    single-process run when every replica draws the same eps.
+Plus the bench/autotune graph-capture hygiene: after ``prepare`` a timed
+``train_steps`` never captures.
+"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture()
+def nccl_world():
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield dist.group.WORLD
+    dist.destroy_process_group()
+
+
+def _data(image, nb, B, dev):
+    X = torch.rand(nb * B, image * image, generator=torch.Generator().manual_seed(3)).to(dev)
+    return X, torch.arange(nb * B, device=dev, dtype=torch.int32)
+
+
+def _trainer(image, B, dev, graphs, **kw):
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    return ConvVaeTrainer(batch_size=B, image=image, z=32 if image == 28 else 64, device=dev, backend="hip",
+                          seed=4, lr=2e-3, use_graphs=graphs, graph_steps=4, **kw)
+
+
+class _CallLog:
+    """Proxy of the native module recording the order of launch-issuing calls."""
+
+    def __init__(self, C, log):
+        self._C, self._log = C, log
+
+    def __getattr__(self, name):
+        f = getattr(self._C, name)
+        if not callable(f) or name[0].isupper():
+            return f
+
+        def wrap(*a, **k):
+            self._log.append(name)
+            return f(*a, **k)
+
+        return wrap
+
+
+class _RedLog:
+    def __init__(self, red, log):
+        self._red, self._log = red, log
+
+    def bounds(self):
+        return self._red.bounds()
+
+    def launch(self, k):
+        self._log.append(f"bucket{k}")
+        return self._red.launch(k)
+
+    def wait_all(self):
+        self._log.append("wait_all")
+        return self._red.wait_all()
+
+    def __getattr__(self, n):
+        return getattr(self._red, n)
+
+
+@pytest.mark.parametrize("image", [28, 128])
+def test_conv_trainer_rccl_reducer_matches_single(nccl_world, native_ext, image):
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+
+    dev = torch.device("cuda", 0)
+    B = 128 if image == 28 else 32
+    nb, steps = 4, 8
+    X, idx = _data(image, nb, B, dev)
+    runs = {}
+    for graphs in (False, True):
+        for mb in ("single", None, 0, 0.5):
+            tr = _trainer(image, B, dev, graphs)
+            if mb != "single":
+                red = make_arena_reducer(nccl_world, tr.grads, tr.bucket_bounds(mb))
+                assert type(red).__name__ == "RcclBucketReducer"
+                tr.attach_reducer(red)
+            tr.bind_train_data(X, idx)
+            tr.set_cursor(0, nb)
+            tr.train_steps(steps)
+            torch.cuda.synchronize()
+            runs[(graphs, mb)] = (tr.params.clone(), tr.loss_history()[:steps].copy(), tr.read_state()["step"])
+            if mb != "single":
+                # host-side launches: every step eagerly, or the capture-time
+                # warm-up step + the 4 captured steps of the S=4 graph
+                assert red.launched_count() == (5 if graphs else steps) * red.num_buckets()
+                assert red.pending() == 0
+    p0, h0, s0 = runs[(False, "single")]
+    assert s0 == steps and np.isfinite(h0).all()
+    for key, (p, h, s) in runs.items():
+        assert s == steps, key
+        # one rank: the all-reduce is an identity; only where Adam runs differs
+        # (fused into the finalize vs one flat launch after the all-reduce)
+        np.testing.assert_allclose(h, h0, rtol=1e-5, err_msg=str(key))
+        torch.testing.assert_close(p, p0, rtol=1e-5, atol=1e-6, msg=str(key))
+
+
+@pytest.mark.parametrize("image", [28, 128])
+def test_conv_bucket_launches_interleave_with_backward(nccl_world, native_ext, image):
+    """Eager step with three or more buckets: the first (decoder-end) bucket's
+    all-reduce is issued before the backward GEMMs of the earlier layers, and
+    the wait comes after the last backward launch."""
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+
+    dev = torch.device("cuda", 0)
+    B = 128 if image == 28 else 32
+    X, idx = _data(image, 2, B, dev)
+    tr = _trainer(image, B, dev, graphs=False)
+    bounds = tr.bucket_bounds(0.25 if image == 28 else 2.0)
+    assert len(bounds) - 1 >= 3, bounds
+    log = []
+    tr.attach_reducer(_RedLog(make_arena_reducer(nccl_world, tr.grads, bounds), log))
+    tr.bind_train_data(X, idx)
+    tr.set_cursor(0, 2)
+    tr.C = _CallLog(tr.C, log)
+    tr.train_steps(1)
+    torch.cuda.synchronize()
+    nbk = len(bounds) - 1
+    first = log.index(f"bucket{nbk - 1}")  # the last arena bucket holds the decoder: ready first
+    wait = log.index("wait_all")
+    bwd = [i for i, n in enumerate(log) if n in ("wgrad", "igemm", "thin_conv", "launch_jobs")]
+    assert any(first < i < wait for i in bwd), log
+    assert all(f"bucket{k}" in log[:wait] for k in range(nbk)), log
+    assert log.index("adam_cast") > wait, log
+
+
+@pytest.mark.parametrize("model", ["conv28", "mlp"])
+def test_prepare_locks_graphs_for_timed_steps(native_ext, model):
+    """bench.py contract: after prepare() the timed train_steps(20) with
+    warmup=5, graph_steps=10 replays only pre-captured graphs."""
+    from multidisttorch_amd.models.mlp_trainer import MlpVaeTrainer
+
+    dev = torch.device("cuda", 0)
+    X, idx = _data(28, 8, 128, dev)
+    if model == "mlp":
+        tr = MlpVaeTrainer(batch_size=128, device=dev, backend="hip", seed=1, use_graphs=True, graph_steps=10)
+    else:
+        tr = _trainer(28, 128, dev, True)
+        tr.graph_steps = 10
+    tr.bind_train_data(X, idx)
+    tr.set_cursor(0, 8)
+    tr.prepare([128])
+    tr.strict_graphs = True
+    keys = set(tr._graphs)
+    assert keys == {(10, 128), (1, 128)}
+    tr.train_steps(5)
+    tr.train_steps(20)
+    torch.cuda.synchronize()
+    assert set(tr._graphs) == keys and tr.read_state()["step"] == 25
+    with pytest.raises(RuntimeError, match="prepare"):
+        tr.train_steps(1, M=64)
+
+
+@pytest.mark.parametrize("s,image,graphs,mb", [(2, 28, 1, "none"), (4, 28, 1, "0.25"), (2, 128, 1, "2"),
+                                               (4, 128, 0, "none")])
+def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb):
+    from multidisttorch_amd.launch import launch
+
+    env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2"}
+    rc, outs = launch([sys.executable, os.path.join(HERE, "conv_ddp_worker.py"), str(image), str(graphs), mb], s,
+                      emulate="torchrun", timeout=150, extra_env=env, capture=True)
+    text = "\n".join(o or "" for o in outs)
+    assert rc == 0, text[-4000:]
+    res = [json.loads(l[7:]) for l in text.splitlines() if l.startswith("RESULT ")]
+    assert len(res) == s, text[-4000:]
+    for r in res:
+        for ph in ("same_eps", "indep_eps"):
+            assert r[ph]["status"] == 0 and r[ph]["finite"], (ph, r)
+            assert all(r[ph]["same"]), (ph, r)  # replicas bitwise identical at every check
+    r0 = [r for r in res if r["rank"] == 0][0]
+    sg = r0["single"]
+    assert sg["max_param_diff"] <= 1e-5 * max(1.0, sg["param_scale"]), sg
+    np.testing.assert_allclose(r0["same_eps"]["loss"], sg["loss"], rtol=1e-5)
+    # independent eps: per-replica losses differ (different samples of z)
+    losses = [tuple(r["indep_eps"]["loss"]) for r in res]
+    assert len(set(losses)) == s

@@ -110,6 +110,7 @@ def test_mlp_trainer_with_rccl_reducer(nccl_world, native_ext):
 def test_trial_groups_split_from_device_bound_world(nccl_world, native_ext):
     """Eager device-bound world -> trial communicators via ncclCommSplit; the
     direct-RCCL reducer then runs on the split communicator."""
+    from multidisttorch_amd.parallel import ddp
     from multidisttorch_amd.parallel.ddp import make_arena_reducer
     from multidisttorch_amd.parallel.groups import setup_ddp_groups
     from multidisttorch_amd.runtime.bootstrap import world_is_device_bound
@@ -117,9 +118,13 @@ def test_trial_groups_split_from_device_bound_world(nccl_world, native_ext):
     assert world_is_device_bound()
     (pg,) = setup_ddp_groups(1, verbose=False)
     assert dist.get_rank(pg) == 0
+    assert pg.bound_device_id is not None
     flat = torch.randn(4096, device="cuda")
     ref = flat.clone()
+    warm = ddp.COMM_WARMUPS[0]
     red = make_arena_reducer(pg, flat, [0, 1024, 4096])
+    # the split communicator exists already: no warm-up all-reduce was needed
+    assert ddp.COMM_WARMUPS[0] == warm
     red.launch_all()
     red.wait_all()
     torch.cuda.synchronize()

@@ -215,3 +215,46 @@ def test_bench_contract_multirank(tmp_path, n, k):
     assert out["config"]["trials"] == K and out["config"]["parallelism"] == f"groups{K}x{n // K}"
     assert out["config"]["valid"] is True
     assert abs(out["value"] - K * 64 * 2 / (out["ms_per_step"] * 2e-3)) / out["value"] < 0.01
+
+
+def test_vae_hpo_conv_ckpt_and_resume(tmp_path):
+    """--model conv --ckpt-dir then --resume (the conv checkpoint
+    path crashed on int(trainer.H) and silently failed the trial)."""
+    rc, outs = _vae_hpo(tmp_path, 2, "--model", "conv", "--epochs", "1", "--ngroups", "1", "--ckpt-dir", "ck",
+                        "--no-results")
+    text = "\n".join(outs)
+    assert rc == 0, text
+    assert "FAILED" not in text
+    assert (tmp_path / "ck" / "trial-0" / "epoch-1.pt").exists()
+    rc, outs = _vae_hpo(tmp_path, 2, "--model", "conv", "--epochs", "2", "--ngroups", "1", "--ckpt-dir", "ck",
+                        "--resume", "--no-results")
+    text = "\n".join(outs)
+    assert rc == 0, text
+    assert "FAILED" not in text
+    assert "resumed trial 0" in text and "Epoch: 2 Average" in text and "Epoch: 1 Average" not in text
+    ck = torch.load(str(tmp_path / "ck" / "trial-0" / "epoch-2.pt"), weights_only=True)
+    assert ck["progress"]["epoch"] == 2 and ck["arch"]["kind"] == "conv"
+    agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
+    assert agg["failed_trials"] == []
+
+
+def test_failure_inside_multi_rank_group(tmp_path):
+    """Group of 2 + a rank-specific mid-epoch fault (isolation only
+    held for single-rank groups). Rank 1 stops issuing steps at step 3 while
+    its peer is inside the step-3 all-reduce: the peer times out, both members
+    agree the trial failed, the other trial finishes, everyone exits 0."""
+    old = dict(ENV)
+    ENV["MDT_FAULT"] = "rank=3,step=3"
+    ENV["MDT_GROUP_TIMEOUT_S"] = "8"
+    try:
+        rc, outs = _vae_hpo(tmp_path, 4, "--epochs", "1", "--ngroups", "2", "--no-results")
+    finally:
+        ENV.clear()
+        ENV.update(old)
+    text = "\n".join(outs)
+    assert rc == 0, text
+    assert "trial 1 (world rank 3) FAILED: InjectedFault" in text
+    assert "trial 1 (world rank 2) FAILED" in text
+    assert re.search(r"^\[0:0\] ====> Test set loss", text, re.M)
+    agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
+    assert agg["failed_trials"] == [1] and agg["trials"] == 2

@@ -58,3 +58,23 @@ def test_master_discovery():
 def test_discover_launcher_name():
     assert E.discover({"SLURM_NPROCS": "2", "SLURM_PROCID": "1"}).launcher == "slurm"
     assert E.discover({}).launcher == "single"
+
+
+def test_eager_device_bound_world_default(monkeypatch):
+    """One GPU per local rank -> eager device-bound RCCL world by default
+    (trial groups then come from ncclCommSplit); shared or unknown -> lazy."""
+    from multidisttorch_amd.runtime import env as E
+    from multidisttorch_amd.runtime.bootstrap import eager_comm_requested
+
+    monkeypatch.delenv("MDT_EAGER_COMM", raising=False)
+    info = E.discover({"WORLD_SIZE": "8", "RANK": "3", "LOCAL_RANK": "3", "LOCAL_WORLD_SIZE": "8"}, ndev=8)
+    assert info.local_size == 8 and eager_comm_requested(info, 8)
+    assert not eager_comm_requested(info, 1)  # 8 ranks sharing one visible GPU
+    info2 = E.discover({"SLURM_NPROCS": "4", "SLURM_PROCID": "1"}, ndev=8)
+    assert info2.local_size is None and not eager_comm_requested(info2, 8)
+    assert E.discover({"OMPI_COMM_WORLD_SIZE": "2", "OMPI_COMM_WORLD_RANK": "0",
+                       "OMPI_COMM_WORLD_LOCAL_SIZE": "2"}).local_size == 2
+    monkeypatch.setenv("MDT_EAGER_COMM", "0")
+    assert not eager_comm_requested(info, 8)
+    monkeypatch.setenv("MDT_EAGER_COMM", "1")
+    assert eager_comm_requested(info2, 8)

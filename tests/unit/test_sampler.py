@@ -29,3 +29,21 @@ def test_epoch_order_fixed_without_set_epoch():
     assert torch.equal(ix(0), ix(5))
     ix2 = EpochIndexer(1000, 2, 1, set_epoch=True)
     assert not torch.equal(ix2(0), ix2(1))
+
+
+@pytest.mark.parametrize("w,k", [(3, 2), (7, 3), (8, 3), (5, 2), (8, 8), (8, 2)])
+def test_reference_num_replicas_and_shards(w, k):
+    """num_replicas = W // (W // K), as /root/reference/vae-hpo.py:146 computes
+    it (world_size // local_size) -- not K when W % K leaves idle ranks."""
+    from multidisttorch_amd.data.sampler import reference_num_replicas
+
+    n = w // k
+    nrep = reference_num_replicas(w, n)
+    assert nrep == w // n
+    if (w, k) == (3, 2):
+        assert nrep == 3  # differs from K = 2
+    if (w, k) == (7, 3):
+        assert nrep == 3
+    for g in range(k):  # every trial group's shard is DistributedSampler(rank=g, num_replicas=W//n)
+        ref = list(DistributedSampler(_DS(60000), num_replicas=w // n, rank=g))
+        assert shard_indices(60000, nrep, g).tolist() == ref

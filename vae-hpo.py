@@ -29,6 +29,7 @@ from multidisttorch_amd.hpo.runner import RunOptions, idle_rank, run_packed_tria
 from multidisttorch_amd.hpo.trial import build_specs, parse_list
 from multidisttorch_amd.parallel.autotune import parse_bucket_mb
 from multidisttorch_amd.runtime.bootstrap import control_group
+from multidisttorch_amd.runtime.faults import create_health_groups
 
 
 def parse_args(argv=None):
@@ -53,6 +54,9 @@ def parse_args(argv=None):
     parser.add_argument("--graph-steps", type=int, default=10)
     parser.add_argument("--backend", type=str, default=None, choices=[None, "hip", "torch"])
     parser.add_argument("--real-data", action="store_true", help="require MNIST IDX files under --data-dir")
+    parser.add_argument("--synthetic", action="store_true",
+                        help="always use the synthetic MNIST-shaped set (default: IDX files under --data-dir "
+                             "or data-dir/MNIST/raw when present, synthetic otherwise)")
     parser.add_argument("--data-dir", type=str, default="data")
     parser.add_argument("--train-samples", type=int, default=None)
     parser.add_argument("--test-samples", type=int, default=None)
@@ -90,6 +94,7 @@ def main(argv=None):
     comm_size, rank = setup_ddp()
     processes_groups = setup_ddp_groups(ngroups)
     control_group()  # world collective: create the gloo control plane on every rank
+    create_health_groups(ngroups)  # world collective: per-trial gloo health agreement (faults.py)
 
     T = max(1, args.trials_per_group)
     specs = build_specs(ngroups * T, args.epochs, parse_list(args.lr), parse_list(args.beta), args.seed,
@@ -99,7 +104,8 @@ def main(argv=None):
                       ckpt_dir=args.ckpt_dir, resume=args.resume, metrics_dir=args.metrics_dir,
                       results=not args.no_results, per_group_results=args.per_group_results,
                       train_samples=args.train_samples, test_samples=args.test_samples,
-                      data_dir=args.data_dir, synthetic=False if args.real_data else True,
+                      data_dir=args.data_dir,
+                      synthetic=False if args.real_data else (True if args.synthetic else None),
                       model=args.model, image_size=args.image_size, bucket_mb=parse_bucket_mb(args.bucket_mb),
                       profile=args.profile)
     results = []
@@ -108,7 +114,7 @@ def main(argv=None):
         if dist.get_rank(group) >= 0:
             member = True
             if T == 1:
-                results.append(run_trial(specs[group_id], group, opts, num_trials=ngroups))
+                results.append(run_trial(specs[group_id], group, opts))
             else:
                 results.extend(run_packed_trials(specs[group_id * T:(group_id + 1) * T], group, opts,
                                                  num_trials=ngroups * T))
