@@ -1,0 +1,889 @@
+// Per-sample fused 28x28 conv-VAE training step for MI355X (gfx950).
+//
+// Why a different decomposition than conv_igemm.hip's layer-by-layer GEMMs:
+// at 28x28 every layer is tiny (M <= 25k rows, K <= 3136, N <= 3136) and a
+// layer-per-launch step is a chain of ~15 dependent launches that each pay a
+// kernel boundary (~1.3 us), a cold first load from another XCD's writes and a
+// short k-loop whose iterations are load-latency bound -- ~116 us per step at
+// B = 128 for 2.8 GFLOP (profiles/r2_bench). A conv-VAE's forward and its
+// backward-data chain, however, never mix samples: every layer of sample n
+// reads only sample n. So one workgroup per sample runs the WHOLE chain with
+// the activations resident in LDS (<= 25 KB per sample), and only the weight
+// gradients (a reduction over the batch) and the optimizer need the batch:
+//
+//   launch 1  f28_fwd_k   (B workgroups): batch gather -> enc1 -> enc2 -> head
+//             -> reparam (Philox) + KLD -> dec_fc -> dec1 -> dec2 -> BCE, dlogits
+//   launch 2  f28_bwd_k   (B workgroups): dec2 / dec1 / dec_fc backward-data,
+//             reparam backward, head / enc2 backward-data, ReLU masks, per-sample
+//             bias-gradient partials
+//   launch 3  jobs_multi_k: the six weight-gradient GEMMs (m-split partial
+//             slabs, conv_igemm_dev.h bodies) + loss reduction / step advance
+//   launch 4  grad_finalize_k: slab reduction + Adam + bf16 re-cast
+//
+// Inside a workgroup (512 threads = 8 waves, one sample) the convolutions run
+// on v_mfma_f32_16x16x32_bf16 with the A operand gathered straight out of the
+// LDS activation image (implicit im2col) and the B operand either streamed
+// from L2 into registers (conv-layout weights, k contiguous) or read with
+// ds_read_b64_tr_b16 from per-tap LDS images (transposed-conv weights), so no
+// transposed weight copies exist. The Linear layers stream their bf16 weights
+// (head 400 KB, dec_fc 200 KB) from L2 with up to 16 loads in flight per lane;
+// that weight stream, not arithmetic, bounds each fused launch.
+//
+// Numerics: f32 accumulation, bf16 activations (same rounding points as the
+// layer-by-layer path), f32 loss / dlogits / mu / logvar / eps; Philox keyed
+// exactly like combine_reparam (element n*Z+c, stream, step) so the torch
+// reference (ops/philox.py) reproduces eps.
+#include "conv_igemm_dev.h"
+#include "conv_small.h"
+#include "vae_mlp.h"
+
+namespace mdt {
+namespace f28 {
+
+constexpr int kThreads = 512;
+constexpr int kFlat = 3136;  // 7 * 7 * 64
+
+struct Weights {
+  const float* W1f;   // enc1 f32 master [32][4][4][1]
+  const float* b1;
+  const __bf16* W2;   // enc2 [64][4][4][32]
+  const float* b2;
+  const __bf16* Wh;   // enc_head [64][3136]
+  const float* bh;
+  const __bf16* Wd;   // dec_fc [3136][32]
+  const float* bd;
+  const __bf16* W3;   // dec1 (convT) [64][4][4][32]
+  const float* b3;
+  const float* W4f;   // dec2 (convT) f32 master [32][4][4][1]
+  const float* b4;
+};
+
+struct FwdArgs {
+  Weights w;
+  const float* X;        // dataset [N][784]
+  const int* idx;        // epoch index list
+  const TrainState* st;  // train or eval state (cursor, step)
+  const HParams* hp;
+  int B;
+  uint32_t stream;
+  int train;             // write the backward's inputs (activations, dlogits)
+  float* xb;             // [M][784] gathered batch
+  __bf16* a1;            // [M][196][32]
+  __bf16* a2;            // [M][3136]
+  float* mulv;           // [M][64]
+  float* eps;            // [M][32]
+  __bf16* z16;           // [M][32]
+  __bf16* d0;            // [M][3136]
+  __bf16* d1;            // [M][196][32]
+  float* dlog;           // [M][784]
+  float* recon;          // optional sigmoid [M][784]
+  float* bce_part;       // [M]
+  float* kld_part;       // [M]
+  float* db4_part;       // [M] (dec2 bias gradient partials)
+  unsigned long long* stamps;  // optional [M][16] s_memrealtime at phase ends (profiling)
+};
+
+struct BwdArgs {
+  Weights w;
+  const HParams* hp;
+  const float* mulv;
+  const float* eps;
+  const __bf16* a1;
+  const __bf16* a2;
+  const __bf16* d0;
+  const __bf16* d1;
+  const float* dlog;
+  __bf16* gd1;       // [M][196][32] masked grad of dec1's output
+  __bf16* gd0;       // [M][3136]    masked grad of dec_fc's output
+  float* dbd_part;   // [M][3136]    dec_fc bias partials (f32 of gd0)
+  float* dmulv;      // [M][64]      d[mu|logvar] (also the head-bias partials)
+  __bf16* dmulv16;   // [M][64]
+  __bf16* ga2;       // [M][3136]    masked grad of enc2's output
+  __bf16* ga1;       // [M][196][32] masked grad of enc1's output
+  float* db3_part;   // [M][32]
+  float* db2_part;   // [M][64]
+  float* db1_part;   // [M][32]
+  unsigned long long* stamps;  // optional [M][16] phase-end timestamps
+};
+
+// 14x14x32 bf16 LDS image, 64-B pixel rows: 16-B chunk ch of pixel p at slot
+// ch ^ ((p >> 1) & 3) -- the stride-2 im2col gathers of 16 lanes then spread
+// over all four chunk slots of a bank row instead of hitting one.
+// Phase timestamp (100 MHz s_memrealtime) of workgroup blockIdx.x, slot k.
+__device__ __forceinline__ void stamp(unsigned long long* st, int k) {
+  if (st && threadIdx.x == 0) st[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ int img14(int pix, int ch) { return (pix << 6) + ((ch ^ ((pix >> 1) & 3)) << 4); }
+
+// Per-tap images of a [64][16][32] bf16 weight (rows c64 = reduction index,
+// 32 columns) are laid out for tr_frag<32> reads: 16 images of 4 KB
+// (TapImageRegs below fills them).
+
+// Weight stream with double buffering: items 0 .. CH*NCH-1, CH 16-B loads per
+// lane in flight while the previous CH are consumed. ld(i) must tolerate i past
+// the end (clamp the address), use(i, v) must skip it. The outer loop is not
+// unrolled so at most 2*CH fragments are live.
+template <int CH, int NCH, class Load, class Use>
+__device__ __forceinline__ void stream2(Load ld, Use use) {
+  bf16x8 bc[CH], bn[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) bc[i] = ld(i);
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+    if (c + 1 < NCH) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) bn[i] = ld((c + 1) * CH + i);
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) use(c * CH + i, bc[i]);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) bc[i] = bn[i];
+  }
+}
+
+// Conv-layout [64][16][32] bf16 weight staged in LDS: row co = 1 KB, 16-B
+// chunk (tap, ch) of row co at slot (tap*4 + ch) ^ (co & 15), so the 16 rows a
+// B-fragment read touches land on 16 different bank groups.
+__device__ __forceinline__ int cimg(int co, int tap, int ch) { return (co << 10) + (((tap * 4 + ch) ^ (co & 15)) << 4); }
+
+__device__ __forceinline__ void stage_conv_image(const __bf16* W, uint8_t* img) {
+  for (int q = threadIdx.x; q < 4096; q += kThreads) {
+    const int co = q >> 6, tap = (q >> 2) & 15, ch = q & 3;
+    *reinterpret_cast<bf16x8*>(img + cimg(co, tap, ch)) = *reinterpret_cast<const bf16x8*>(W + q * 8);
+  }
+}
+
+// B fragment of n-tile j, k-step (tap) t: lane holds W[16j + (l & 15)][t][8(l >> 4) ..]
+__device__ __forceinline__ bf16x8 conv_bfrag(const uint8_t* img, int j, int t, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + cimg(16 * j + (lane & 15), t, lane >> 4));
+}
+
+// Per-tap image loads held in registers across phases (8 chunks per thread),
+// then written: the LDS-staged weight of a LATER phase streams in while the
+// phases in between run.
+struct TapImageRegs {
+  bf16x8 v[8];
+  __device__ __forceinline__ void load(const __bf16* W) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const bf16x8*>(W + (threadIdx.x + i * kThreads) * 8);
+  }
+  __device__ __forceinline__ void store(uint8_t* img) const {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = threadIdx.x + i * kThreads;
+      const int c64 = q >> 6, tap = (q >> 2) & 15, ch = q & 3;
+      *reinterpret_cast<bf16x8*>(img + tap * 4096 + timg<32>(c64, ch)) = v[i];
+    }
+  }
+};
+
+// Stride-2 4x4 conv 14x14x32 -> 7x7x64 (+ per-element epilogue) of one sample:
+// GEMM rows = 49 output pixels (4 m-tiles), cols = 64 (4 n-tiles), k = 16 taps
+// x 32 channels. Wave w owns n-tile w & 3 and m-tiles (w >> 2) and (w >> 2) + 2.
+// pre(p, col) is evaluated for every output element BEFORE the MFMA loop (its
+// global loads -- bias, ReLU mask -- overlap the loop instead of stalling the
+// epilogue); epi(p, col, acc, pre_value).
+template <class BFrag, class Pre, class Epi>
+__device__ __forceinline__ void conv14to7(const uint8_t* in_img, BFrag bfrag, Pre pre, Epi epi) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = w & 3;
+  float pv[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int p = ((w >> 2) + 2 * q) * 16 + 4 * (lane >> 4) + rr;
+      pv[q][rr] = p < 49 ? pre(p, 16 * j + (lane & 15)) : 0.f;
+    }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int mt = (w >> 2) + 2 * q;
+    const int r = mt * 16 + (lane & 15);
+    const int oy = r / 7, ox = r - 7 * (r / 7);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
+      const bool ok = r < 49 && (unsigned)iy < 14u && (unsigned)ix < 14u;
+      const bf16x8 a = ok ? *reinterpret_cast<const bf16x8*>(in_img + img14(iy * 14 + ix, lane >> 4)) : zero8();
+      acc = mfma_bf16(a, bfrag(j, t), acc);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int p = mt * 16 + 4 * (lane >> 4) + rr;
+      if (p < 49) epi(p, 16 * j + (lane & 15), acc[rr], pv[q][rr]);
+    }
+  }
+}
+
+// Stride-2 4x4 transposed conv 7x7x64 -> 14x14x32 of one sample, as four
+// stride-parity classes (a, b) = (oy & 1, ox & 1) without zero-insertion taps:
+// class rows = 49 pixels (jy, jx) with (oy, ox) = (2jy + a, 2jx + b), k = 2x2
+// taps (ky = 1 - a + 2ty, iy = jy + a - ty) x 64 channels, cols = 32. A from the
+// [49][64] LDS image `in`, B via tr_frag from the per-tap images `wimg`.
+// 32 items (class, m-tile, n-tile), four per wave. `cs` (optional) receives
+// the per-column sums of the epilogue values of this wave's items.
+template <class Pre, class Epi>
+__device__ __forceinline__ void tconv7to14(const __bf16* in, const uint8_t* wimg, Pre pre, Epi epi, float (&cs)[2]) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  cs[0] = cs[1] = 0.f;
+  // items it = w + 8q: class q, m-tile (w >> 1) & 3, n-tile w & 1 (fixed per wave)
+  const int mt = (w >> 1) & 3, nj = w & 1;
+  float pv[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r2 = mt * 16 + 4 * (lane >> 4) + rr;
+      const int jy2 = r2 / 7, jx2 = r2 - 7 * (r2 / 7);
+      pv[q][rr] = r2 < 49 ? pre((2 * jy2 + (q >> 1)) * 14 + 2 * jx2 + (q & 1), 16 * nj + (lane & 15)) : 0.f;
+    }
+#pragma unroll 2
+  for (int q = 0; q < 4; ++q) {
+    const int a = q >> 1, b = q & 1;
+    const int r = mt * 16 + (lane & 15);
+    const int jy = r / 7, jx = r - 7 * (r / 7);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int ty = ks >> 2, tx = (ks >> 1) & 1, hh = ks & 1;
+      const int iy = jy + a - ty, ix = jx + b - tx;
+      const bool ok = r < 49 && (unsigned)iy < 7u && (unsigned)ix < 7u;
+      const bf16x8 av =
+          ok ? *reinterpret_cast<const bf16x8*>(in + (iy * 7 + ix) * 64 + 32 * hh + 8 * (lane >> 4)) : zero8();
+      const int tap = ((1 - a) + 2 * ty) * 4 + (1 - b) + 2 * tx;
+      const bf16x8 bv = tr_frag<32>(wimg + tap * 4096, 16 * nj, 32 * hh, lane);
+      acc = mfma_bf16(av, bv, acc);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r2 = mt * 16 + 4 * (lane >> 4) + rr;
+      if (r2 < 49) {
+        const int jy2 = r2 / 7, jx2 = r2 - 7 * (r2 / 7);
+        s += epi((2 * jy2 + a) * 14 + 2 * jx2 + b, 16 * nj + (lane & 15), acc[rr], pv[q][rr]);
+      }
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    cs[nj] += s;
+  }
+}
+
+// ------------------------------------------------------------------ forward
+// LDS map (bytes)
+constexpr int kFX = 0;                      // f32 [784] input image
+constexpr int kFW1 = kFX + 784 * 4;         // f32 [16][32] enc1 weights, tap-major
+constexpr int kFW4 = kFW1 + 512 * 4;        // f32 [16][32] dec2 weights, tap-major
+constexpr int kFA1 = kFW4 + 512 * 4;        // bf16 img14 [196][32] (enc1 out, later dec1 out)
+constexpr int kFA2 = kFA1 + 196 * 64;       // bf16 [3136] enc2 out (NHWC flatten)
+constexpr int kFD0 = kFA2 + kFlat * 2;      // bf16 [3136] dec_fc out
+constexpr int kFH = kFD0 + kFlat * 2;       // f32 [64] head out
+constexpr int kFZ = kFH + 64 * 4;           // bf16 [32] z
+constexpr int kFRed = kFZ + 64;             // f32 [4][16] head k-half partials
+constexpr int kFScr = kFRed + 64 * 4;       // f32 [32] block-sum scratch
+constexpr int kFW3 = kFScr + 32 * 4;        // 16 x 4 KB dec1 tap images
+constexpr int kFDummy = kFW3 + 65536;       // 8 x 1 KB landing zone of the L2 prefetch DMAs
+constexpr int kFBd = kFDummy + 8192;        // f32 [3136] dec_fc bias
+constexpr int kFLds = kFBd + kFlat * 4;
+static_assert(kFA1 % 16 == 0 && kFA2 % 16 == 0 && kFD0 % 16 == 0 && kFW3 % 16 == 0, "LDS alignment");
+
+__global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kFLds];
+  float* Xs = reinterpret_cast<float*>(lds + kFX);
+  float* W1s = reinterpret_cast<float*>(lds + kFW1);
+  float* W4s = reinterpret_cast<float*>(lds + kFW4);
+  uint8_t* A1s = lds + kFA1;
+  __bf16* A2s = reinterpret_cast<__bf16*>(lds + kFA2);
+  __bf16* D0s = reinterpret_cast<__bf16*>(lds + kFD0);
+  float* Hs = reinterpret_cast<float*>(lds + kFH);
+  __bf16* Zs = reinterpret_cast<__bf16*>(lds + kFZ);
+  float* Red = reinterpret_cast<float*>(lds + kFRed);
+  float* Scr = reinterpret_cast<float*>(lds + kFScr);
+  uint8_t* W3s = lds + kFW3;
+  __bf16* D1s = reinterpret_cast<__bf16*>(lds + kFA1);  // aliases A1s (dead after enc2)
+
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Weights& W = a.w;
+  stamp(a.stamps, 0);
+
+  // ---- P0: L2 prefetch of the Linear weights, batch row gather, small
+  // weights, dec1 tap images, enc2 B fragments.
+  // The head (400 KB) and dec_fc (200 KB) weights were just rewritten by the
+  // optimizer on other XCDs, so P3 / P5 would stream them from the Infinity
+  // Cache at ~2 us per round trip. The 16 workgroups that share an XCD (block
+  // ids b, b+8, ...: round-robin dispatch; a wrong guess costs speed only)
+  // each pull one 1/16 slice into that XCD's L2 now, through LDS-DMA loads
+  // into a scratch LDS zone (nothing reads it), during P0-P2.
+  {
+    constexpr int kWh = kFlat * 64 * 2, kWd = kFlat * 32 * 2, kSlice = (kWh + kWd) / 16;
+    const int r = (n >> 3) & 15;
+    for (int k = w; k * 1024 < kSlice; k += 8) {
+      const int off = r * kSlice + k * 1024 + lane * 16;
+      const uint8_t* src = off < kWh ? reinterpret_cast<const uint8_t*>(W.Wh) + off
+                                     : reinterpret_cast<const uint8_t*>(W.Wd) + (off - kWh < kWd ? off - kWh : 0);
+      glds16(src, lds + kFDummy + w * 1024);
+    }
+  }
+  {
+    const int row = a.idx[(size_t)a.st->cursor * a.B + n];
+    const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)row * 784);
+    if (tid < 196) {
+      const float4 v = src[tid];
+      reinterpret_cast<float4*>(Xs)[tid] = v;
+      if (a.train) reinterpret_cast<float4*>(a.xb + (size_t)n * 784)[tid] = v;
+    }
+    const int c = tid >> 4, t = tid & 15;  // 512 threads = 32 channels x 16 taps
+    W1s[t * 32 + c] = W.W1f[tid];
+    W4s[t * 32 + c] = W.W4f[tid];
+    for (int e = tid; e < kFlat / 4; e += kThreads)
+      reinterpret_cast<float4*>(lds + kFBd)[e] = reinterpret_cast<const float4*>(W.bd)[e];
+  }
+  stage_conv_image(W.W2, W3s);  // enc2 weights first; dec1's tap images replace them after P2
+  __syncthreads();
+
+  stamp(a.stamps, 1);
+  // ---- P1: enc1 (1 -> 32, 28x28 -> 14x14, VALU), ReLU
+  if (tid < 196) {
+    const int oy = tid / 14, ox = tid - 14 * (tid / 14);
+    float acc[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) acc[c] = W.b1[c];
+#pragma unroll 2
+    for (int t = 0; t < 16; ++t) {
+      const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
+      const bool ok = (unsigned)iy < 28u && (unsigned)ix < 28u;
+      const float x = ok ? Xs[iy * 28 + ix] : 0.f;
+#pragma unroll
+      for (int c4 = 0; c4 < 8; ++c4) {
+        const float4 wv = reinterpret_cast<const float4*>(W1s + t * 32)[c4];
+        acc[4 * c4 + 0] = fmaf(x, wv.x, acc[4 * c4 + 0]);
+        acc[4 * c4 + 1] = fmaf(x, wv.y, acc[4 * c4 + 1]);
+        acc[4 * c4 + 2] = fmaf(x, wv.z, acc[4 * c4 + 2]);
+        acc[4 * c4 + 3] = fmaf(x, wv.w, acc[4 * c4 + 3]);
+      }
+    }
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch) {
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (__bf16)fmaxf(acc[8 * ch + e], 0.f);
+      *reinterpret_cast<bf16x8*>(A1s + img14(tid, ch)) = o;
+      if (a.train) *reinterpret_cast<bf16x8*>(a.a1 + ((size_t)n * 196 + tid) * 32 + 8 * ch) = o;
+    }
+  }
+  __syncthreads();
+
+  stamp(a.stamps, 2);
+  // ---- P2: enc2 (32 -> 64, 14x14 -> 7x7, MFMA), ReLU
+  conv14to7(A1s, [&](int j, int t) { return conv_bfrag(W3s, j, t, lane); }, [&](int, int col) { return W.b2[col]; },
+            [&](int p, int col, float v, float bias) {
+    const __bf16 o = (__bf16)fmaxf(v + bias, 0.f);
+    A2s[p * 64 + col] = o;
+    if (a.train) a.a2[(size_t)n * kFlat + p * 64 + col] = o;
+  });
+  __syncthreads();
+
+  TapImageRegs w3r;
+  w3r.load(W.W3);  // dec1 tap images: in flight during P3-P5, written after P5
+  stamp(a.stamps, 3);
+  // ---- P3: encoder head (3136 -> 64) on VALU with fully contiguous weight
+  // loads. Wave w owns output rows o = w + 8c (c = 0..7); one row = 7 wave
+  // loads of 1 KB (lane l covers k = 512i + 8l .. +7). A 16-row MFMA fragment
+  // would touch 16 separate 64-B segments per load and the per-CU address
+  // path (TA), not bandwidth, bounded that version (12.5 us; PMC TA_BUSY).
+  // The next row's 7 loads are in flight while this row's dot products and
+  // cross-lane reduction run.
+  {
+    bf16x8 av[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int k = 512 * i + 8 * lane;
+      av[i] = k < kFlat ? *reinterpret_cast<const bf16x8*>(A2s + k) : zero8();
+    }
+    auto ld_row = [&](int o, bf16x8 (&v)[7]) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const int k = 512 * i + 8 * lane;
+        v[i] = *reinterpret_cast<const bf16x8*>(W.Wh + (size_t)o * kFlat + (k < kFlat ? k : 0));
+      }
+    };
+    bf16x8 vc[7], vn[7];
+    ld_row(w, vc);
+#pragma unroll 1
+    for (int c = 0; c < 8; ++c) {
+      if (c + 1 < 8) ld_row(w + 8 * (c + 1), vn);
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        if (512 * i + 8 * lane < kFlat) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d = fmaf((float)av[i][e], (float)vc[i][e], d);
+        }
+      }
+      d = wave_sum(d);
+      if (lane == 0) Hs[w + 8 * c] = d + W.bh[w + 8 * c];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) vc[i] = vn[i];
+    }
+  }
+  __syncthreads();
+
+  stamp(a.stamps, 4);
+  // ---- P4: reparameterisation (Philox eps) + KLD
+  if (tid < 64) {
+    float kl = 0.f;
+    if (tid < 32) {
+      const int c = tid;
+      const float mu = Hs[c], lv = Hs[32 + c];
+      const unsigned long long stp = (unsigned long long)a.st->step;
+      const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(n * 32 + c), a.stream, (uint32_t)(stp & 0xffffffffu),
+                                             (uint32_t)(stp >> 32)},
+                                       a.hp->seed_lo, a.hp->seed_hi);
+      const float ep = normal_from_bits(bits.x, bits.y);
+      const float sd = expf(0.5f * lv);
+      const float zz = mu + ep * sd;
+      kl = 1.f + lv - mu * mu - sd * sd;
+      Zs[c] = (__bf16)zz;
+      if (a.train) {
+        a.mulv[(size_t)n * 64 + c] = mu;
+        a.mulv[(size_t)n * 64 + 32 + c] = lv;
+        a.eps[(size_t)n * 32 + c] = ep;
+        a.z16[(size_t)n * 32 + c] = (__bf16)zz;
+      }
+    }
+    kl = wave_sum(kl);
+    if (tid == 0) Scr[0] = -0.5f * kl;
+  }
+  __syncthreads();
+
+  stamp(a.stamps, 5);
+  // ---- P5: dec_fc (32 -> 3136, MFMA K = 32), ReLU. Wave w: n-tiles w + 8i.
+  {
+    const bf16x8 av = (lane & 15) == 0 ? *reinterpret_cast<const bf16x8*>(Zs + 8 * (lane >> 4)) : zero8();
+    const __bf16* wp = W.Wd + (size_t)(lane & 15) * 32 + 8 * (lane >> 4);
+    // n-tiles t = w + 8i (i < 25, t < 196): 2 chunks of 13 loads
+    stream2<13, 2>(
+        [&](int i) {
+          const int t = w + 8 * i;
+          return *reinterpret_cast<const bf16x8*>(wp + (size_t)(t < 196 ? t : 0) * 512);
+        },
+        [&](int i, const bf16x8& b) {
+          const int t = w + 8 * i;
+          if (t < 196) {
+            const f32x4 acc = mfma_bf16(av, b, f32x4{0.f, 0.f, 0.f, 0.f});
+            if (lane < 16) {
+              const int jj = 16 * t + lane;
+              const __bf16 o = (__bf16)fmaxf(acc[0] + reinterpret_cast<const float*>(lds + kFBd)[jj], 0.f);
+              D0s[jj] = o;
+              if (a.train) a.d0[(size_t)n * kFlat + jj] = o;
+            }
+          }
+        });
+  }
+  w3r.store(W3s);
+  __syncthreads();
+
+  stamp(a.stamps, 6);
+  // ---- P6: dec1 (convT 64 -> 32, 7x7 -> 14x14, MFMA), ReLU
+  {
+    float cs[2];
+    tconv7to14(D0s, W3s, [&](int, int co) { return W.b3[co]; }, [&](int pix, int co, float v, float bias) {
+      const __bf16 o = (__bf16)fmaxf(v + bias, 0.f);
+      D1s[pix * 32 + co] = o;
+      if (a.train) a.d1[((size_t)n * 196 + pix) * 32 + co] = o;
+      return 0.f;
+    }, cs);
+  }
+  __syncthreads();
+
+  stamp(a.stamps, 7);
+  // ---- P7: dec2 (convT 32 -> 1, 14x14 -> 28x28, VALU) + BCE + dlogits
+  float loss = 0.f, gsum = 0.f;
+  for (int pix = tid; pix < 784; pix += kThreads) {
+    const int oy = pix / 28, ox = pix - 28 * (pix / 28);
+    const int ca = oy & 1, cb = ox & 1, jy = oy >> 1, jx = ox >> 1;
+    float t = W.b4[0];
+#pragma unroll 1
+    for (int ty = 0; ty < 2; ++ty)
+#pragma unroll
+      for (int tx = 0; tx < 2; ++tx) {
+        const int iy = jy + ca - ty, ix = jx + cb - tx;
+        if ((unsigned)iy < 14u && (unsigned)ix < 14u) {
+          const int tap = ((1 - ca) + 2 * ty) * 4 + (1 - cb) + 2 * tx;
+          const bf16x8* dp = reinterpret_cast<const bf16x8*>(D1s + (iy * 14 + ix) * 32);
+          const float4* wp = reinterpret_cast<const float4*>(W4s + tap * 32);
+#pragma unroll
+          for (int ch = 0; ch < 4; ++ch) {
+            const bf16x8 dv = dp[ch];
+            const float4 w0 = wp[2 * ch], w1 = wp[2 * ch + 1];
+            t = fmaf((float)dv[0], w0.x, t); t = fmaf((float)dv[1], w0.y, t);
+            t = fmaf((float)dv[2], w0.z, t); t = fmaf((float)dv[3], w0.w, t);
+            t = fmaf((float)dv[4], w1.x, t); t = fmaf((float)dv[5], w1.y, t);
+            t = fmaf((float)dv[6], w1.z, t); t = fmaf((float)dv[7], w1.w, t);
+          }
+        }
+      }
+    const float x = Xs[pix];
+    const float p = 1.f / (1.f + expf(-t));
+    const float g = p - x;
+    const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));
+    loss += x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
+    gsum += g;
+    if (a.train) a.dlog[(size_t)n * 784 + pix] = g;
+    if (a.recon) a.recon[(size_t)n * 784 + pix] = p;
+  }
+  loss = wave_sum(loss);
+  gsum = wave_sum(gsum);
+  if (lane == 0) {
+    Scr[8 + w] = loss;
+    Scr[16 + w] = gsum;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float sl = 0.f, sg = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sl += Scr[8 + i];
+      sg += Scr[16 + i];
+    }
+    a.bce_part[n] = sl;
+    a.kld_part[n] = Scr[0];
+    if (a.db4_part) a.db4_part[n] = sg;
+  }
+  stamp(a.stamps, 8);
+}
+
+// ----------------------------------------------------------------- backward
+constexpr int kBG = 0;                      // f32 [784] dlogits
+constexpr int kBW4 = kBG + 784 * 4;         // f32 [16][32] dec2 weights, tap-major
+constexpr int kBGD1 = kBW4 + 512 * 4;       // bf16 img14 [196][32]
+constexpr int kBGD0 = kBGD1 + 196 * 64;     // bf16 [3136]
+constexpr int kBDM = kBGD0 + kFlat * 2;     // f32 [64] d[mu|lv]
+constexpr int kBDZR = kBDM + 64 * 4;        // f32 [8][32] dz wave partials
+constexpr int kBGA2 = kBDZR + 256 * 4;      // bf16 [3136]
+constexpr int kBGA2F = kBGA2 + kFlat * 2;   // f32 [3136] (colsum source)
+constexpr int kBCS = kBGA2F + kFlat * 4;    // f32 [8][64] colsum scratch
+constexpr int kBW2 = kBCS + 512 * 4;        // 16 x 4 KB enc2 tap images
+constexpr int kBCSB = kBW2 + 65536;         // f32 [32][197] dec1-bias column-sum transpose
+constexpr int kBLds = kBCSB + 32 * 197 * 4;
+static_assert(kBGD1 % 16 == 0 && kBGD0 % 16 == 0 && kBGA2 % 16 == 0 && kBGA2F % 16 == 0 && kBW2 % 16 == 0,
+              "LDS alignment");
+
+__global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kBLds];
+  float* Gs = reinterpret_cast<float*>(lds + kBG);
+  float* W4s = reinterpret_cast<float*>(lds + kBW4);
+  uint8_t* GD1s = lds + kBGD1;
+  __bf16* GD0s = reinterpret_cast<__bf16*>(lds + kBGD0);
+  float* DMs = reinterpret_cast<float*>(lds + kBDM);
+  float* DZR = reinterpret_cast<float*>(lds + kBDZR);
+  __bf16* GA2s = reinterpret_cast<__bf16*>(lds + kBGA2);
+  float* GA2F = reinterpret_cast<float*>(lds + kBGA2F);
+  float* CS = reinterpret_cast<float*>(lds + kBCS);
+  uint8_t* W2s = lds + kBW2;
+  float* CSB = reinterpret_cast<float*>(lds + kBCSB);
+
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Weights& W = a.w;
+  stamp(a.stamps, 0);
+
+  // ---- Q0: dlogits, dec2 weights, dec1 B fragments (conv layout), enc2 tap images
+  if (tid < 196) reinterpret_cast<float4*>(Gs)[tid] = reinterpret_cast<const float4*>(a.dlog + (size_t)n * 784)[tid];
+  {
+    const int c = tid >> 4, t = tid & 15;
+    W4s[t * 32 + c] = W.W4f[tid];
+  }
+  stage_conv_image(W.W3, W2s);  // dec1 weights (conv layout) first; enc2's tap images after Q2
+  __syncthreads();
+
+  stamp(a.stamps, 1);
+  // ---- Q1: dec2 backward-data (conv 1 -> 32 on the dlogits, 28 -> 14) x dec1 ReLU mask
+  {
+    float acc[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) acc[c] = 0.f;
+    if (tid < 196) {
+      const int oy = tid / 14, ox = tid - 14 * (tid / 14);
+      // the dec1 ReLU mask, loaded before the FMAs so its latency overlaps them
+      bf16x8 mk[4];
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch) mk[ch] = reinterpret_cast<const bf16x8*>(a.d1 + ((size_t)n * 196 + tid) * 32)[ch];
+#pragma unroll 2
+      for (int t = 0; t < 16; ++t) {
+        const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
+        const bool ok = (unsigned)iy < 28u && (unsigned)ix < 28u;
+        const float g = ok ? Gs[iy * 28 + ix] : 0.f;
+#pragma unroll
+        for (int c4 = 0; c4 < 8; ++c4) {
+          const float4 wv = reinterpret_cast<const float4*>(W4s + t * 32)[c4];
+          acc[4 * c4 + 0] = fmaf(g, wv.x, acc[4 * c4 + 0]);
+          acc[4 * c4 + 1] = fmaf(g, wv.y, acc[4 * c4 + 1]);
+          acc[4 * c4 + 2] = fmaf(g, wv.z, acc[4 * c4 + 2]);
+          acc[4 * c4 + 3] = fmaf(g, wv.w, acc[4 * c4 + 3]);
+        }
+      }
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch) {
+        const bf16x8 m = mk[ch];
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = (float)m[e] > 0.f ? acc[8 * ch + e] : 0.f;
+          acc[8 * ch + e] = v;
+          o[e] = (__bf16)v;
+        }
+        *reinterpret_cast<bf16x8*>(GD1s + img14(tid, ch)) = o;
+        *reinterpret_cast<bf16x8*>(a.gd1 + ((size_t)n * 196 + tid) * 32 + 8 * ch) = o;
+      }
+    }
+    // dec1 bias partials: transpose the f32 values through LDS, then 8 lanes
+    // per channel sum strided pixels and combine in a fixed order (a wave_sum
+    // per channel was 192 dependent cross-lane steps per wave: ~5 us)
+    if (tid < 196) {
+#pragma unroll
+      for (int c = 0; c < 32; ++c) CSB[c * 197 + tid] = acc[c];
+    }
+  }
+  __syncthreads();
+  if (tid < 256) {
+    const int c = tid >> 3, part = tid & 7;
+    float s = 0.f;
+    for (int p = part; p < 196; p += 8) s += CSB[c * 197 + p];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (part == 0) a.db3_part[(size_t)n * 32 + c] = s;
+  }
+
+  stamp(a.stamps, 2);
+  // ---- Q2: dec1 backward-data (conv 32 -> 64 with the convT weights, 14 -> 7) x dec_fc ReLU mask
+  conv14to7(GD1s, [&](int j, int t) { return conv_bfrag(W2s, j, t, lane); },
+            [&](int p, int col) { return (float)a.d0[(size_t)n * kFlat + p * 64 + col]; },
+            [&](int p, int col, float v, float mask) {
+    const size_t e = (size_t)n * kFlat + p * 64 + col;
+    const float g = mask > 0.f ? v : 0.f;
+    const __bf16 o = (__bf16)g;
+    GD0s[p * 64 + col] = o;
+    a.gd0[e] = o;
+    a.dbd_part[e] = g;
+  });
+  __syncthreads();
+
+  TapImageRegs w2r;
+  w2r.load(W.W2);  // enc2 tap images: in flight during Q3-Q5, written before Q6
+  stamp(a.stamps, 3);
+  // ---- Q3: dec_fc backward-data dz = g . Wd (VALU over [3136][32] rows) ----
+  {
+    const int c8 = lane & 3, jr = lane >> 2;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    // 25 row groups of 128 (3136 rows): 2 chunks of 13 loads
+    stream2<13, 2>(
+        [&](int it) {
+          const int jj = it * 128 + w * 16 + jr;
+          return *reinterpret_cast<const bf16x8*>(W.Wd + (size_t)(jj < kFlat ? jj : 0) * 32 + 8 * c8);
+        },
+        [&](int it, const bf16x8& wv) {
+          const int jj = it * 128 + w * 16 + jr;
+          if (jj < kFlat) {
+            const float g = (float)GD0s[jj];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] = fmaf(g, (float)wv[e], acc[e]);
+          }
+        });
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = acc[e];
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      acc[e] = v;
+    }
+    if (lane < 4) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) DZR[w * 32 + 8 * lane + e] = acc[e];
+    }
+  }
+  __syncthreads();
+  stamp(a.stamps, 4);
+  // ---- Q4: reparameterisation backward -> d[mu | logvar]
+  if (tid < 32) {
+    const int c = tid;
+    float dz = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dz += DZR[i * 32 + c];
+    const float beta = a.hp->kl_beta;
+    const float mu = a.mulv[(size_t)n * 64 + c], lv = a.mulv[(size_t)n * 64 + 32 + c];
+    const float sd = expf(0.5f * lv);
+    const float dm = dz + beta * mu;
+    const float dl = 0.5f * dz * a.eps[(size_t)n * 32 + c] * sd + 0.5f * beta * (sd * sd - 1.f);
+    DMs[c] = dm;
+    DMs[32 + c] = dl;
+    a.dmulv[(size_t)n * 64 + c] = dm;
+    a.dmulv[(size_t)n * 64 + 32 + c] = dl;
+    a.dmulv16[(size_t)n * 64 + c] = (__bf16)dm;
+    a.dmulv16[(size_t)n * 64 + 32 + c] = (__bf16)dl;
+  }
+  __syncthreads();
+
+  stamp(a.stamps, 5);
+  // ---- Q5: head backward-data g = dmulv . Wh (VALU over 392 chunks of 8) x enc2 ReLU mask
+  if (tid < kFlat / 8) {
+    const int k0 = 8 * tid;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    // 64 weight rows: 4 chunks of 16 loads
+    stream2<16, 4>([&](int o) { return *reinterpret_cast<const bf16x8*>(W.Wh + (size_t)o * kFlat + k0); },
+                   [&](int o, const bf16x8& wv) {
+                     const float dm = DMs[o];
+#pragma unroll
+                     for (int e = 0; e < 8; ++e) acc[e] = fmaf(dm, (float)wv[e], acc[e]);
+                   });
+    const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.a2 + (size_t)n * kFlat + k0);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (float)mk[e] > 0.f ? acc[e] : 0.f;
+      o[e] = (__bf16)v;
+      GA2F[k0 + e] = v;
+    }
+    *reinterpret_cast<bf16x8*>(GA2s + k0) = o;
+    *reinterpret_cast<bf16x8*>(a.ga2 + (size_t)n * kFlat + k0) = o;
+  }
+  w2r.store(W2s);
+  __syncthreads();
+  if (tid < 64) {  // enc2 bias partials: sum over the 49 pixels in order
+    float s = 0.f;
+    for (int p = 0; p < 49; ++p) s += GA2F[p * 64 + tid];
+    a.db2_part[(size_t)n * 64 + tid] = s;
+  }
+
+  stamp(a.stamps, 6);
+  // ---- Q6: enc2 backward-data (convT 64 -> 32 with the conv weights, 7 -> 14) x enc1 ReLU mask
+  {
+    float cs[2];
+    tconv7to14(GA2s, W2s, [&](int pix, int co) { return (float)a.a1[((size_t)n * 196 + pix) * 32 + co]; },
+               [&](int pix, int co, float v, float mask) {
+      const size_t e = ((size_t)n * 196 + pix) * 32 + co;
+      const float g = mask > 0.f ? v : 0.f;
+      a.ga1[e] = (__bf16)g;
+      return g;
+    }, cs);
+    if (lane < 16) {
+      CS[w * 64 + lane] = cs[0];
+      CS[w * 64 + 16 + lane] = cs[1];
+    }
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += CS[i * 64 + tid];
+    a.db1_part[(size_t)n * 32 + tid] = s;
+  }
+  stamp(a.stamps, 7);
+}
+
+}  // namespace f28
+}  // namespace mdt
+
+using namespace mdt;
+
+namespace {
+
+template <class T>
+T* P(const long long* p, int i) {
+  return reinterpret_cast<T*>((intptr_t)p[i]);
+}
+
+void fill_weights(f28::Weights& w, const long long* p) {
+  w.W1f = P<const float>(p, 0);
+  w.b1 = P<const float>(p, 1);
+  w.W2 = P<const __bf16>(p, 2);
+  w.b2 = P<const float>(p, 3);
+  w.Wh = P<const __bf16>(p, 4);
+  w.bh = P<const float>(p, 5);
+  w.Wd = P<const __bf16>(p, 6);
+  w.bd = P<const float>(p, 7);
+  w.W3 = P<const __bf16>(p, 8);
+  w.b3 = P<const float>(p, 9);
+  w.W4f = P<const float>(p, 10);
+  w.b4 = P<const float>(p, 11);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Pointer tables (validated by the caller, csrc/runtime/conv_ops.cpp):
+// forward  [0..11] weights (W1f b1 W2 b2 Wh bh Wd bd W3 b3 W4f b4), 12 X, 13 idx,
+//          14 state, 15 hparams, 16 xb, 17 a1, 18 a2, 19 mulv, 20 eps, 21 z16,
+//          22 d0, 23 d1, 24 dlog, 25 recon, 26 bce_part, 27 kld_part, 28 db4_part,
+//          29 stamps (optional)
+// backward [0..11] weights, 12 hparams, 13 mulv, 14 eps, 15 a1, 16 a2, 17 d0,
+//          18 d1, 19 dlog, 20 gd1, 21 gd0, 22 dbd_part, 23 dmulv, 24 dmulv16,
+//          25 ga2, 26 ga1, 27 db3_part, 28 db2_part, 29 db1_part, 30 stamps (optional)
+int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train, hipStream_t s) {
+  if (M <= 0 || M > B) return 1;
+  f28::FwdArgs a{};
+  fill_weights(a.w, p);
+  a.X = P<const float>(p, 12);
+  a.idx = P<const int>(p, 13);
+  a.st = P<const TrainState>(p, 14);
+  a.hp = P<const HParams>(p, 15);
+  a.B = B;
+  a.stream = stream;
+  a.train = train;
+  a.xb = P<float>(p, 16);
+  a.a1 = P<__bf16>(p, 17);
+  a.a2 = P<__bf16>(p, 18);
+  a.mulv = P<float>(p, 19);
+  a.eps = P<float>(p, 20);
+  a.z16 = P<__bf16>(p, 21);
+  a.d0 = P<__bf16>(p, 22);
+  a.d1 = P<__bf16>(p, 23);
+  a.dlog = P<float>(p, 24);
+  a.recon = P<float>(p, 25);
+  a.bce_part = P<float>(p, 26);
+  a.kld_part = P<float>(p, 27);
+  a.db4_part = P<float>(p, 28);
+  a.stamps = P<unsigned long long>(p, 29);
+  hipLaunchKernelGGL(f28::f28_fwd_k, dim3(M), dim3(f28::kThreads), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int mdt_f28_backward(const long long* p, int M, hipStream_t s) {
+  if (M <= 0) return 1;
+  f28::BwdArgs a{};
+  fill_weights(a.w, p);
+  a.hp = P<const HParams>(p, 12);
+  a.mulv = P<const float>(p, 13);
+  a.eps = P<const float>(p, 14);
+  a.a1 = P<const __bf16>(p, 15);
+  a.a2 = P<const __bf16>(p, 16);
+  a.d0 = P<const __bf16>(p, 17);
+  a.d1 = P<const __bf16>(p, 18);
+  a.dlog = P<const float>(p, 19);
+  a.gd1 = P<__bf16>(p, 20);
+  a.gd0 = P<__bf16>(p, 21);
+  a.dbd_part = P<float>(p, 22);
+  a.dmulv = P<float>(p, 23);
+  a.dmulv16 = P<__bf16>(p, 24);
+  a.ga2 = P<__bf16>(p, 25);
+  a.ga1 = P<__bf16>(p, 26);
+  a.db3_part = P<float>(p, 27);
+  a.db2_part = P<float>(p, 28);
+  a.db1_part = P<float>(p, 29);
+  a.stamps = P<unsigned long long>(p, 30);
+  hipLaunchKernelGGL(f28::f28_bwd_k, dim3(M), dim3(f28::kThreads), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

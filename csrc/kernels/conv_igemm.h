@@ -120,6 +120,10 @@ enum JobKindBase : int {
   kJobCombine = 5002,
   kJobFinalize = 5003,
   kJobWtrans = 5004,
+  kJobLossStep = 5005,   // loss reduction + step advance (fused 28x28 step)
 };
+
+// Up to kMaxMultiJobs jobs of any kind of the multi-job kernel (jobs_multi_k).
+constexpr int kMaxMultiJobs = 8;
 
 }  // namespace mdt

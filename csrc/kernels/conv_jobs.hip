@@ -106,7 +106,82 @@ struct JWtrans {
   }
 };
 
+struct JLossStep {
+  static constexpr int ID = kJobLossStep, LDS = 64;
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int) {
+    loss_step_body(job_args<LossArgs>(j), reinterpret_cast<float*>(lds));
+  }
+};
+
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+// ------------------------------------------------------------ multi-job ----
+// Up to kMaxMultiJobs independent jobs of any supported kind in ONE launch,
+// dispatched per workgroup by a runtime switch (the fused 28x28 step's six
+// weight gradients + its loss/step job). Unlike jobs_k it needs no
+// instantiation per combination; its register allocation is the maximum over
+// the bodies, which is what those bodies use anyway.
+struct JobPackN {
+  JobBlob j[kMaxMultiJobs];
+  int start[kMaxMultiJobs + 1];
+  int n;
+};
+
+constexpr int kMultiLds = cmax(cmax(cmax(wgrad_lds_bytes<W0>(), wgrad_lds_bytes<W1>()),
+                                    cmax(wgrad_lds_bytes<W3>(), wgrad_lds_bytes<W4>())),
+                               cmax(cmax(wgrad_lds_bytes<W2>(), wgrad_lds_bytes<W5>()),
+                                    cmax(JFinalize::LDS, JColsum::LDS + 64)));
+
+template <int CFG, class TC>
+__device__ __forceinline__ bool run_wg_cfg(const JobBlob& j, uint8_t* lds, int b) {
+  if (j.kind == kJobWgrad + CFG) {
+    wgrad_body<__bf16, true, TC>(job_args<WgArgs>(j), lds, b, j.nblk);
+    return true;
+  }
+  if (j.kind == kJobWgradThin + CFG) {
+    wgrad_body<__bf16, false, TC>(job_args<WgArgs>(j), lds, b, j.nblk);
+    return true;
+  }
+  if (j.kind == kJobWgradThin + 20 + CFG) {
+    wgrad_body<float, false, TC>(job_args<WgArgs>(j), lds, b, j.nblk);
+    return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ void run_multi_job(const JobBlob& j, uint8_t* lds, int lb) {
+  if (run_wg_cfg<0, W0>(j, lds, lb) || run_wg_cfg<1, W1>(j, lds, lb) || run_wg_cfg<2, W2>(j, lds, lb) ||
+      run_wg_cfg<3, W3>(j, lds, lb) || run_wg_cfg<4, W4>(j, lds, lb) || run_wg_cfg<5, W5>(j, lds, lb))
+    return;
+  switch (j.kind) {
+    case kJobLossStep: JLossStep::run(j, lds, lb); break;
+    case kJobLoss: JLoss::run(j, lds, lb); break;
+    case kJobFinalize: JFinalize::run(j, lds, lb); break;
+    case kJobColsum: JColsum::run(j, lds, lb); break;
+    default: break;
+  }
+}
+
+// The job table lives in DEVICE memory (packed once per plan by the host,
+// static across graph replays): a runtime index into a kernel-argument struct
+// makes the compiler copy the whole 2.4 KB pack into per-lane scratch
+// (measured 2368 B/lane, the launch ~10x slower), and selecting it with
+// constant indices inlines every body eight times (1100+ SGPR spills).
+__global__ void __launch_bounds__(256) jobs_multi_k(const JobPackN* __restrict__ p) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kMultiLds];
+  const int b = blockIdx.x;
+  const int n = p->n;
+  int i = 0;
+  while (i + 1 < n && b >= p->start[i + 1]) ++i;
+  run_multi_job(p->j[i], lds, b - p->start[i]);
+}
+
+__host__ inline bool multi_kind_ok(int k) {
+  if (k >= kJobWgrad && k <= kJobWgrad + 5) return true;
+  if (k >= kJobWgradThin && k <= kJobWgradThin + 5) return true;
+  if (k >= kJobWgradThin + 20 && k <= kJobWgradThin + 25) return true;
+  return k == kJobLossStep || k == kJobLoss || k == kJobFinalize || k == kJobColsum;
+}
 
 template <class A, class B, class C>
 __global__ void __launch_bounds__(256) jobs_k(JobPack p) {
@@ -336,7 +411,9 @@ int mdt_job_colsum(JobBlob* j, const void* G16, int M, int N, int rows_per, floa
 int mdt_job_loss(JobBlob* j, const float* bce_part, int nb, const float* kld_part, int nk, void* st, const void* hp,
                  int advance_cursor) {
   memset(j, 0, sizeof(*j));
-  j->kind = kJobLoss;
+  // bit 0: advance the batch cursor; bit 1: also advance the step (loss_step_body)
+  j->kind = (advance_cursor & 2) ? kJobLossStep : kJobLoss;
+  advance_cursor &= 1;
   j->nblk = 1;
   put_args(j, LossArgs{bce_part, nb, kld_part, nk, reinterpret_cast<TrainState*>(st),
                        reinterpret_cast<const HParams*>(hp), advance_cursor});
@@ -410,6 +487,36 @@ int mdt_launch_tail(const JobBlob* wg, const JobBlob* fin0, const JobBlob* finr,
   if (wg->kind == WgT5f::ID) hipLaunchKernelGGL((tail_k<WgT5f>), dim3(grid), dim3(256), 0, s, p, ticket);
   else if (wg->kind == WgT5::ID) hipLaunchKernelGGL((tail_k<WgT5>), dim3(grid), dim3(256), 0, s, p, ticket);
   else return 1;
+  return (int)hipGetLastError() ? -1 : 0;
+}
+
+// Pack 1..kMaxMultiJobs jobs of any supported kinds into a JobPackN image at
+// `dst` (host memory, mdt_jobs_multi_bytes() bytes; the caller uploads it once).
+// Returns the grid size, 0 for an unsupported kind, -1 for bad input.
+int mdt_jobs_multi_bytes() { return (int)sizeof(JobPackN); }
+
+int mdt_pack_jobs_multi(const JobBlob* jobs, int n, void* dst) {
+  if (n < 1 || n > kMaxMultiJobs) return -1;
+  JobPackN p;
+  memset(&p, 0, sizeof(p));
+  int grid = 0;
+  for (int i = 0; i < n; ++i) {
+    if (jobs[i].nblk <= 0) return -1;
+    if (!multi_kind_ok(jobs[i].kind)) return 0;
+    p.j[i] = jobs[i];
+    p.start[i] = grid;
+    grid += jobs[i].nblk;
+  }
+  p.start[n] = grid;
+  p.n = n;
+  memcpy(dst, &p, sizeof(p));
+  return grid;
+}
+
+// ONE jobs_multi_k launch over a packed table already in device memory.
+int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s) {
+  if (!dev_pack || grid <= 0) return 2;
+  hipLaunchKernelGGL(jobs_multi_k, dim3(grid), dim3(256), 0, s, reinterpret_cast<const JobPackN*>(dev_pack));
   return (int)hipGetLastError() ? -1 : 0;
 }
 

@@ -41,6 +41,36 @@ __device__ __forceinline__ void loss_finalize_body(const LossArgs& la, float* sc
   }
 }
 
+// Loss reduction that also ADVANCES the step (the fused 28x28 step,
+// conv28_fused.hip): its forward reads `step` as the running step's RNG
+// counter, so the increment happens here, after the forward and backward
+// launches and before the finalize launch reads beta^t for Adam. Same state
+// layout and the same loss ring slot (step - 1 after the increment) as
+// loss_finalize_body after a step_begin.
+__device__ __forceinline__ void loss_step_body(const LossArgs& la, float* scratch) {
+  float sb = 0.f, sk = 0.f;
+  for (int i = threadIdx.x; i < la.nb; i += blockDim.x) sb += la.bce_part[i];
+  for (int i = threadIdx.x; i < la.nk; i += blockDim.x) sk += la.kld_part[i];
+  const float bce = block_sum(sb, scratch);
+  __syncthreads();
+  const float kld = block_sum(sk, scratch);
+  if (threadIdx.x == 0) {
+    TrainState* st = la.st;
+    st->step = st->step + 1;
+    st->b1pow *= la.hp->beta1_d;
+    st->b2pow *= la.hp->beta2_d;
+    const float loss = bce + la.hp->kl_beta * kld;
+    st->loss_hist[(st->step - 1) % kLossHist] = loss;
+    st->epoch_loss += (double)loss;
+    st->epoch_count += 1.0;
+    if (la.advance_cursor) {
+      int c = st->cursor + 1;
+      if (st->nbatches > 0 && c >= st->nbatches) c = 0;
+      st->cursor = c;
+    }
+  }
+}
+
 // Split-K combines fused with the reparameterisation (forward) and its
 // backward. A block owns cnt = 256/rp consecutive latent elements e = i*Z + c;
 // rp threads per element sum the interleaved k-slices z = r, r+rp, ... (loads

@@ -62,6 +62,11 @@ int mdt_job_colsum(mdt::JobBlob* j, const void* G16, int M, int N, int rows_per,
 int mdt_job_loss(mdt::JobBlob* j, const float* bce_part, int nb, const float* kld_part, int nk, void* st,
                  const void* hp, int advance_cursor);
 int mdt_launch_jobs(const mdt::JobBlob* jobs, int n, hipStream_t s);
+int mdt_jobs_multi_bytes();
+int mdt_pack_jobs_multi(const mdt::JobBlob* jobs, int n, void* dst);
+int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s);
+int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train, hipStream_t s);
+int mdt_f28_backward(const long long* p, int M, hipStream_t s);
 int mdt_launch_job1(const mdt::JobBlob* j, hipStream_t s);
 int mdt_launch_tail(const mdt::JobBlob* wg, const mdt::JobBlob* fin0, const mdt::JobBlob* finr, int* ticket,
                     hipStream_t s);
@@ -297,13 +302,15 @@ void bce_logits(const at::Tensor& logits, const at::Tensor& X, const c10::option
 }
 
 void loss_finalize2(const at::Tensor& bce_part, int64_t nb, const at::Tensor& kld_part, int64_t nk, at::Tensor state,
-                    const at::Tensor& hparams, bool advance_cursor, Job* job) {
+                    const at::Tensor& hparams, bool advance_cursor, Job* job, bool advance_step) {
+  TORCH_CHECK(bce_part.numel() >= nb && kld_part.numel() >= nk, "loss partials too small");
   if (job) {
     rc(mdt_job_loss(&job->main, bce_part.data_ptr<float>(), (int)nb, kld_part.data_ptr<float>(), (int)nk,
-                    state.data_ptr(), hparams.data_ptr(), advance_cursor ? 1 : 0),
+                    state.data_ptr(), hparams.data_ptr(), (advance_cursor ? 1 : 0) | (advance_step ? 2 : 0)),
        "job_loss");
     return;
   }
+  TORCH_CHECK(!advance_step, "loss_finalize2: advance_step needs a job (jobs_multi)");
   rc(mdt_conv_loss_finalize(bce_part.data_ptr<float>(), (int)nb, kld_part.data_ptr<float>(), (int)nk,
                             state.data_ptr(), hparams.data_ptr(), advance_cursor ? 1 : 0, cur()),
      "loss_finalize");
@@ -337,6 +344,113 @@ bool launch_jobs(const std::vector<Job*>& jobs) {
   for (auto* j : jobs)
     if (j->has_post()) rc(mdt_launch_job1(&j->post, cur()), "job follow-up");
   return true;
+}
+
+// Pack recorded jobs (any supported kinds, up to 8) into a job table for ONE
+// jobs_multi_k launch: returns (uint8 CPU tensor image, grid). The caller keeps
+// the table in device memory for the lifetime of the plan (graph replays).
+std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs) {
+  TORCH_CHECK(!jobs.empty() && jobs.size() <= 8, "pack_jobs_multi takes 1..8 jobs");
+  std::vector<JobBlob> v;
+  for (auto* j : jobs) {
+    TORCH_CHECK(j != nullptr && !j->has_post(), "pack_jobs_multi: null job or job with a follow-up pass");
+    TORCH_CHECK(j->main.kind > 0, "pack_jobs_multi: job has no fused form (kind 0)");
+    v.push_back(j->main);
+  }
+  auto img = torch::zeros({(int64_t)mdt_jobs_multi_bytes()}, torch::kUInt8);
+  const int grid = mdt_pack_jobs_multi(v.data(), (int)v.size(), img.data_ptr());
+  TORCH_CHECK(grid > 0, "pack_jobs_multi: unsupported job kind or bad job (", grid, ")");
+  return {img, (int64_t)grid};
+}
+
+void launch_jobs_multi(const at::Tensor& dev_pack, int64_t grid) {
+  TORCH_CHECK(dev_pack.is_cuda() && dev_pack.scalar_type() == torch::kUInt8 &&
+                  dev_pack.numel() >= mdt_jobs_multi_bytes(), "launch_jobs_multi: device job table");
+  const int r = mdt_launch_jobs_multi(dev_pack.data_ptr(), (int)grid, cur());
+  TORCH_CHECK(r == 0, "mdt: launch_jobs_multi failed (", r, ")");
+}
+
+// Fused 28x28 step launches (conv28_fused.hip). `t` lists the tensors in the
+// kernel's pointer-table order (None -> nullptr where optional); every tensor is
+// checked for device, contiguity, dtype and minimum size BEFORE the launch so
+// a shape mistake is a Python error, never an out-of-bounds access on the GPU.
+namespace {
+struct Slot {
+  const char* name;
+  char dtype;        // 'f' f32, 'b' bf16, 'i' int32, 'u' uint8 (state blobs)
+  int64_t per_m;     // elements per sample (or fixed count when fixed)
+  bool fixed;        // per_m is a fixed element count
+  bool optional;
+};
+
+std::vector<long long> f28_ptrs(const std::vector<c10::optional<at::Tensor>>& t, const std::vector<Slot>& slots,
+                                int64_t M, int dev) {
+  TORCH_CHECK(t.size() == slots.size(), "f28: expected ", slots.size(), " tensors, got ", t.size());
+  std::vector<long long> p(t.size(), 0);
+  for (size_t i = 0; i < t.size(); ++i) {
+    const Slot& s = slots[i];
+    if (!t[i].has_value() || !t[i]->defined()) {
+      TORCH_CHECK(s.optional, "f28: tensor ", s.name, " is required");
+      continue;
+    }
+    const at::Tensor& x = *t[i];
+    TORCH_CHECK(x.is_cuda() && x.device().index() == dev && x.is_contiguous(), "f28: ", s.name,
+                " must be a contiguous tensor on cuda:", dev);
+    const auto st = x.scalar_type();
+    const bool ok = (s.dtype == 'f' && st == torch::kFloat32) || (s.dtype == 'b' && st == torch::kBFloat16) ||
+                    (s.dtype == 'i' && st == torch::kInt32) || (s.dtype == 'u' && st == torch::kUInt8) ||
+                    (s.dtype == 'l' && st == torch::kInt64);
+    TORCH_CHECK(ok, "f28: ", s.name, " has dtype ", st);
+    const int64_t need = s.fixed ? s.per_m : s.per_m * M;
+    TORCH_CHECK(x.numel() >= need, "f28: ", s.name, " has ", x.numel(), " elements, needs ", need);
+    p[i] = (long long)(intptr_t)x.data_ptr();
+  }
+  return p;
+}
+
+const std::vector<Slot>& f28_weight_slots() {
+  static const std::vector<Slot> w = {
+      {"W1f", 'f', 512, true, false},    {"b1", 'f', 32, true, false},    {"W2", 'b', 32768, true, false},
+      {"b2", 'f', 64, true, false},      {"Wh", 'b', 200704, true, false}, {"bh", 'f', 64, true, false},
+      {"Wd", 'b', 100352, true, false},  {"bd", 'f', 3136, true, false},  {"W3", 'b', 32768, true, false},
+      {"b3", 'f', 32, true, false},      {"W4f", 'f', 512, true, false},  {"b4", 'f', 1, true, false}};
+  return w;
+}
+}  // namespace
+
+void f28_forward(const std::vector<c10::optional<at::Tensor>>& t, int64_t B, int64_t M, int64_t stream, bool train) {
+  TORCH_CHECK(M > 0 && M <= B, "f28_forward: bad M ", M, " for B ", B);
+  std::vector<Slot> slots = f28_weight_slots();
+  const std::vector<Slot> rest = {
+      {"X", 'f', 784, true, false},        {"idx", 'i', B, true, false},
+      {"state", 'u', (int64_t)sizeof(TrainState), true, false}, {"hparams", 'u', (int64_t)sizeof(HParams), true, false},
+      {"xb", 'f', 784, false, !train},     {"a1", 'b', 6272, false, !train},  {"a2", 'b', 3136, false, !train},
+      {"mulv", 'f', 64, false, !train},    {"eps", 'f', 32, false, !train},   {"z16", 'b', 32, false, !train},
+      {"d0", 'b', 3136, false, !train},    {"d1", 'b', 6272, false, !train},  {"dlog", 'f', 784, false, !train},
+      {"recon", 'f', 784, false, true},    {"bce_part", 'f', 1, false, false}, {"kld_part", 'f', 1, false, false},
+      {"db4_part", 'f', 1, false, true},   {"stamps", 'l', 16, false, true}};
+  slots.insert(slots.end(), rest.begin(), rest.end());
+  const int dev = t[0].has_value() ? (int)t[0]->device().index() : 0;
+  const auto p = f28_ptrs(t, slots, M, dev);
+  rc(mdt_f28_forward(p.data(), (int)B, (int)M, (unsigned)stream, train ? 1 : 0, cur()), "f28_forward");
+}
+
+void f28_backward(const std::vector<c10::optional<at::Tensor>>& t, int64_t M) {
+  TORCH_CHECK(M > 0, "f28_backward: bad M");
+  std::vector<Slot> slots = f28_weight_slots();
+  const std::vector<Slot> rest = {
+      {"hparams", 'u', (int64_t)sizeof(HParams), true, false},
+      {"mulv", 'f', 64, false, false},     {"eps", 'f', 32, false, false},     {"a1", 'b', 6272, false, false},
+      {"a2", 'b', 3136, false, false},     {"d0", 'b', 3136, false, false},    {"d1", 'b', 6272, false, false},
+      {"dlog", 'f', 784, false, false},    {"gd1", 'b', 6272, false, false},   {"gd0", 'b', 3136, false, false},
+      {"dbd_part", 'f', 3136, false, false}, {"dmulv", 'f', 64, false, false}, {"dmulv16", 'b', 64, false, false},
+      {"ga2", 'b', 3136, false, false},    {"ga1", 'b', 6272, false, false},   {"db3_part", 'f', 32, false, false},
+      {"db2_part", 'f', 64, false, false}, {"db1_part", 'f', 32, false, false},
+      {"stamps", 'l', 16, false, true}};
+  slots.insert(slots.end(), rest.begin(), rest.end());
+  const int dev = t[0].has_value() ? (int)t[0]->device().index() : 0;
+  const auto p = f28_ptrs(t, slots, M, dev);
+  rc(mdt_f28_backward(p.data(), (int)M, cur()), "f28_backward");
 }
 
 void step_begin(at::Tensor state, const at::Tensor& hparams) {
@@ -524,6 +638,11 @@ void bind_conv(pybind11::module& m) {
       .def_property_readonly("kind", &Job::kind)
       .def_property_readonly("has_post", &Job::has_post);
   m.def("launch_jobs", &launch_jobs);
+  m.def("pack_jobs_multi", &pack_jobs_multi);
+  m.def("launch_jobs_multi", &launch_jobs_multi);
+  m.def("f28_forward", &f28_forward, py::arg("tensors"), py::arg("B"), py::arg("M"), py::arg("stream"),
+        py::arg("train"));
+  m.def("f28_backward", &f28_backward, py::arg("tensors"), py::arg("M"));
   m.def("launch_tail", &launch_tail);
   m.def("igemm", &igemm, py::arg("mode"), py::arg("A"), py::arg("B16"), py::arg("desc"), py::arg("bias"),
         py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),
@@ -547,7 +666,8 @@ void bind_conv(pybind11::module& m) {
   m.def("bce_logits", &bce_logits, py::arg("logits"), py::arg("X"), py::arg("rows"), py::arg("B"), py::arg("P"),
         py::arg("dlog16"), py::arg("recon"), py::arg("part"), py::arg("gpart") = py::none());
   m.def("loss_finalize2", &loss_finalize2, py::arg("bce_part"), py::arg("nb"), py::arg("kld_part"), py::arg("nk"),
-        py::arg("state"), py::arg("hparams"), py::arg("advance_cursor"), py::arg("job") = py::none());
+        py::arg("state"), py::arg("hparams"), py::arg("advance_cursor"), py::arg("job") = py::none(),
+        py::arg("advance_step") = false);
   m.def("step_begin", &step_begin);
   m.def("make_grad_segs", &make_grad_segs);
   m.def("make_grad_units", &make_grad_units);

@@ -258,6 +258,16 @@ class ConvVaeTrainer:
         mode = os.getenv("MDT_CONV_DEFER_WT", "2" if image <= 64 else "0")
         self.defer_wt = mode in ("1", "2")
         self.wt_in_dec = mode == "2"
+        # per-sample fused 28x28 step (csrc/kernels/conv28_fused.hip): forward,
+        # backward-data, weight gradients and optimizer in 4 launches instead of
+        # the layer-by-layer path's 15. MDT_CONV_F28=0 keeps the layer path.
+        self.f28 = (backend == "hip" and image == 28 and channels == 1 and z == 32
+                    and os.getenv("MDT_CONV_F28", "1") != "0")
+        self._plans28 = {}
+        self.f28_skip_adam = False  # tests: leave the reduced gradients in `grads`, no update
+        # profiling: int64 [B*16] tensors (fwd, bwd) receiving per-workgroup
+        # phase-end s_memrealtime stamps (obs/f28_phases.py); None = off
+        self.f28_stamps = (None, None)
         self._fused_launches = 0
         self._data = None
         torch.manual_seed(self.seed if init_seed is None else init_seed)
@@ -372,6 +382,7 @@ class ConvVaeTrainer:
             idx = torch.cat([idx, idx[:1].expand(pad)])
         self._data = (X.contiguous(), idx.contiguous(), n, nb)
         self._graphs.clear()
+        self._plans28.clear()
 
     def attach_reducer(self, reducer):
         """Reducer over ``self.grads`` whose bucket bounds fall on layer starts
@@ -475,6 +486,10 @@ class ConvVaeTrainer:
         self.bce_part = torch.zeros(max(self._n_bce(B), 1), **f32)
         self.kld_part = torch.zeros(B * zf, **f32)  # >= KLD partials of reparam / combine_reparam
         self._plans = {}
+        if self.f28:
+            self.dlog32 = torch.zeros(B * self.D, **f32)
+            self.f28_part = torch.zeros(3 * B, **f32)                  # bce | kld | dec2-bias partials
+            self.f28_bias = torch.zeros(B * (3136 + 32 + 64 + 32), **f32)  # dec_fc | dec1 | enc2 | enc1
         self._cast_weights()
 
     def _n_bce(self, M):
@@ -586,6 +601,18 @@ class ConvVaeTrainer:
         else:
             raise NotImplementedError("conv-VAE HIP path: multi-channel images need the per-channel dlogits sum")
         segs = self._seg_rows(slabs)
+        units, layer_units = self._finalize_units(segs)
+        p = dict(slabs=slabs, colsum=colsum, gpart=gpart, ws=torch.empty(max(ws_need, 1), **f32), rows_per=rows_per,
+                 ws_a=ws_a, ks_a=ks_a,
+                 segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
+                 nunits=len(units), layer_units=layer_units)
+        self._plans[M] = p
+        return p
+
+    @staticmethod
+    def _finalize_units(segs):
+        """GradUnit rows (seg, start, count) of the finalize kernel for GradSeg
+        rows ``segs``; layer i owns units [layer_units[i], layer_units[i+1])."""
         units, layer_units = [], []
         for si, (off, numel, ptr, ns, *_rest) in enumerate(segs):
             if si % 2 == 0:
@@ -599,13 +626,8 @@ class ConvVaeTrainer:
                 cnt = 4 * 256  # grad_finalize_vec4: 4 elements per thread, 16-B accesses
             for st in range(0, numel, cnt):
                 units.append([si, st, min(cnt, numel - st)])
-        layer_units.append(len(units))  # layer i owns units [layer_units[i], layer_units[i+1])
-        p = dict(slabs=slabs, colsum=colsum, gpart=gpart, ws=torch.empty(max(ws_need, 1), **f32), rows_per=rows_per,
-                 ws_a=ws_a, ks_a=ks_a,
-                 segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
-                 nunits=len(units), layer_units=layer_units)
-        self._plans[M] = p
-        return p
+        layer_units.append(len(units))
+        return units, layer_units
 
     def _cast_weights(self):
         h = self.state
@@ -932,6 +954,9 @@ class ConvVaeTrainer:
         red.launch(k)
 
     def _step_hip(self, M):
+        if self.f28:
+            self._step28(M)
+            return
         C = self.C
         X, idx = self._data[0], self._data[1]
         st = self.state
@@ -954,6 +979,81 @@ class ConvVaeTrainer:
         C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
                     st.train_state, st.hparams, True)
         self._transpose_weights()
+
+    # ----------------------------------------------------------- fused 28x28
+    def _plan28(self, M):
+        """Pointer tables, weight-gradient jobs and finalize units of the fused
+        28x28 step for a batch of M (built once per M and data binding; the
+        tensors never move, so captured graphs stay valid)."""
+        p = self._plans28.get(M)
+        if p is not None:
+            return p
+        C, dev, B = self.C, self.device, self.B
+        f32 = dict(dtype=torch.float32, device=dev)
+        L = {l.name: l for l in self.spec}
+        X, idx = self._data[0], self._data[1]
+        st = self.state
+        w = [self._wf32(L["enc1"]), self._b(L["enc1"]), self._w(L["enc2"]), self._b(L["enc2"]),
+             self._w(L["enc_head"]), self._b(L["enc_head"]), self._w(L["dec_fc"]), self._b(L["dec_fc"]),
+             self._w(L["dec1"]), self._b(L["dec1"]), self._wf32(L["dec2"]), self._b(L["dec2"])]
+        part = self.f28_part
+        bce, kld, db4 = part.narrow(0, 0, B), part.narrow(0, B, B), part.narrow(0, 2 * B, B)
+        bias = self.f28_bias
+        dbd = bias.narrow(0, 0, B * 3136)
+        db3 = bias.narrow(0, B * 3136, B * 32)
+        db2 = bias.narrow(0, B * 3168, B * 64)
+        db1 = bias.narrow(0, B * 3232, B * 32)
+        a1, a2, d0, d1 = self.acts["enc1"], self.acts["enc2"], self.acts["dec_fc"], self.acts["dec1"]
+        gd1, gd0, ga2, ga1 = self.gacts["dec1"], self.gacts["dec_fc"], self.gacts["enc2"], self.gacts["enc1"]
+        fwd = w + [X, idx, st.train_state, st.hparams, self.xb, a1, a2, self.mulv, self.eps, self.z16, d0, d1,
+                   self.dlog32, None, bce, kld, db4, self.f28_stamps[0]]
+        bwd = w + [st.hparams, self.mulv, self.eps, a1, a2, d0, d1, self.dlog32, gd1, gd0, dbd, self.dmulv,
+                   self.dmulv16, ga2, ga1, db3, db2, db1, self.f28_stamps[1]]
+        # weight gradients: (G, X) per layer in the conv view (see _backward_hip)
+        srcs = {"enc1": (ga1, self.xb), "enc2": (ga2, a1), "enc_head": (self.dmulv16, a2),
+                "dec_fc": (gd0, self.z16), "dec1": (d0, gd1), "dec2": (d1, self.dlog32)}
+        slabs, jobs = {}, []
+        for name, (G, Xw) in srcs.items():
+            l = L[name]
+            d = self._desc(l, M)
+            ns = C.wgrad_plan(d)[6]
+            t = torch.empty(ns * math.prod(_w_shape(l)), **f32)
+            slabs[name + ".weight"] = (t, ns)
+            j = C.Job()
+            C.wgrad(G, Xw, d, t, job=j)
+            jobs.append(j)
+        j = C.Job()
+        C.loss_finalize2(bce, M, kld, M, st.train_state, st.hparams, True, job=j, advance_step=True)
+        jobs.append(j)
+        # bias gradients: per-sample partial rows written by the fused kernels
+        for name, t, width in (("enc1", db1, 32), ("enc2", db2, 64), ("enc_head", self.dmulv, 64),
+                               ("dec_fc", dbd, 3136), ("dec1", db3, 32), ("dec2", db4, 1)):
+            slabs[name + ".bias"] = (t, M)
+        segs = self._seg_rows(slabs)
+        units, layer_units = self._finalize_units(segs)
+        pack, grid = C.pack_jobs_multi(jobs)
+        p = dict(fwd=fwd, bwd=bwd, jobs=jobs, jobs_pack=pack.to(dev), jobs_grid=grid, slabs=slabs,
+                 segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
+                 nunits=len(units))
+        self._plans28[M] = p
+        return p
+
+    def _step28(self, M):
+        """Fused 28x28 step: forward || backward-data || weight gradients +
+        loss/step || finalize + Adam, 4 launches (DDP: finalize without Adam,
+        bucket all-reduce, then Adam + bf16 cast)."""
+        C, p, st = self.C, self._plan28(M), self.state
+        C.f28_forward(p["fwd"], self.B, M, self.rng_stream, True)
+        C.f28_backward(p["bwd"], M)
+        C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
+        red = self.reducer
+        C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
+                        p["nunits"], st.train_state, st.hparams, red is None and not self.f28_skip_adam)
+        if red is not None:
+            red.launch_all()
+            red.wait_all()
+            C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
+                        st.train_state, st.hparams, True)
 
     # layer groups whose gradients are finalized together (optimizer + bf16
     # re-cast + transposed copies) on the side stream once the backward-data
@@ -1089,9 +1189,10 @@ class ConvVaeTrainer:
                 n -= S
             for _ in range(n):
                 self._replay(1, M)
-        if self._wt_deferred():
+        if self._wt_deferred() or self.f28:
             # the last step's transposed weight copies (deferred to the next
-            # step's first launch): written here so w16t is current between calls
+            # step's first launch, or never needed by the fused 28x28 step):
+            # written here so w16t is current for eval / decode between calls
             self._wtrans_layers(1, len(self.spec))
 
     def prepare(self, batch_sizes, eval_rows=None):

@@ -1,0 +1,231 @@
+"""Fused 28x28 conv-VAE step (csrc/kernels/conv28_fused.hip) on one MI355X.
+
+The numerical oracle is a float64 torch re-implementation of the SAME
+computation with bf16 rounding applied at exactly the points where the
+kernels store bf16 (activations a1/a2/d0/d1, z, the masked gradients
+gd1/gd0/ga2/ga1, d[mu|lv] for the head weight gradient, the f32 input and
+dlogits as the wgrad kernels' bf16 operands) and the bf16 weight copies the
+GEMMs read. What remains between kernel and oracle is f32 accumulation order,
+so every gradient tensor is asserted to 1e-2 relative error (measured <= 4e-3) (the layer-path
+test accepts 0.12 against a plain fp32 reference). Then: eager == graph
+replay bitwise, tail batches, the fused Adam against torch.optim.Adam, and
+training parity with the layer-by-layer path.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float64)
+
+
+def _rel(a, b):
+    a, b = a.detach().double().flatten(), b.detach().double().flatten()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _trainer(B=128, seed=1, **kw):
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    tr = ConvVaeTrainer(batch_size=B, image=28, device=torch.device("cuda"), backend="hip", seed=seed, **kw)
+    assert tr.f28
+    return tr
+
+
+def _emulated_reference(tr, x32, eps, beta=1.0):
+    """float64 forward + backward of the conv-VAE with the fused step's bf16
+    rounding points. Returns (loss, {arena name: gradient})."""
+    P = {k: v.detach().double() for k, v in tr.named_parameters().items()}
+    W1 = P["enc1.weight"].permute(0, 3, 1, 2)            # [32,1,4,4] f32 master
+    W2 = _bf(P["enc2.weight"]).permute(0, 3, 1, 2)       # [64,32,4,4] bf16 copy
+    Wh = _bf(P["enc_head.weight"]).reshape(64, 3136)
+    Wd = _bf(P["dec_fc.weight"]).reshape(3136, 32)
+    W3 = _bf(P["dec1.weight"]).permute(0, 3, 1, 2)       # convT [in 64, out 32, 4, 4]
+    W4 = P["dec2.weight"].permute(0, 3, 1, 2)            # convT [32, 1, 4, 4] f32 master
+    b = {k.split(".")[0]: v for k, v in P.items() if k.endswith(".bias")}
+    M = x32.shape[0]
+    x = x32.double().view(M, 1, 28, 28)
+    nhwc = lambda t: t.permute(0, 2, 3, 1).reshape(M, -1)
+    nchw = lambda t, c, hw: t.view(M, hw, hw, c).permute(0, 3, 1, 2)
+
+    def vjp(fn, inp, wt, gout):
+        inp = inp.detach().requires_grad_()
+        wt = wt.detach().requires_grad_()
+        out = fn(inp, wt)
+        return torch.autograd.grad(out, (inp, wt), gout)
+
+    conv = lambda i, w: F.conv2d(i, w, stride=2, padding=1)
+    tconv = lambda i, w: F.conv_transpose2d(i, w, stride=2, padding=1)
+    # ---- forward
+    a1 = _bf(F.relu(conv(x, W1) + b["enc1"].view(1, -1, 1, 1)))
+    a2 = _bf(F.relu(conv(a1, W2) + b["enc2"].view(1, -1, 1, 1)))
+    a2f = nhwc(a2)
+    h = a2f @ Wh.t() + b["enc_head"]
+    mu, lv = h[:, :32], h[:, 32:]
+    e = eps.double()
+    sd = torch.exp(0.5 * lv)
+    z = _bf(mu + e * sd)
+    d0f = _bf(F.relu(z @ Wd.t() + b["dec_fc"]))
+    d0 = nchw(d0f, 64, 7)
+    d1 = _bf(F.relu(tconv(d0, W3) + b["dec1"].view(1, -1, 1, 1)))
+    t = tconv(d1, W4) + b["dec2"].view(1, -1, 1, 1)
+    sp = torch.clamp(t, min=0) + torch.log1p(torch.exp(-t.abs()))
+    bce = (x * torch.clamp(sp - t, max=100.0) + (1 - x) * torch.clamp(sp, max=100.0)).sum()
+    kld = -0.5 * torch.sum(1 + lv - mu.pow(2) - lv.exp())
+    loss = bce + beta * kld
+    # ---- backward (kernel order and rounding)
+    g = {}
+    dlog = torch.sigmoid(t) - x
+    gi, _ = vjp(tconv, d1, W4, dlog)
+    _, g["dec2.weight"] = vjp(tconv, d1, W4, _bf(dlog))
+    g["dec2.bias"] = dlog.sum().view(1)
+    gd1f = gi * (d1 > 0)
+    gd1 = _bf(gd1f)
+    g["dec1.bias"] = gd1f.sum((0, 2, 3))
+    gi, g["dec1.weight"] = vjp(tconv, d0, W3, gd1)
+    gd0f = nhwc(gi) * (d0f > 0)
+    gd0 = _bf(gd0f)
+    g["dec_fc.bias"] = gd0f.sum(0)
+    dz = gd0 @ Wd
+    g["dec_fc.weight"] = gd0.t() @ z
+    dm = dz + beta * mu
+    dl = 0.5 * dz * e * sd + 0.5 * beta * (sd * sd - 1)
+    dmulv = torch.cat([dm, dl], 1)
+    g["enc_head.bias"] = dmulv.sum(0)
+    g["enc_head.weight"] = _bf(dmulv).t() @ a2f
+    ga2f = (dmulv @ Wh) * (a2f > 0)
+    ga2 = _bf(ga2f)
+    g["enc2.bias"] = ga2f.view(M, 49, 64).sum((0, 1))
+    gi, g["enc2.weight"] = vjp(conv, a1, W2, nchw(ga2, 64, 7))
+    ga1f = gi * (a1 > 0)
+    ga1 = _bf(ga1f)
+    g["enc1.bias"] = ga1f.sum((0, 2, 3))
+    _, g["enc1.weight"] = vjp(conv, _bf(x), W1, ga1)
+    out = {}
+    for k, v in g.items():
+        if k.endswith(".weight") and v.dim() == 4:
+            v = v.permute(0, 2, 3, 1)  # torch [O][I][kh][kw] (convT: [in][out]) -> arena [O][kh][kw][I]
+        out[k] = v.reshape(tr.named_grads()[k].shape)
+    return float(loss), out
+
+
+@pytest.mark.parametrize("M", [128, 100])
+def test_f28_gradients_match_bf16_emulated_reference(M, native_ext):
+    from multidisttorch_amd.ops.philox import reparam_eps
+
+    dev = torch.device("cuda")
+    tr = _trainer(B=128, seed=2, use_graphs=False)
+    X = torch.rand(512, 784, generator=torch.Generator().manual_seed(7)).to(dev)
+    idx = torch.randperm(512, generator=torch.Generator().manual_seed(8)).to(dev, torch.int32)
+    tr.bind_train_data(X, idx)
+    tr.set_cursor(0, 4)
+    tr.f28_skip_adam = True
+    p0 = tr.params.clone()
+    tr.train_steps(1, M=M)
+    torch.cuda.synchronize()
+    assert torch.equal(tr.params, p0)  # no update: the gradients stay in `grads`
+    assert tr.read_state()["step"] == 1 and tr.read_state()["cursor"] == 1
+    x = X[idx[:M].long()]
+    torch.testing.assert_close(tr.xb[:M], x, rtol=0, atol=0)
+    eps = torch.from_numpy(reparam_eps(M, 32, tr.seed, tr.rng_stream, 0)).to(dev)
+    torch.testing.assert_close(tr.eps[:M], eps, rtol=1e-5, atol=1e-5)  # Philox parity
+    loss, gref = _emulated_reference(tr, x, eps)
+    kloss = float(tr.loss_history()[0])
+    assert abs(kloss - loss) / abs(loss) < 1e-4, (kloss, loss)
+    errs = {n: _rel(tr.named_grads()[n], gref[n]) for n in gref}
+    print("f28 grad rel-err vs bf16-emulated f64:", {k: round(v, 6) for k, v in errs.items()})
+    bad = {n: e for n, e in errs.items() if not e < 1e-2}
+    assert not bad, bad
+
+
+def test_f28_eager_equals_graph_and_trains(native_ext):
+    from multidisttorch_amd.data.datasets import synthetic_images
+
+    dev = torch.device("cuda")
+    X = synthetic_images(2048, device=dev)
+    idx = torch.arange(2048, device=dev, dtype=torch.int32)
+    res = []
+    for graphs in (False, True):
+        tr = _trainer(seed=3, use_graphs=graphs, graph_steps=4)
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 16)
+        tr.train_steps(40)
+        torch.cuda.synchronize()
+        h = tr.loss_history()[:40]
+        assert np.all(np.isfinite(h)) and h[-5:].mean() < 0.7 * h[:5].mean(), h
+        res.append((h.copy(), tr.params.clone(), tr.exp_avg_sq.clone(), tr.read_state()))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+    assert res[0][3]["step"] == res[1][3]["step"] == 40 and res[0][3]["cursor"] == res[1][3]["cursor"] == 8
+    # eval / decode (layer path kernels) see current transposed weights
+    total, first = tr.evaluate(X, torch.arange(300, device=dev, dtype=torch.int32))
+    assert np.isfinite(total) and first.shape == (128, 784)
+
+
+def test_f28_adam_matches_torch_optim(native_ext):
+    """The finalize + fused Adam of the fused step against torch.optim.Adam
+    fed with the kernel's own gradients, over 3 steps (lr, betas, eps, bias
+    corrections, bf16 re-cast of the weight copies)."""
+    dev = torch.device("cuda")
+    X = torch.rand(512, 784, generator=torch.Generator().manual_seed(1)).to(dev)
+    idx = torch.arange(512, device=dev, dtype=torch.int32)
+    a = _trainer(seed=5, use_graphs=False, lr=3e-3, betas=(0.8, 0.95), eps=1e-6)
+    b = _trainer(seed=5, use_graphs=False, lr=3e-3, betas=(0.8, 0.95), eps=1e-6)
+    for tr in (a, b):
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 4)
+    b.f28_skip_adam = True
+    ref = torch.nn.Parameter(a.params.detach().clone())
+    opt = torch.optim.Adam([ref], lr=3e-3, betas=(0.8, 0.95), eps=1e-6)
+    for step in range(3):
+        p_prev = a.params.detach().clone()
+        b.params.copy_(p_prev)      # b's gradient at a's current weights: bitwise a's own gradient
+        b.refresh_weights()
+        b.set_step(step)
+        b.set_cursor(step, 4)
+        b.train_steps(1)
+        a.train_steps(1)            # fused finalize + Adam
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            ref.copy_(p_prev)
+        ref.grad = b.grads.detach().clone()
+        opt.step()
+        torch.testing.assert_close(a.params, ref.detach(), rtol=1e-5, atol=1e-7)
+        # moments: rounding-level agreement relative to the gradient scale (the
+        # kernel's fmaf lerp vs torch's lerp_ differ in the last ulp of g)
+        gmax = float(ref.grad.abs().max())
+        torch.testing.assert_close(a.exp_avg, opt.state[ref]["exp_avg"], rtol=1e-5, atol=1e-6 * gmax)
+        torch.testing.assert_close(a.exp_avg_sq, opt.state[ref]["exp_avg_sq"], rtol=1e-5, atol=1e-6 * gmax * gmax)
+        assert torch.equal(a.w16, a.params.to(torch.bfloat16))  # bf16 re-cast of the updated masters
+
+
+def test_f28_matches_layer_path_training(native_ext, monkeypatch):
+    """Same trial trained by the fused step and by the layer-by-layer step:
+    the per-step losses track each other (different bf16 rounding points and
+    f32 summation orders, nothing else)."""
+    from multidisttorch_amd.data.datasets import synthetic_images
+
+    dev = torch.device("cuda")
+    X = synthetic_images(1024, device=dev)
+    idx = torch.arange(1024, device=dev, dtype=torch.int32)
+    hist = []
+    for f28 in ("1", "0"):
+        monkeypatch.setenv("MDT_CONV_F28", f28)
+        from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+        tr = ConvVaeTrainer(batch_size=128, image=28, device=dev, backend="hip", seed=4, use_graphs=True,
+                            graph_steps=5)
+        assert tr.f28 == (f28 == "1")
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 8)
+        tr.train_steps(20)
+        torch.cuda.synchronize()
+        hist.append(tr.loss_history()[:20].copy())
+    np.testing.assert_allclose(hist[0], hist[1], rtol=3e-2)
+    assert hist[0][-1] < 0.8 * hist[0][0]

@@ -1,9 +1,19 @@
-"""Conv-VAE bf16 MFMA kernels vs the fp32 torch reference network (GPU)."""
+"""Conv-VAE bf16 MFMA kernels vs the fp32 torch reference network (GPU).
+
+These tests exercise the LAYER-BY-LAYER path (conv_igemm / conv_jobs /
+conv_thin kernels), which 128x128 images use and 28x28 images fall back to
+with MDT_CONV_F28=0; the fused 28x28 step has its own tests
+(test_conv28_fused.py)."""
 import numpy as np
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _layer_path(monkeypatch):
+    monkeypatch.setenv("MDT_CONV_F28", "0")
 
 
 def _wt_layers(tr):
