@@ -116,6 +116,12 @@ __device__ __forceinline__ void stamp(unsigned long long* st, int k) {
 
 __device__ __forceinline__ int img14(int pix, int ch) { return (pix << 6) + ((ch ^ ((pix >> 1) & 3)) << 4); }
 
+// 7x7x64 bf16 LDS image, 128-B pixel rows: 16-B chunk c of pixel p at slot
+// c ^ (p & 7), so the transposed-conv A gathers (16 class pixels at one chunk)
+// spread over the banks.
+__device__ __forceinline__ int img49(int pix, int ch) { return (pix << 7) + ((ch ^ (pix & 7)) << 4); }
+__device__ __forceinline__ int img49e(int pix, int c) { return img49(pix, c >> 3) + ((c & 7) << 1); }
+
 // Per-tap images of a [64][16][32] bf16 weight (rows c64 = reduction index,
 // 32 columns) are laid out for tr_frag<32> reads: 16 images of 4 KB
 // (TapImageRegs below fills them).
@@ -221,11 +227,11 @@ __device__ __forceinline__ void conv14to7(const uint8_t* in_img, BFrag bfrag, Pr
 // stride-parity classes (a, b) = (oy & 1, ox & 1) without zero-insertion taps:
 // class rows = 49 pixels (jy, jx) with (oy, ox) = (2jy + a, 2jx + b), k = 2x2
 // taps (ky = 1 - a + 2ty, iy = jy + a - ty) x 64 channels, cols = 32. A from the
-// [49][64] LDS image `in`, B via tr_frag from the per-tap images `wimg`.
+// img49 LDS image `in`, B via tr_frag from the per-tap images `wimg`.
 // 32 items (class, m-tile, n-tile), four per wave. `cs` (optional) receives
 // the per-column sums of the epilogue values of this wave's items.
 template <class Pre, class Epi>
-__device__ __forceinline__ void tconv7to14(const __bf16* in, const uint8_t* wimg, Pre pre, Epi epi, float (&cs)[2]) {
+__device__ __forceinline__ void tconv7to14(const uint8_t* in, const uint8_t* wimg, Pre pre, Epi epi, float (&cs)[2]) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   cs[0] = cs[1] = 0.f;
   // items it = w + 8q: class q, m-tile (w >> 1) & 3, n-tile w & 1 (fixed per wave)
@@ -250,8 +256,7 @@ __device__ __forceinline__ void tconv7to14(const __bf16* in, const uint8_t* wimg
       const int ty = ks >> 2, tx = (ks >> 1) & 1, hh = ks & 1;
       const int iy = jy + a - ty, ix = jx + b - tx;
       const bool ok = r < 49 && (unsigned)iy < 7u && (unsigned)ix < 7u;
-      const bf16x8 av =
-          ok ? *reinterpret_cast<const bf16x8*>(in + (iy * 7 + ix) * 64 + 32 * hh + 8 * (lane >> 4)) : zero8();
+      const bf16x8 av = ok ? *reinterpret_cast<const bf16x8*>(in + img49(iy * 7 + ix, 4 * hh + (lane >> 4))) : zero8();
       const int tap = ((1 - a) + 2 * ty) * 4 + (1 - b) + 2 * tx;
       const bf16x8 bv = tr_frag<32>(wimg + tap * 4096, 16 * nj, 32 * hh, lane);
       acc = mfma_bf16(av, bv, acc);
@@ -296,7 +301,7 @@ __global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
   float* W4s = reinterpret_cast<float*>(lds + kFW4);
   uint8_t* A1s = lds + kFA1;
   __bf16* A2s = reinterpret_cast<__bf16*>(lds + kFA2);
-  __bf16* D0s = reinterpret_cast<__bf16*>(lds + kFD0);
+  uint8_t* D0u = lds + kFD0;  // img49 image
   float* Hs = reinterpret_cast<float*>(lds + kFH);
   __bf16* Zs = reinterpret_cast<__bf16*>(lds + kFZ);
   float* Red = reinterpret_cast<float*>(lds + kFRed);
@@ -477,7 +482,7 @@ __global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
             if (lane < 16) {
               const int jj = 16 * t + lane;
               const __bf16 o = (__bf16)fmaxf(acc[0] + reinterpret_cast<const float*>(lds + kFBd)[jj], 0.f);
-              D0s[jj] = o;
+              *reinterpret_cast<__bf16*>(D0u + img49e(jj >> 6, jj & 63)) = o;
               if (a.train) a.d0[(size_t)n * kFlat + jj] = o;
             }
           }
@@ -490,7 +495,7 @@ __global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
   // ---- P6: dec1 (convT 64 -> 32, 7x7 -> 14x14, MFMA), ReLU
   {
     float cs[2];
-    tconv7to14(D0s, W3s, [&](int, int co) { return W.b3[co]; }, [&](int pix, int co, float v, float bias) {
+    tconv7to14(D0u, W3s, [&](int, int co) { return W.b3[co]; }, [&](int pix, int co, float v, float bias) {
       const __bf16 o = (__bf16)fmaxf(v + bias, 0.f);
       D1s[pix * 32 + co] = o;
       if (a.train) a.d1[((size_t)n * 196 + pix) * 32 + co] = o;
@@ -580,7 +585,7 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
   __bf16* GD0s = reinterpret_cast<__bf16*>(lds + kBGD0);
   float* DMs = reinterpret_cast<float*>(lds + kBDM);
   float* DZR = reinterpret_cast<float*>(lds + kBDZR);
-  __bf16* GA2s = reinterpret_cast<__bf16*>(lds + kBGA2);
+  uint8_t* GA2u = lds + kBGA2;  // img49 image
   float* GA2F = reinterpret_cast<float*>(lds + kBGA2F);
   float* CS = reinterpret_cast<float*>(lds + kBCS);
   uint8_t* W2s = lds + kBW2;
@@ -754,7 +759,7 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
       o[e] = (__bf16)v;
       GA2F[k0 + e] = v;
     }
-    *reinterpret_cast<bf16x8*>(GA2s + k0) = o;
+    *reinterpret_cast<bf16x8*>(GA2u + img49(tid >> 3, tid & 7)) = o;
     *reinterpret_cast<bf16x8*>(a.ga2 + (size_t)n * kFlat + k0) = o;
   }
   w2r.store(W2s);
@@ -769,7 +774,7 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
   // ---- Q6: enc2 backward-data (convT 64 -> 32 with the conv weights, 7 -> 14) x enc1 ReLU mask
   {
     float cs[2];
-    tconv7to14(GA2s, W2s, [&](int pix, int co) { return (float)a.a1[((size_t)n * 196 + pix) * 32 + co]; },
+    tconv7to14(GA2u, W2s, [&](int pix, int co) { return (float)a.a1[((size_t)n * 196 + pix) * 32 + co]; },
                [&](int pix, int co, float v, float mask) {
       const size_t e = ((size_t)n * 196 + pix) * 32 + co;
       const float g = mask > 0.f ? v : 0.f;

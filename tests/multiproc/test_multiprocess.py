@@ -25,13 +25,14 @@ def _results(outs):
     return res
 
 
-def _run(args, n, emulate="torchrun", timeout=180, cwd=None):
+def _run(args, n, emulate="torchrun", timeout=180, cwd=None, extra_env=None):
     cmd = [sys.executable] + args
     old = os.getcwd()
     if cwd:
         os.chdir(cwd)
     try:
-        rc, outs = launch(cmd, n, emulate=emulate, timeout=timeout, extra_env=ENV, capture=True)
+        rc, outs = launch(cmd, n, emulate=emulate, timeout=timeout, extra_env={**ENV, **(extra_env or {})},
+                          capture=True)
     finally:
         os.chdir(old)
     return rc, outs
@@ -215,6 +216,25 @@ def test_bench_contract_multirank(tmp_path, n, k):
     assert out["config"]["trials"] == K and out["config"]["parallelism"] == f"groups{K}x{n // K}"
     assert out["config"]["valid"] is True
     assert abs(out["value"] - K * 64 * 2 / (out["ms_per_step"] * 2e-3)) / out["value"] < 0.01
+
+
+@pytest.mark.parametrize("model,k,bs", [("conv28", 4, 128), ("conv128", 2, 8)])
+def test_bench_contract_conv_groups_n8(tmp_path, model, k, bs):
+    """BASELINE configs #4/#5 shape at n = 8 (torch backend, gloo): K trial
+    groups of 8 // K ranks each run intra-group DDP; one JSON line with the
+    group layout and samples counted once per trial."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "2", "--warmup", "1", "--model", model,
+            "--ngroups", str(k), "--batch-size", str(bs), "--backend", "torch"]
+    rc, outs = _run(args, 8, "torchrun", timeout=400, cwd=str(tmp_path), extra_env={"OMP_NUM_THREADS": "1"})
+    text = "\n".join(o or "" for o in outs)
+    assert rc == 0, text[-4000:]
+    lines = [l for l in text.splitlines() if l.startswith("{\"metric\"")]
+    assert len(lines) == 1, text[-4000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["trials"] == k
+    assert out["config"]["parallelism"] == f"groups{k}x{8 // k}"
+    assert out["config"]["model"].startswith("conv")
+    assert abs(out["value"] - k * bs * 2 / (out["ms_per_step"] * 2e-3)) / out["value"] < 0.01
 
 
 def test_vae_hpo_conv_ckpt_and_resume(tmp_path):
