@@ -51,6 +51,7 @@ struct FwdPlan {
   int ksplit, kt_per_split;
   int colsum_rows;  // rows of the per-block column-sum partials (classes * mtiles)
   int thin;         // 1: per-element im2col gather (channel count not a multiple of 8)
+  int direct;       // > 0: patch-resident direct kernel configuration + 1 (conv_direct.h)
 };
 
 // Weight-gradient GEMM plan: dW[CO][KH*KW*C] = sum_m G[m][co] * im2col(X)[m][k'].

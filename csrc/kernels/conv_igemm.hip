@@ -24,6 +24,7 @@
 #include <algorithm>
 
 #include "conv_igemm_dev.h"
+#include "conv_direct.h"
 
 namespace mdt {
 
@@ -46,8 +47,58 @@ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 namespace mdt {
 using namespace mdt::tiles;
 
-bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p) {
+// Patch-resident direct kernel (conv_direct.h) for a geometry: configuration
+// index, or -1. MDT_CONV_DIRECT=0 keeps every layer on the im2col kernels.
+struct DcInfo {
+  int RB, NBB, MT, NB;
+};
+template <class CF>
+constexpr DcInfo dc_info() { return DcInfo{CF::RB, CF::NBB, CF::MT, CF::NB}; }
+static const DcInfo kDcInfo[] = {dc_info<DcS1>(),  dc_info<DcS2>(),  dc_info<DcT2>(),  dc_info<DcT3>(),
+                                  dc_info<DcS1b>(), dc_info<DcS2b>(), dc_info<DcT2b>(), dc_info<DcT3b>()};
+
+int direct_cfg(int mode, const ConvDesc& d) {
+  static const bool on = [] {
+    const char* e = getenv("MDT_CONV_DIRECT");
+    return !(e && e[0] == '0');
+  }();
+  // default: the two-workgroups-per-CU tiles (R = 4), measured 15-18 % faster
+  // than the one-per-CU R = 8 tiles at B = 64 and 128 (profiles/r2_dconv);
+  // MDT_DCONV_ALT=0 selects the latter
+  static const int alt = [] {
+    const char* e = getenv("MDT_DCONV_ALT");
+    return e && e[0] == '0' ? 0 : 4;
+  }();
+  if (!on || d.KH != 4 || d.KW != 4 || d.S != 2 || d.P != 1) return -1;
+  if (d.H != d.W || d.OH != d.OW || d.H != 2 * d.OH) return -1;
+  if (mode == kModeConv) {  // A = input (H, C), columns = CO
+    if (d.C == 32 && d.H == 64 && d.CO == 64) return 0 + alt;
+    if (d.C == 64 && d.H == 32 && d.CO == 128) return 1 + alt;
+  } else {  // A = conv output (OH, CO), columns = C
+    if (d.CO == 128 && d.OH == 16 && d.C == 64) return 2 + alt;
+    if (d.CO == 64 && d.OH == 32 && d.C == 32) return 3 + alt;
+  }
+  return -1;
+}
+
+bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p, bool allow_direct) {
   FwdPlan q{};
+  const int dc = allow_direct ? direct_cfg(mode, d) : -1;
+  if (dc >= 0) {
+    const DcInfo& di = kDcInfo[dc];
+    q.direct = dc + 1;
+    q.classes = mode == kModeConv ? 1 : 4;
+    q.M = mode == kModeConv ? d.N * d.OH * d.OW : d.N * d.OH * d.OW;
+    q.Ncols = mode == kModeConv ? d.CO : d.C;
+    q.K = mode == kModeConv ? 16 * d.C : 4 * d.CO;
+    q.BM = di.MT; q.BN = di.NB;
+    q.mtiles = d.N * di.RB; q.ntiles = di.NBB; q.ktiles = q.K / 64;
+    q.ksplit = 1; q.kt_per_split = q.ktiles;
+    q.colsum_rows = d.N * di.RB;
+    q.cfg = 100 + dc;
+    *p = q;
+    return true;
+  }
   if (mode == kModeConv) {
     q.classes = 1;
     q.M = d.N * d.OH * d.OW;
@@ -196,7 +247,7 @@ int build_igemm(int mode, const void* A, const void* B16, ConvDesc d, const floa
                 int* nc) {
   FwdPlan q;
   const bool can_split = ws != nullptr && omask == nullptr && colsum == nullptr;
-  if (!plan_fwd(mode, d, can_split, &q)) return 1;
+  if (!plan_fwd(mode, d, can_split, &q, false)) return 1;
   IgArgs a{};
   a.d = d;
   a.A = A;
@@ -244,6 +295,40 @@ int build_wgrad(const void* G16, const void* X, ConvDesc d, float* out, WgArgs* 
   *pa = a;
   *pq = q;
   return 0;
+}
+
+static unsigned long long* g_dc_stamps = nullptr;
+
+template <class CF>
+void launch_dc(const DcArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((dconv_k<CF>), dim3(a.nimg * CF::RB * CF::NBB), dim3(CF::THREADS), 0, s, a);
+}
+
+int launch_direct(int cfg, const void* A, const void* B16, const ConvDesc& d, const float* bias, int relu, void* y16,
+                  float* y32, const void* omask, float* colsum, hipStream_t s) {
+  DcArgs a{};
+  a.A = reinterpret_cast<const __bf16*>(A);
+  a.B = reinterpret_cast<const __bf16*>(B16);
+  a.y16 = reinterpret_cast<__bf16*>(y16);
+  a.y32 = y32;
+  a.bias = bias;
+  a.omask = reinterpret_cast<const __bf16*>(omask);
+  a.colsum = colsum;
+  a.stamps = g_dc_stamps;
+  a.relu = relu;
+  a.nimg = d.N;
+  switch (cfg) {
+    case 0: launch_dc<DcS1>(a, s); break;
+    case 1: launch_dc<DcS2>(a, s); break;
+    case 2: launch_dc<DcT2>(a, s); break;
+    case 3: launch_dc<DcT3>(a, s); break;
+    case 4: launch_dc<DcS1b>(a, s); break;
+    case 5: launch_dc<DcS2b>(a, s); break;
+    case 6: launch_dc<DcT2b>(a, s); break;
+    case 7: launch_dc<DcT3b>(a, s); break;
+    default: return 2;
+  }
+  return (int)hipGetLastError();
 }
 
 int launch_splitk_combine(const CombineArgs& c, int nblk, hipStream_t s) {
@@ -351,6 +436,11 @@ int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d
   FwdPlan q;
   CombineArgs c;
   int nc = 0;
+  const int dc = direct_cfg(mode, d);
+  if (dc >= 0) {  // the planner reported the direct tiling: never fall back silently
+    if ((pro && pro->slab) || a_is_f32) return 5;
+    return launch_direct(dc, A, B16, d, bias, relu, y16, y32, omask, colsum, s);
+  }
   if (build_igemm(mode, A, B16, d, bias, relu, y16, y32, omask, colsum, ws, &a, &q, &c, &nc)) return 1;
   int rc;
   if (pro && pro->slab) {
@@ -411,6 +501,9 @@ int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* o
   }
   return (int)hipGetLastError();
 }
+
+// Profiling: per-workgroup s_memrealtime stamps ([grid][8]) of the direct kernels, or null.
+void mdt_dconv_stamps(unsigned long long* p) { g_dc_stamps = p; }
 
 int mdt_colsum(const void* G16, int M, int N, int rows_per, float* slab, hipStream_t s) {
   if (N % 8 || rows_per < 1) return 1;

@@ -356,7 +356,9 @@ int mdt_job_igemm(JobBlob* g, JobBlob* c, int mode, const void* A, int a_is_f32,
   if (build_igemm(mode, A, B16, d, bias, relu, y16, y32, omask, colsum, ws, &a, &q, &cb, &nc)) return 1;
   memset(g, 0, sizeof(*g));
   memset(c, 0, sizeof(*c));
-  const bool ok = !a_is_f32 && !q.thin && !use_glds();
+  // direct-kernel geometries have no job form yet: kind 0 sends the caller
+  // to mdt_igemm (their column-sum rows follow the direct plan)
+  const bool ok = !a_is_f32 && !q.thin && !use_glds() && direct_cfg(mode, d) < 0;
   g->kind = ok ? kJobIgemm + mode * 100 + q.cfg : 0;
   g->nblk = q.mtiles * q.ntiles * q.ksplit * q.classes;
   g->aux[0] = q.mtiles * q.ntiles;

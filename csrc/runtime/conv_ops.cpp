@@ -16,6 +16,7 @@
 
 extern "C" {
 int mdt_igemm_plan(int mode, mdt::ConvDesc d, int allow_split, int* info);
+void mdt_dconv_stamps(unsigned long long* p);
 int mdt_wgrad_plan(mdt::ConvDesc d, int* info);
 int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, mdt::ConvDesc d, const float* bias, int relu,
               void* y16, float* y32, const void* omask, float* colsum, float* ws, int skip_combine, hipStream_t s,
@@ -632,6 +633,15 @@ class TrialStateBuf {
 void bind_conv(pybind11::module& m) {
   namespace py = pybind11;
   m.def("igemm_plan", &igemm_plan);
+  m.def("dconv_stamps", [](const c10::optional<at::Tensor>& t) {
+    // profiling: per-workgroup s_memrealtime stamps of the direct conv kernels ([grid][8] int64), None = off
+    if (t.has_value() && t->defined()) {
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt64, "dconv_stamps: int64 CUDA tensor");
+      mdt_dconv_stamps(reinterpret_cast<unsigned long long*>(t->data_ptr()));
+    } else {
+      mdt_dconv_stamps(nullptr);
+    }
+  });
   m.def("wgrad_plan", &wgrad_plan);
   py::class_<Job>(m, "Job")
       .def(py::init<>())

@@ -91,6 +91,18 @@ def hip_flags():
             "-Wno-unused-result", "-I" + os.path.join(CSRC, "kernels")] + extra
 
 
+# Per-file code-generation flags. -amdgpu-mfma-vgpr-form: MFMA accumulators in
+# the VGPR file. With the default AGPR form the compiler copied every loop-
+# carried accumulator AGPR -> VGPR -> AGPR around the k-loop back edge of the
+# conv GEMM kernels (3-4 thousand v_accvgpr moves per file; none in the fused
+# 28x28 / MLP kernels, which keep the default).
+FILE_FLAGS = {
+    "conv_igemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+    "conv_jobs.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+    "conv_thin.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+}
+
+
 def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     inc, tlib, abi = _torch_paths()
     os.makedirs(BUILD, exist_ok=True)
@@ -108,6 +120,8 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     for s in kern:
         obj = os.path.join(BUILD, os.path.basename(s) + ".o")
         flags = hip_flags()
+        if os.getenv("MDT_MFMA_VGPR", "1") != "0":
+            flags = flags + FILE_FLAGS.get(os.path.basename(s), [])
         cmd = [hipcc] + flags + ["-c", s, "-o", obj]
         jobsl.append((cmd, s, obj, _stamp([s] + hdrs, flags + ["force" if force else ""])))
     for s in host:

@@ -1,0 +1,87 @@
+"""Patch-resident direct conv kernels (csrc/kernels/conv_direct.h) vs fp32 torch.
+
+The 128x128 conv-VAE's stride-2 4x4 layers run on these kernels through the
+same ``igemm`` entry point as the im2col kernels (the planner picks them by
+geometry). Each case feeds bf16-exact inputs and compares the bf16/f32 outputs,
+the ReLU / ReLU-backward mask epilogue and the per-workgroup column sums with
+``conv2d`` / ``conv_transpose2d`` in fp32 (the kernels accumulate in f32, so
+the only difference is summation order and the final bf16 rounding)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _parity_B(Wc):
+    """Conv-view weight [CO][C][4][4] -> per-class B[cls][C][(t0, t1, co)] of the
+    parity-class transposed conv (class (ca, cb) -> output parity (oa, ob) =
+    ((ca+1)&1, (cb+1)&1); tap (t0, t1) reads A row a + ea - t0 with
+    ea = (oa+1-ca)>>1, i.e. kernel row ky = oa + 1 - 2 ea + 2 t0)."""
+    CO, C = Wc.shape[:2]
+    out = []
+    for cls in range(4):
+        ca, cb = cls >> 1, cls & 1
+        oa, ob = (ca + 1) & 1, (cb + 1) & 1
+        ea, eb = (oa + 1 - ca) >> 1, (ob + 1 - cb) >> 1
+        taps = []
+        for t0 in range(2):
+            for t1 in range(2):
+                ky, kx = oa + 1 - 2 * ea + 2 * t0, ob + 1 - 2 * eb + 2 * t1
+                taps.append(Wc[:, :, ky, kx].t())  # [C][CO]
+        out.append(torch.stack(taps, 1).reshape(C, 4 * CO))
+    return torch.stack(out, 0).contiguous()
+
+
+# (mode, H, C, OH, CO) in conv view: mode 0 = conv (A = H x H x C), mode 1 =
+# transposed conv (A = OH x OH x CO, output H x H x C)
+CASES = [(0, 64, 32, 32, 64), (0, 32, 64, 16, 128), (1, 32, 64, 16, 128), (1, 64, 32, 32, 64)]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"mode{c[0]}_{c[1]}x{c[2]}_{c[3]}x{c[4]}")
+@pytest.mark.parametrize("epi", ["bias_relu", "mask_colsum"])
+def test_direct_conv_matches_torch(case, epi, native_ext):
+    C_ = native_ext
+    mode, H, C, OH, CO = case
+    N = 3
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(11 + mode + H)
+    Wc = (torch.randn(CO, C, 4, 4, generator=g) * 0.05).bfloat16().float().to(dev)
+    d = [N, H, H, C, OH, OH, CO, 4, 4, 2, 1]
+    info = C_.igemm_plan(mode, d, False)
+    assert info[0] >= 100, f"direct kernel not selected: {info}"
+    if mode == 0:
+        A = torch.randn(N, C, H, H, generator=g).bfloat16().float().to(dev)
+        ref = F.conv2d(A, Wc, stride=2, padding=1)          # [N][CO][OH][OH]
+        B16 = Wc.permute(0, 2, 3, 1).contiguous().bfloat16()
+        ncols = CO
+    else:
+        A = torch.randn(N, CO, OH, OH, generator=g).bfloat16().float().to(dev)
+        ref = F.conv_transpose2d(A, Wc, stride=2, padding=1)  # [N][C][H][H]
+        B16 = _parity_B(Wc).bfloat16()
+        ncols = C
+    A16 = A.permute(0, 2, 3, 1).contiguous().bfloat16()
+    ref = ref.permute(0, 2, 3, 1).contiguous()  # NHWC
+    y16 = torch.empty(ref.numel(), dtype=torch.bfloat16, device=dev)
+    y32 = torch.empty(ref.numel(), dtype=torch.float32, device=dev)
+    bias = mask = cs = None
+    relu = False
+    if epi == "bias_relu":
+        bias = (torch.randn(ncols, generator=g) * 0.1).to(dev)
+        relu = True
+        ref = torch.relu(ref + bias)
+    else:
+        mask = (torch.rand(ref.shape, generator=g) > 0.4).bfloat16().to(dev)
+        ref = ref * mask.float()
+        cs = torch.full((info[11] * ncols,), float("nan"), device=dev)
+    C_.igemm(mode, A16, B16, d, bias, relu, y16, y32, mask, cs)
+    torch.cuda.synchronize()
+    r = ref.flatten()
+    err = float((y32 - r).abs().max() / r.abs().max())
+    assert err < 1e-5, err
+    torch.testing.assert_close(y16.float(), r.bfloat16().float(), rtol=1e-2, atol=1e-2 * float(r.abs().max()))
+    if cs is not None:
+        assert torch.isfinite(cs).all()
+        tot = cs.view(info[11], ncols).double().sum(0)
+        torch.testing.assert_close(tot, ref.reshape(-1, ncols).double().sum(0), rtol=1e-5,
+                                   atol=1e-5 * float(ref.abs().sum(0).max()))
