@@ -294,20 +294,26 @@ constexpr int kFBd = kFDummy + 8192;        // f32 [3136] dec_fc bias
 constexpr int kFLds = kFBd + kFlat * 4;
 static_assert(kFA1 % 16 == 0 && kFA2 % 16 == 0 && kFD0 % 16 == 0 && kFW3 % 16 == 0, "LDS alignment");
 
-__global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kFLds];
-  float* Xs = reinterpret_cast<float*>(lds + kFX);
-  float* W1s = reinterpret_cast<float*>(lds + kFW1);
-  float* W4s = reinterpret_cast<float*>(lds + kFW4);
-  uint8_t* A1s = lds + kFA1;
-  __bf16* A2s = reinterpret_cast<__bf16*>(lds + kFA2);
-  uint8_t* D0u = lds + kFD0;  // img49 image
-  float* Hs = reinterpret_cast<float*>(lds + kFH);
-  __bf16* Zs = reinterpret_cast<__bf16*>(lds + kFZ);
-  float* Red = reinterpret_cast<float*>(lds + kFRed);
-  float* Scr = reinterpret_cast<float*>(lds + kFScr);
-  uint8_t* W3s = lds + kFW3;
-  __bf16* D1s = reinterpret_cast<__bf16*>(lds + kFA1);  // aliases A1s (dead after enc2)
+struct FwdLayout {
+  static constexpr int X = kFX, W1 = kFW1, W4 = kFW4, A1 = kFA1, A2 = kFA2, D0 = kFD0, H = kFH, Z = kFZ;
+  static constexpr int Red = kFRed, Scr = kFScr, IMG = kFW3, Dummy = kFDummy, Bd = kFBd;
+  static constexpr int G = -1;  // dlogits stay in global memory only
+  static constexpr int LDS = kFLds;
+};
+
+template <class L>
+__device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
+  float* Xs = reinterpret_cast<float*>(lds + L::X);
+  float* W1s = reinterpret_cast<float*>(lds + L::W1);
+  float* W4s = reinterpret_cast<float*>(lds + L::W4);
+  uint8_t* A1s = lds + L::A1;
+  __bf16* A2s = reinterpret_cast<__bf16*>(lds + L::A2);
+  uint8_t* D0u = lds + L::D0;  // img49 image
+  float* Hs = reinterpret_cast<float*>(lds + L::H);
+  __bf16* Zs = reinterpret_cast<__bf16*>(lds + L::Z);
+  float* Scr = reinterpret_cast<float*>(lds + L::Scr);
+  uint8_t* W3s = lds + L::IMG;
+  __bf16* D1s = reinterpret_cast<__bf16*>(lds + L::A1);  // aliases A1s (dead after enc2)
 
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -329,7 +335,7 @@ __global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
       const int off = r * kSlice + k * 1024 + lane * 16;
       const uint8_t* src = off < kWh ? reinterpret_cast<const uint8_t*>(W.Wh) + off
                                      : reinterpret_cast<const uint8_t*>(W.Wd) + (off - kWh < kWd ? off - kWh : 0);
-      glds16(src, lds + kFDummy + w * 1024);
+      glds16(src, lds + L::Dummy + w * 1024);
     }
   }
   {
@@ -344,7 +350,7 @@ __global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
     W1s[t * 32 + c] = W.W1f[tid];
     W4s[t * 32 + c] = W.W4f[tid];
     for (int e = tid; e < kFlat / 4; e += kThreads)
-      reinterpret_cast<float4*>(lds + kFBd)[e] = reinterpret_cast<const float4*>(W.bd)[e];
+      reinterpret_cast<float4*>(lds + L::Bd)[e] = reinterpret_cast<const float4*>(W.bd)[e];
   }
   stage_conv_image(W.W2, W3s);  // enc2 weights first; dec1's tap images replace them after P2
   __syncthreads();
@@ -481,7 +487,7 @@ __global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
             const f32x4 acc = mfma_bf16(av, b, f32x4{0.f, 0.f, 0.f, 0.f});
             if (lane < 16) {
               const int jj = 16 * t + lane;
-              const __bf16 o = (__bf16)fmaxf(acc[0] + reinterpret_cast<const float*>(lds + kFBd)[jj], 0.f);
+              const __bf16 o = (__bf16)fmaxf(acc[0] + reinterpret_cast<const float*>(lds + L::Bd)[jj], 0.f);
               *reinterpret_cast<__bf16*>(D0u + img49e(jj >> 6, jj & 63)) = o;
               if (a.train) a.d0[(size_t)n * kFlat + jj] = o;
             }
@@ -538,6 +544,7 @@ __global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
     loss += x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
     gsum += g;
     if (a.train) a.dlog[(size_t)n * 784 + pix] = g;
+    if constexpr (L::G >= 0) reinterpret_cast<float*>(lds + L::G)[pix] = g;  // the merged step's backward
     if (a.recon) a.recon[(size_t)n * 784 + pix] = p;
   }
   loss = wave_sum(loss);
@@ -561,6 +568,11 @@ __global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
   stamp(a.stamps, 8);
 }
 
+__global__ void __launch_bounds__(kThreads) f28_fwd_k(FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[FwdLayout::LDS];
+  fwd_body<FwdLayout>(a, lds);
+}
+
 // ----------------------------------------------------------------- backward
 constexpr int kBG = 0;                      // f32 [784] dlogits
 constexpr int kBW4 = kBG + 784 * 4;         // f32 [16][32] dec2 weights, tap-major
@@ -577,19 +589,30 @@ constexpr int kBLds = kBCSB + 32 * 197 * 4;
 static_assert(kBGD1 % 16 == 0 && kBGD0 % 16 == 0 && kBGA2 % 16 == 0 && kBGA2F % 16 == 0 && kBW2 % 16 == 0,
               "LDS alignment");
 
-__global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kBLds];
-  float* Gs = reinterpret_cast<float*>(lds + kBG);
-  float* W4s = reinterpret_cast<float*>(lds + kBW4);
-  uint8_t* GD1s = lds + kBGD1;
-  __bf16* GD0s = reinterpret_cast<__bf16*>(lds + kBGD0);
-  float* DMs = reinterpret_cast<float*>(lds + kBDM);
-  float* DZR = reinterpret_cast<float*>(lds + kBDZR);
-  uint8_t* GA2u = lds + kBGA2;  // img49 image
-  float* GA2F = reinterpret_cast<float*>(lds + kBGA2F);
-  float* CS = reinterpret_cast<float*>(lds + kBCS);
-  uint8_t* W2s = lds + kBW2;
-  float* CSB = reinterpret_cast<float*>(lds + kBCSB);
+struct BwdLayout {
+  static constexpr int G = kBG, W4 = kBW4, GD1 = kBGD1, GD0 = kBGD0, DM = kBDM, DZR = kBDZR, GA2 = kBGA2;
+  static constexpr int GA2F = kBGA2F, CS = kBCS, IMG = kBW2, CSB = kBCSB, LDS = kBLds;
+  static constexpr int D1 = -1, D0 = -1, A2 = -1;  // masks come from global memory
+};
+
+// MERGED: the backward runs in the forward's workgroup right after it (one
+// launch per step) and takes from LDS what the forward left there: the
+// dlogits (L::G), dec2 weights (W4), dec1's tap images (IMG; Q2 reads its
+// conv-layout B fragments straight out of them), and the ReLU masks d1
+// (A1 region), d0 (img49 D0 region) and a2 (A2 region).
+template <class L, bool MERGED>
+__device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
+  float* Gs = reinterpret_cast<float*>(lds + L::G);
+  float* W4s = reinterpret_cast<float*>(lds + L::W4);
+  uint8_t* GD1s = lds + L::GD1;
+  __bf16* GD0s = reinterpret_cast<__bf16*>(lds + L::GD0);
+  float* DMs = reinterpret_cast<float*>(lds + L::DM);
+  float* DZR = reinterpret_cast<float*>(lds + L::DZR);
+  uint8_t* GA2u = lds + L::GA2;  // img49 image
+  float* GA2F = reinterpret_cast<float*>(lds + L::GA2F);
+  float* CS = reinterpret_cast<float*>(lds + L::CS);
+  uint8_t* W2s = lds + L::IMG;
+  float* CSB = reinterpret_cast<float*>(lds + L::CSB);
 
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -597,13 +620,15 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
   stamp(a.stamps, 0);
 
   // ---- Q0: dlogits, dec2 weights, dec1 B fragments (conv layout), enc2 tap images
-  if (tid < 196) reinterpret_cast<float4*>(Gs)[tid] = reinterpret_cast<const float4*>(a.dlog + (size_t)n * 784)[tid];
-  {
-    const int c = tid >> 4, t = tid & 15;
-    W4s[t * 32 + c] = W.W4f[tid];
+  if constexpr (!MERGED) {
+    if (tid < 196) reinterpret_cast<float4*>(Gs)[tid] = reinterpret_cast<const float4*>(a.dlog + (size_t)n * 784)[tid];
+    {
+      const int c = tid >> 4, t = tid & 15;
+      W4s[t * 32 + c] = W.W4f[tid];
+    }
+    stage_conv_image(W.W3, W2s);  // dec1 weights (conv layout) first; enc2's tap images after Q2
+    __syncthreads();
   }
-  stage_conv_image(W.W3, W2s);  // dec1 weights (conv layout) first; enc2's tap images after Q2
-  __syncthreads();
 
   stamp(a.stamps, 1);
   // ---- Q1: dec2 backward-data (conv 1 -> 32 on the dlogits, 28 -> 14) x dec1 ReLU mask
@@ -616,7 +641,9 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
       // the dec1 ReLU mask, loaded before the FMAs so its latency overlaps them
       bf16x8 mk[4];
 #pragma unroll
-      for (int ch = 0; ch < 4; ++ch) mk[ch] = reinterpret_cast<const bf16x8*>(a.d1 + ((size_t)n * 196 + tid) * 32)[ch];
+      for (int ch = 0; ch < 4; ++ch)
+        mk[ch] = MERGED ? reinterpret_cast<const bf16x8*>(lds + L::D1 + tid * 64)[ch]
+                        : reinterpret_cast<const bf16x8*>(a.d1 + ((size_t)n * 196 + tid) * 32)[ch];
 #pragma unroll 2
       for (int t = 0; t < 16; ++t) {
         const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
@@ -666,8 +693,17 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
 
   stamp(a.stamps, 2);
   // ---- Q2: dec1 backward-data (conv 32 -> 64 with the convT weights, 14 -> 7) x dec_fc ReLU mask
-  conv14to7(GD1s, [&](int j, int t) { return conv_bfrag(W2s, j, t, lane); },
-            [&](int p, int col) { return (float)a.d0[(size_t)n * kFlat + p * 64 + col]; },
+  conv14to7(GD1s,
+            [&](int j, int t) {
+              if constexpr (MERGED)  // dec1's per-tap image t: row c64 = 16 j + (l & 15), chunk l >> 4
+                return *reinterpret_cast<const bf16x8*>(W2s + t * 4096 + timg<32>(16 * j + (lane & 15), lane >> 4));
+              else
+                return conv_bfrag(W2s, j, t, lane);
+            },
+            [&](int p, int col) {
+              if constexpr (MERGED) return (float)*reinterpret_cast<const __bf16*>(lds + L::D0 + img49e(p, col));
+              else return (float)a.d0[(size_t)n * kFlat + p * 64 + col];
+            },
             [&](int p, int col, float v, float mask) {
     const size_t e = (size_t)n * kFlat + p * 64 + col;
     const float g = mask > 0.f ? v : 0.f;
@@ -751,7 +787,8 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
 #pragma unroll
                      for (int e = 0; e < 8; ++e) acc[e] = fmaf(dm, (float)wv[e], acc[e]);
                    });
-    const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.a2 + (size_t)n * kFlat + k0);
+    const bf16x8 mk = MERGED ? *reinterpret_cast<const bf16x8*>(lds + L::A2 + 2 * k0)
+                             : *reinterpret_cast<const bf16x8*>(a.a2 + (size_t)n * kFlat + k0);
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -794,6 +831,53 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
     a.db1_part[(size_t)n * 32 + tid] = s;
   }
   stamp(a.stamps, 7);
+}
+
+__global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[BwdLayout::LDS];
+  bwd_body<BwdLayout, false>(a, lds);
+}
+
+// ------------------------------------------------------- merged step (one launch)
+// One LDS map for both halves; backward regions alias forward regions that are
+// dead by then (noted per line). dec1's tap images stay in IMG from P5 to Q2,
+// then enc2's tap images replace them for Q6.
+struct StepLayout {
+  static constexpr int IMG = 0;                  // 64 KB: W2 conv image (P0-P2), W3 taps (P5-Q2), W2 taps (Q6)
+  static constexpr int W1 = IMG + 65536;         // f32 [16][32]
+  static constexpr int CS = W1;                  //   bwd colsum scratch (W1 dead after P1)
+  static constexpr int W4 = W1 + 512 * 4;        // f32 [16][32], both halves
+  static constexpr int X = W4 + 512 * 4;         // f32 [784]
+  static constexpr int DM = X;                   //   bwd d[mu|lv] (X dead after P7)
+  static constexpr int DZR = X + 64 * 4;         //   bwd dz partials
+  static constexpr int G = X + 784 * 4;          // f32 [784] dlogits (P7 -> Q1)
+  static constexpr int A1 = G + 784 * 4;         // bf16 img14: enc1 out, then dec1 out (Q1 mask)
+  static constexpr int D1 = A1;
+  static constexpr int GA2F = A1;                //   bwd f32 [3136] (A1/D1 dead after Q1)
+  static constexpr int A2 = A1 + kFlat * 4;      // bf16 [3136] enc2 out (P3 input, Q5 mask)
+  static constexpr int D0 = A2 + kFlat * 2;      // bf16 img49 dec_fc out (P6 input, Q2 mask)
+  static constexpr int GA2 = D0;                 //   bwd img49 (D0 dead after Q2)
+  static constexpr int H = D0 + kFlat * 2;       // f32 [64]
+  static constexpr int Z = H + 64 * 4;           // bf16 [32]
+  static constexpr int Red = Z + 64;
+  static constexpr int Scr = Red + 64 * 4;       // f32 [32]
+  static constexpr int Dummy = Scr + 32 * 4;     // 8 KB DMA landing zone
+  static constexpr int GD0 = Dummy;              //   bwd bf16 [3136]
+  static constexpr int Bd = Dummy + 8192;        // f32 [3136] dec_fc bias (P5 only)
+  static constexpr int GD1 = Bd;                 //   bwd bf16 img14
+  static constexpr int CSB = Bd + kFlat * 4;     // f32 [32][197]
+  static constexpr int LDS = CSB + 32 * 197 * 4;
+  static_assert(W1 % 16 == 0 && X % 16 == 0 && G % 16 == 0 && A1 % 16 == 0 && A2 % 16 == 0 && D0 % 16 == 0 &&
+                    Dummy % 16 == 0 && Bd % 16 == 0 && CSB % 16 == 0 && LDS <= 160 * 1024,
+                "step LDS map");
+  static_assert(196 * 64 <= kFlat * 4 && 64 * 4 + 256 * 4 <= 784 * 4 && kFlat * 2 <= 8192, "step LDS aliases");
+};
+
+__global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[StepLayout::LDS];
+  fwd_body<StepLayout>(fa, lds);
+  __syncthreads();
+  bwd_body<StepLayout, true>(ba, lds);
 }
 
 }  // namespace f28
@@ -864,9 +948,41 @@ int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train
   return (int)hipGetLastError();
 }
 
-int mdt_f28_backward(const long long* p, int M, hipStream_t s) {
-  if (M <= 0) return 1;
-  f28::BwdArgs a{};
+static void fill_bwd(f28::BwdArgs& a, const long long* p);
+
+// One launch per training step: forward then backward in the same workgroup.
+int mdt_f28_step(const long long* pf, const long long* pb, int B, int M, unsigned stream, hipStream_t s) {
+  if (M <= 0 || M > B) return 1;
+  f28::FwdArgs fa{};
+  fill_weights(fa.w, pf);
+  fa.X = P<const float>(pf, 12);
+  fa.idx = P<const int>(pf, 13);
+  fa.st = P<const TrainState>(pf, 14);
+  fa.hp = P<const HParams>(pf, 15);
+  fa.B = B;
+  fa.stream = stream;
+  fa.train = 1;
+  fa.xb = P<float>(pf, 16);
+  fa.a1 = P<__bf16>(pf, 17);
+  fa.a2 = P<__bf16>(pf, 18);
+  fa.mulv = P<float>(pf, 19);
+  fa.eps = P<float>(pf, 20);
+  fa.z16 = P<__bf16>(pf, 21);
+  fa.d0 = P<__bf16>(pf, 22);
+  fa.d1 = P<__bf16>(pf, 23);
+  fa.dlog = P<float>(pf, 24);
+  fa.recon = P<float>(pf, 25);
+  fa.bce_part = P<float>(pf, 26);
+  fa.kld_part = P<float>(pf, 27);
+  fa.db4_part = P<float>(pf, 28);
+  fa.stamps = P<unsigned long long>(pf, 29);
+  f28::BwdArgs ba{};
+  fill_bwd(ba, pb);
+  hipLaunchKernelGGL(f28::f28_step_k, dim3(M), dim3(f28::kThreads), 0, s, fa, ba);
+  return (int)hipGetLastError();
+}
+
+static void fill_bwd(f28::BwdArgs& a, const long long* p) {
   fill_weights(a.w, p);
   a.hp = P<const HParams>(p, 12);
   a.mulv = P<const float>(p, 13);
@@ -887,6 +1003,12 @@ int mdt_f28_backward(const long long* p, int M, hipStream_t s) {
   a.db2_part = P<float>(p, 28);
   a.db1_part = P<float>(p, 29);
   a.stamps = P<unsigned long long>(p, 30);
+}
+
+int mdt_f28_backward(const long long* p, int M, hipStream_t s) {
+  if (M <= 0) return 1;
+  f28::BwdArgs a{};
+  fill_bwd(a, p);
   hipLaunchKernelGGL(f28::f28_bwd_k, dim3(M), dim3(f28::kThreads), 0, s, a);
   return (int)hipGetLastError();
 }

@@ -68,6 +68,7 @@ int mdt_pack_jobs_multi(const mdt::JobBlob* jobs, int n, void* dst);
 int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s);
 int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train, hipStream_t s);
 int mdt_f28_backward(const long long* p, int M, hipStream_t s);
+int mdt_f28_step(const long long* pf, const long long* pb, int B, int M, unsigned stream, hipStream_t s);
 int mdt_launch_job1(const mdt::JobBlob* j, hipStream_t s);
 int mdt_launch_tail(const mdt::JobBlob* wg, const mdt::JobBlob* fin0, const mdt::JobBlob* finr, int* ticket,
                     hipStream_t s);
@@ -419,8 +420,7 @@ const std::vector<Slot>& f28_weight_slots() {
 }
 }  // namespace
 
-void f28_forward(const std::vector<c10::optional<at::Tensor>>& t, int64_t B, int64_t M, int64_t stream, bool train) {
-  TORCH_CHECK(M > 0 && M <= B, "f28_forward: bad M ", M, " for B ", B);
+std::vector<Slot> f28_fwd_slots(int64_t B, bool train) {
   std::vector<Slot> slots = f28_weight_slots();
   const std::vector<Slot> rest = {
       {"X", 'f', 784, true, false},        {"idx", 'i', B, true, false},
@@ -431,13 +431,10 @@ void f28_forward(const std::vector<c10::optional<at::Tensor>>& t, int64_t B, int
       {"recon", 'f', 784, false, true},    {"bce_part", 'f', 1, false, false}, {"kld_part", 'f', 1, false, false},
       {"db4_part", 'f', 1, false, true},   {"stamps", 'l', 16, false, true}};
   slots.insert(slots.end(), rest.begin(), rest.end());
-  const int dev = t[0].has_value() ? (int)t[0]->device().index() : 0;
-  const auto p = f28_ptrs(t, slots, M, dev);
-  rc(mdt_f28_forward(p.data(), (int)B, (int)M, (unsigned)stream, train ? 1 : 0, cur()), "f28_forward");
+  return slots;
 }
 
-void f28_backward(const std::vector<c10::optional<at::Tensor>>& t, int64_t M) {
-  TORCH_CHECK(M > 0, "f28_backward: bad M");
+std::vector<Slot> f28_bwd_slots() {
   std::vector<Slot> slots = f28_weight_slots();
   const std::vector<Slot> rest = {
       {"hparams", 'u', (int64_t)sizeof(HParams), true, false},
@@ -449,9 +446,31 @@ void f28_backward(const std::vector<c10::optional<at::Tensor>>& t, int64_t M) {
       {"db2_part", 'f', 64, false, false}, {"db1_part", 'f', 32, false, false},
       {"stamps", 'l', 16, false, true}};
   slots.insert(slots.end(), rest.begin(), rest.end());
+  return slots;
+}
+
+void f28_forward(const std::vector<c10::optional<at::Tensor>>& t, int64_t B, int64_t M, int64_t stream, bool train) {
+  TORCH_CHECK(M > 0 && M <= B, "f28_forward: bad M ", M, " for B ", B);
   const int dev = t[0].has_value() ? (int)t[0]->device().index() : 0;
-  const auto p = f28_ptrs(t, slots, M, dev);
+  const auto p = f28_ptrs(t, f28_fwd_slots(B, train), M, dev);
+  rc(mdt_f28_forward(p.data(), (int)B, (int)M, (unsigned)stream, train ? 1 : 0, cur()), "f28_forward");
+}
+
+void f28_backward(const std::vector<c10::optional<at::Tensor>>& t, int64_t M) {
+  TORCH_CHECK(M > 0, "f28_backward: bad M");
+  const int dev = t[0].has_value() ? (int)t[0]->device().index() : 0;
+  const auto p = f28_ptrs(t, f28_bwd_slots(), M, dev);
   rc(mdt_f28_backward(p.data(), (int)M, cur()), "f28_backward");
+}
+
+// Forward + backward of one training step in ONE launch (f28_step_k).
+void f28_step(const std::vector<c10::optional<at::Tensor>>& tf, const std::vector<c10::optional<at::Tensor>>& tb,
+              int64_t B, int64_t M, int64_t stream) {
+  TORCH_CHECK(M > 0 && M <= B, "f28_step: bad M ", M, " for B ", B);
+  const int dev = tf[0].has_value() ? (int)tf[0]->device().index() : 0;
+  const auto pf = f28_ptrs(tf, f28_fwd_slots(B, true), M, dev);
+  const auto pb = f28_ptrs(tb, f28_bwd_slots(), M, dev);
+  rc(mdt_f28_step(pf.data(), pb.data(), (int)B, (int)M, (unsigned)stream, cur()), "f28_step");
 }
 
 void step_begin(at::Tensor state, const at::Tensor& hparams) {
@@ -653,6 +672,8 @@ void bind_conv(pybind11::module& m) {
   m.def("f28_forward", &f28_forward, py::arg("tensors"), py::arg("B"), py::arg("M"), py::arg("stream"),
         py::arg("train"));
   m.def("f28_backward", &f28_backward, py::arg("tensors"), py::arg("M"));
+  m.def("f28_step", &f28_step, py::arg("fwd_tensors"), py::arg("bwd_tensors"), py::arg("B"), py::arg("M"),
+        py::arg("stream"));
   m.def("launch_tail", &launch_tail);
   m.def("igemm", &igemm, py::arg("mode"), py::arg("A"), py::arg("B16"), py::arg("desc"), py::arg("bias"),
         py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),
@@ -683,6 +704,12 @@ void bind_conv(pybind11::module& m) {
   m.def("make_grad_units", &make_grad_units);
   m.def("make_tr_units", &make_tr_units);
   m.def("adam_cast", &adam_cast);
+  m.def("graph_upload", [](int64_t exec) {
+    // Upload an instantiated step graph to the device ahead of its first
+    // replay, so that launch's one-time cost stays out of a timed region.
+    TORCH_CHECK(exec != 0, "graph_upload: null graph exec");
+    rc((int)hipGraphUpload(reinterpret_cast<hipGraphExec_t>((intptr_t)exec), cur()), "hipGraphUpload");
+  });
   m.def("grad_finalize", &grad_finalize, py::arg("P"), py::arg("G"), py::arg("M"), py::arg("V"), py::arg("w16"),
         py::arg("segs"), py::arg("units"), py::arg("nunits"), py::arg("state"), py::arg("hparams"),
         py::arg("do_adam"), py::arg("job") = py::none());

@@ -265,6 +265,8 @@ class ConvVaeTrainer:
                     and os.getenv("MDT_CONV_F28", "1") != "0")
         self._plans28 = {}
         self.f28_skip_adam = False  # tests: leave the reduced gradients in `grads`, no update
+        # forward and backward of the fused step in one launch (MDT_F28_MERGE=0: two)
+        self.f28_merge = os.getenv("MDT_F28_MERGE", "1") != "0"
         # profiling: int64 [B*16] tensors (fwd, bwd) receiving per-workgroup
         # phase-end s_memrealtime stamps (obs/f28_phases.py); None = off
         self.f28_stamps = (None, None)
@@ -1039,12 +1041,16 @@ class ConvVaeTrainer:
         return p
 
     def _step28(self, M):
-        """Fused 28x28 step: forward || backward-data || weight gradients +
-        loss/step || finalize + Adam, 4 launches (DDP: finalize without Adam,
-        bucket all-reduce, then Adam + bf16 cast)."""
+        """Fused 28x28 step: forward + backward-data (one launch: f28_step_k,
+        or two with MDT_F28_MERGE=0) || weight gradients + loss/step ||
+        finalize + Adam (DDP: finalize without Adam, bucket all-reduce, then
+        Adam + bf16 cast)."""
         C, p, st = self.C, self._plan28(M), self.state
-        C.f28_forward(p["fwd"], self.B, M, self.rng_stream, True)
-        C.f28_backward(p["bwd"], M)
+        if self.f28_merge:
+            C.f28_step(p["fwd"], p["bwd"], self.B, M, self.rng_stream)
+        else:
+            C.f28_forward(p["fwd"], self.B, M, self.rng_stream, True)
+            C.f28_backward(p["bwd"], M)
         C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
         red = self.reducer
         C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
@@ -1243,6 +1249,7 @@ class ConvVaeTrainer:
         for t, v in zip((self.params, self.exp_avg, self.exp_avg_sq, self.state.train_state), snap):
             t.copy_(v)
         self._cast_weights()
+        native.upload_graph(g)
         return g
 
     @torch.no_grad()

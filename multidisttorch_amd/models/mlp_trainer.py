@@ -314,6 +314,7 @@ class MlpVaeTrainer:
                 self._step_hip(M)
         for t, v in zip((self.params, self.exp_avg, self.exp_avg_sq, self.engine.train_state), snap):
             t.copy_(v)
+        native.upload_graph(g)
         return g
 
     # ------------------------------------------------------------------ eval / sample

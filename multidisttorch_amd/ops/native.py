@@ -76,3 +76,11 @@ def ensure_built(jobs: int = 8):
 def gpu_backend_default() -> str:
     """'hip' when a GPU is visible (extension mandatory), else 'torch'."""
     return "hip" if torch.cuda.is_available() else "torch"
+
+
+def upload_graph(g) -> None:
+    """hipGraphUpload a captured torch CUDAGraph (its one-time upload then
+    happens here, not inside the first -- possibly timed -- replay)."""
+    exec_ptr = int(g.raw_cuda_graph_exec())
+    if exec_ptr:
+        require().graph_upload(exec_ptr)

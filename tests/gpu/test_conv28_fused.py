@@ -168,6 +168,33 @@ def test_f28_eager_equals_graph_and_trains(native_ext):
     assert np.isfinite(total) and first.shape == (128, 784)
 
 
+@pytest.mark.parametrize("M", [128, 77])
+def test_f28_merged_step_is_bitwise_two_launches(M, native_ext):
+    """f28_step_k (forward + backward in one workgroup, masks / dlogits / dec1
+    taps taken from LDS) computes exactly what the two-launch forward then
+    backward computes: same losses, weights, Adam moments and every backward
+    output, eager and graph-replayed."""
+    from multidisttorch_amd.data.datasets import synthetic_images
+
+    dev = torch.device("cuda")
+    X = synthetic_images(1024, device=dev)
+    idx = torch.arange(1024, device=dev, dtype=torch.int32)
+    res = []
+    for merge, graphs in ((False, False), (True, False), (True, True)):
+        tr = _trainer(seed=6, use_graphs=graphs, graph_steps=3)
+        tr.f28_merge = merge
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 8)
+        tr.train_steps(6, M=M)
+        torch.cuda.synchronize()
+        res.append((tr.loss_history()[:6].copy(), tr.params.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone(),
+                    {k: v.clone() for k, v in tr.gacts.items()}, tr.dmulv.clone()))
+    for h, p, m, v, ga, dm in res[1:]:
+        np.testing.assert_array_equal(h, res[0][0])
+        assert torch.equal(p, res[0][1]) and torch.equal(m, res[0][2]) and torch.equal(v, res[0][3])
+        assert all(torch.equal(ga[k], res[0][4][k]) for k in ga) and torch.equal(dm, res[0][5])
+
+
 def test_f28_adam_matches_torch_optim(native_ext):
     """The finalize + fused Adam of the fused step against torch.optim.Adam
     fed with the kernel's own gradients, over 3 steps (lr, betas, eps, bias
