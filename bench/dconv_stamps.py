@@ -17,7 +17,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-CASES = [(0, 64, 32, 32, 64), (0, 32, 64, 16, 128), (1, 32, 64, 16, 128), (1, 64, 32, 32, 64)]
+CASES = [(0, 64, 32, 32, 64), (0, 32, 64, 16, 128), (1, 32, 64, 16, 128), (1, 64, 32, 32, 64),
+         (0, 16, 128, 8, 256), (1, 16, 128, 8, 256)]
 
 
 def main():
@@ -34,7 +35,7 @@ def main():
     out = {}
     for mode, H, Cc, OH, CO in CASES:
         d = [N, H, H, Cc, OH, OH, CO, 4, 4, 2, 1]
-        info = C.igemm_plan(mode, d, False)
+        info = C.igemm_plan(mode, d, False, fwd=True)
         if mode == 0:
             A = torch.randn(N * H * H * Cc, device=dev).bfloat16()
             B = torch.randn(CO * 16 * Cc, device=dev).bfloat16()
@@ -47,7 +48,7 @@ def main():
             ncols = Cc
         y16 = torch.empty(ny, device=dev, dtype=torch.bfloat16)
         bias = torch.zeros(ncols, device=dev)
-        run = lambda: C.igemm(mode, A, B, d, bias, True, y16, None)
+        run = lambda: C.igemm(mode, A, B, d, bias, True, y16, None, fwd=True)
         for _ in range(5):
             run()
         torch.cuda.synchronize()

@@ -55,9 +55,19 @@ struct DcInfo {
 template <class CF>
 constexpr DcInfo dc_info() { return DcInfo{CF::RB, CF::NBB, CF::MT, CF::NB}; }
 static const DcInfo kDcInfo[] = {dc_info<DcS1>(),  dc_info<DcS2>(),  dc_info<DcT2>(),  dc_info<DcT3>(),
-                                  dc_info<DcS1b>(), dc_info<DcS2b>(), dc_info<DcT2b>(), dc_info<DcT3b>()};
+                                  dc_info<DcS1b>(), dc_info<DcS2b>(), dc_info<DcT2b>(), dc_info<DcT3b>(),
+                                  dc_info<DcS3>(),  dc_info<DcT1>()};
 
-int direct_cfg(int mode, const ConvDesc& d) {
+// the 16x16 <-> 8x8 geometries (MDT_DCONV_SMALL=0 keeps them on im2col)
+static bool direct_small() {
+  static const bool on = [] {
+    const char* e = getenv("MDT_DCONV_SMALL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int direct_cfg(int mode, const ConvDesc& d, bool fwd) {
   static const bool on = [] {
     const char* e = getenv("MDT_CONV_DIRECT");
     return !(e && e[0] == '0');
@@ -69,21 +79,31 @@ int direct_cfg(int mode, const ConvDesc& d) {
     const char* e = getenv("MDT_DCONV_ALT");
     return e && e[0] == '0' ? 0 : 4;
   }();
+  // MDT_DCONV_BWD=0: forward calls only (backward-data keeps the fusable im2col kernel)
+  static const bool bwd = [] {
+    const char* e = getenv("MDT_DCONV_BWD");
+    return !(e && e[0] == '0');
+  }();
   if (!on || d.KH != 4 || d.KW != 4 || d.S != 2 || d.P != 1) return -1;
+  if (!fwd && !bwd) return -1;
   if (d.H != d.W || d.OH != d.OW || d.H != 2 * d.OH) return -1;
   if (mode == kModeConv) {  // A = input (H, C), columns = CO
     if (d.C == 32 && d.H == 64 && d.CO == 64) return 0 + alt;
     if (d.C == 64 && d.H == 32 && d.CO == 128) return 1 + alt;
+    // 16x16 -> 8x8: forward only; as a backward-data GEMM the im2col kernel
+    // fuses with the weight gradient in one launch, which measured faster
+    if (d.C == 128 && d.H == 16 && d.CO == 256 && fwd && direct_small()) return 8;
   } else {  // A = conv output (OH, CO), columns = C
     if (d.CO == 128 && d.OH == 16 && d.C == 64) return 2 + alt;
     if (d.CO == 64 && d.OH == 32 && d.C == 32) return 3 + alt;
+    if (d.CO == 256 && d.OH == 8 && d.C == 128 && fwd && direct_small()) return 9;
   }
   return -1;
 }
 
-bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p, bool allow_direct) {
+bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p, bool allow_direct, bool fwd) {
   FwdPlan q{};
-  const int dc = allow_direct ? direct_cfg(mode, d) : -1;
+  const int dc = allow_direct ? direct_cfg(mode, d, fwd) : -1;
   if (dc >= 0) {
     const DcInfo& di = kDcInfo[dc];
     q.direct = dc + 1;
@@ -326,6 +346,8 @@ int launch_direct(int cfg, const void* A, const void* B16, const ConvDesc& d, co
     case 5: launch_dc<DcS2b>(a, s); break;
     case 6: launch_dc<DcT2b>(a, s); break;
     case 7: launch_dc<DcT3b>(a, s); break;
+    case 8: launch_dc<DcS3>(a, s); break;
+    case 9: launch_dc<DcT1>(a, s); break;
     default: return 2;
   }
   return (int)hipGetLastError();
@@ -408,9 +430,9 @@ void launch_wg(const WgArgs& a, const WgradPlan& q, hipStream_t s) {
 extern "C" {
 
 // info[12] = {cfg, BM, BN, classes, M, Ncols, K, mtiles, ntiles, ktiles, ksplit, colsum_rows}
-int mdt_igemm_plan(int mode, ConvDesc d, int allow_split, int* info) {
+int mdt_igemm_plan(int mode, ConvDesc d, int allow_split, int* info, int fwd) {
   FwdPlan q;
-  if (!plan_fwd(mode, d, allow_split != 0, &q)) return 1;
+  if (!plan_fwd(mode, d, allow_split != 0, &q, true, fwd != 0)) return 1;
   const int v[12] = {q.cfg, q.BM, q.BN, q.classes, q.M, q.Ncols, q.K, q.mtiles, q.ntiles, q.ktiles, q.ksplit,
                      q.colsum_rows};
   for (int i = 0; i < 12; ++i) info[i] = v[i];
@@ -431,12 +453,12 @@ int mdt_wgrad_plan(ConvDesc d, int* info) {
 // pass; omask/colsum are not allowed with split-K).
 int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d, const float* bias, int relu,
               void* y16, float* y32, const void* omask, float* colsum, float* ws, int skip_combine, hipStream_t s,
-              const APro* pro) {
+              const APro* pro, int fwd) {
   IgArgs a;
   FwdPlan q;
   CombineArgs c;
   int nc = 0;
-  const int dc = direct_cfg(mode, d);
+  const int dc = direct_cfg(mode, d, fwd != 0);
   if (dc >= 0) {  // the planner reported the direct tiling: never fall back silently
     if ((pro && pro->slab) || a_is_f32) return 5;
     return launch_direct(dc, A, B16, d, bias, relu, y16, y32, omask, colsum, s);

@@ -1082,8 +1082,9 @@ using W5 = TileCfg<32, 16, 2, 1>;
 
 // Host-side builders shared by the stand-alone entry points (conv_igemm.hip)
 // and the job builders (conv_jobs.hip).
-bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p, bool allow_direct = true);
-int direct_cfg(int mode, const ConvDesc& d);
+bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p, bool allow_direct = true,
+              bool fwd = false);
+int direct_cfg(int mode, const ConvDesc& d, bool fwd);
 bool plan_wgrad(const ConvDesc& d, WgradPlan* p);
 bool use_glds();
 // Kernel arguments of one forward-type GEMM; with split-K (q->ksplit > 1) `c`

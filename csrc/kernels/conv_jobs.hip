@@ -358,7 +358,7 @@ int mdt_job_igemm(JobBlob* g, JobBlob* c, int mode, const void* A, int a_is_f32,
   memset(c, 0, sizeof(*c));
   // direct-kernel geometries have no job form yet: kind 0 sends the caller
   // to mdt_igemm (their column-sum rows follow the direct plan)
-  const bool ok = !a_is_f32 && !q.thin && !use_glds() && direct_cfg(mode, d) < 0;
+  const bool ok = !a_is_f32 && !q.thin && !use_glds() && direct_cfg(mode, d, false) < 0;
   g->kind = ok ? kJobIgemm + mode * 100 + q.cfg : 0;
   g->nblk = q.mtiles * q.ntiles * q.ksplit * q.classes;
   g->aux[0] = q.mtiles * q.ntiles;

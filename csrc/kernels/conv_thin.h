@@ -374,4 +374,120 @@ __device__ __forceinline__ void thin_tconv4_body(const ThinTconvArgs& ta, uint8_
   }
 }
 
+// Halo-patch variant of thin_tconv4 (the default where it applies: CO = 32,
+// class grid WS columns with WS | 256). One workgroup = one image's R = 256 / WS
+// class-grid rows x all WS columns, one thread per class pixel (all four
+// parity outputs). The (R+2) x (WS+2) x CO bf16 neighbourhood is staged in LDS
+// once with contiguous 16-B row loads (zero padding materialised), instead of
+// every thread gathering its own 3x3 neighbourhood through the TA (each input
+// chunk 9/4 times: 151 MB of 16-B gathers per 128x128 B=64 step, TA-bound at
+// ~25 us). Chunk q of slot x sits at q ^ ((x >> 2) & 3): the 16 consecutive
+// slots a lane group reads land on 16 different bank groups. Same arithmetic
+// order as thin_tconv4_body, same fused BCE / dlogits / partials.
+template <int CO, int WS>
+constexpr int thin_tconv_patch_lds_bytes() { return (256 / WS + 2) * (WS + 2) * CO * 2 + (16 * CO + 16) * 4; }
+
+template <int CO, int WS>
+__device__ __forceinline__ void thin_tconv_patch_body(const ThinTconvArgs& ta, uint8_t* lds, int bid) {
+  static_assert(CO == 32 && 256 % WS == 0, "thin_tconv_patch: CO = 32, WS | 256");
+  constexpr int R = 256 / WS, PC = WS + 2, NCH = CO / 8, PB = CO * 2;
+  const ConvDesc& d = ta.d;
+  const int rbn = d.OH / R;
+  const int n = bid / rbn, j0 = (bid - n * rbn) * R;
+  uint8_t* patch = lds;
+  float* wl = reinterpret_cast<float*>(lds + (R + 2) * PC * PB);
+  float* scratch = wl + 16 * CO;
+  const __bf16* Gn = ta.G + (size_t)n * d.OH * d.OW * CO;
+  for (int e = threadIdx.x; e < (R + 2) * PC * NCH; e += blockDim.x) {
+    const int pix = e / NCH, q = e - (e / NCH) * NCH;
+    const int y = pix / PC, x = pix - (pix / PC) * PC;
+    const int gy = j0 - 1 + y, gx = x - 1;
+    bf16x8 v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (__bf16)0.f;
+    if ((unsigned)gy < (unsigned)d.OH && (unsigned)gx < (unsigned)d.OW)
+      v = *reinterpret_cast<const bf16x8*>(Gn + ((size_t)gy * d.OW + gx) * CO + 8 * q);
+    *reinterpret_cast<bf16x8*>(patch + pix * PB + 16 * (q ^ ((x >> 2) & 3))) = v;
+  }
+  for (int e = threadIdx.x; e < 16 * CO; e += blockDim.x) {
+    const int tap = e / CO, c = e - tap * CO;
+    const int ca = tap >> 3, cb = (tap >> 2) & 1, ty = (tap >> 1) & 1, tx = tap & 1;
+    wl[e] = ta.Wf[(c * 4 + ca + 2 * ty) * 4 + cb + 2 * tx];
+  }
+  __syncthreads();
+  const int jr = threadIdx.x / WS, i = threadIdx.x - jr * WS, j = j0 + jr;
+  const float b0 = ta.bias ? ta.bias[0] : 0.f;
+  float acc[2][2] = {{b0, b0}, {b0, b0}};
+#pragma unroll 1
+  for (int c8 = 0; c8 < NCH; ++c8) {
+    bf16x8 g[3][3];  // converted at use: 36 VGPRs instead of 72 per chunk
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int x = i + c;
+        g[r][c] = *reinterpret_cast<const bf16x8*>(patch + ((jr + r) * PC + x) * PB + 16 * (c8 ^ ((x >> 2) & 3)));
+      }
+#pragma unroll
+    for (int ca = 0; ca < 2; ++ca)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int ty = 0; ty < 2; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 2; ++tx) {
+            const int r = (1 - ca) - ty + 1, c = (1 - cb) - tx + 1;
+            const float* w = wl + (((ca * 2 + cb) * 2 + ty) * 2 + tx) * CO + 8 * c8;
+            const float4 w0 = *reinterpret_cast<const float4*>(w), w1 = *reinterpret_cast<const float4*>(w + 4);
+            const bf16x8& gv = g[r][c];
+            float a = acc[ca][cb];
+            a = fmaf((float)gv[0], w0.x, a); a = fmaf((float)gv[1], w0.y, a);
+            a = fmaf((float)gv[2], w0.z, a); a = fmaf((float)gv[3], w0.w, a);
+            a = fmaf((float)gv[4], w1.x, a); a = fmaf((float)gv[5], w1.y, a);
+            a = fmaf((float)gv[6], w1.z, a); a = fmaf((float)gv[7], w1.w, a);
+            acc[ca][cb] = a;
+          }
+  }
+  float loss = 0.f, gsum = 0.f;
+#pragma unroll
+  for (int ca = 0; ca < 2; ++ca) {
+    const int iy = 2 * j + (1 - ca);
+    const size_t e = ((size_t)n * d.H + iy) * d.W + 2 * i;
+    const float t0 = acc[ca][1], t1 = acc[ca][0];  // columns 2i, 2i+1
+    if (ta.y32) *reinterpret_cast<float2*>(ta.y32 + e) = make_float2(t0, t1);
+    if (ta.X) {
+      const float2 x2 = *reinterpret_cast<const float2*>(ta.X + e);
+      const float tv[2] = {t0, t1}, xv[2] = {x2.x, x2.y};
+      float pv[2], gv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float t = tv[u], x = xv[u];
+        const float p = 1.f / (1.f + expf(-t));
+        pv[u] = p;
+        gv[u] = p - x;
+        const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));
+        loss += x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
+        gsum += gv[u];
+      }
+      if (ta.dlog) {
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        bf16x2 g2;
+        g2[0] = (__bf16)gv[0];
+        g2[1] = (__bf16)gv[1];
+        *reinterpret_cast<bf16x2*>(ta.dlog + e) = g2;
+      }
+      if (ta.recon) *reinterpret_cast<float2*>(ta.recon + e) = make_float2(pv[0], pv[1]);
+    }
+  }
+  if (ta.X) {
+    const float sl = block_sum(loss, scratch);
+    if (threadIdx.x == 0) ta.part[bid] = sl;
+    if (ta.gpart) {
+      __syncthreads();
+      const float gs = block_sum(gsum, scratch);
+      if (threadIdx.x == 0) ta.gpart[bid] = gs;
+    }
+  }
+}
+
 }  // namespace mdt

@@ -32,6 +32,12 @@ __global__ void __launch_bounds__(256) thin_tconv4_k(ThinTconvArgs ta) {
   thin_tconv4_body<CO>(ta, lds, blockIdx.x);
 }
 
+template <int CO, int WS>
+__global__ void __launch_bounds__(256) thin_tconv_patch_k(ThinTconvArgs ta) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[thin_tconv_patch_lds_bytes<CO, WS>()];
+  thin_tconv_patch_body<CO, WS>(ta, lds, blockIdx.x);
+}
+
 template <int CO, int K, int S>
 __global__ void __launch_bounds__(256) thin_tconv_k(ThinTconvArgs ta) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[thin_tconv_lds_bytes<CO, K, S>()];
@@ -89,8 +95,20 @@ static bool tconv4_ok(const ConvDesc& d) {
   return on && d.KH == 4 && d.KW == 4 && d.S == 2 && d.P == 1;
 }
 
+// Halo-patch kernel (thin_tconv_patch_body): CO = 32, square 4x4/s2/p1, class
+// grid width 64 (the 128x128 model's last layer). MDT_THIN_PATCH=0 disables.
+static bool tconv_patch_ok(const ConvDesc& d) {
+  static const bool on = [] {
+    const char* e = getenv("MDT_THIN_PATCH");
+    return !(e && e[0] == '0');
+  }();
+  return on && d.CO == 32 && d.KH == 4 && d.KW == 4 && d.S == 2 && d.P == 1 && d.H == d.W && d.OH == d.OW &&
+         d.H == 2 * d.OH && d.OW == 64;
+}
+
 int mdt_thin_blocks(int tconv, ConvDesc d) {
   if (!tconv) return cdiv_t((long long)d.N * d.OH * d.OW, 256);
+  if (tconv_patch_ok(d)) return d.N * (d.OH / 4);
   if (tconv4_ok(d)) return cdiv_t((long long)d.N * (d.H / 2) * (d.W / 2), 256);
   return cdiv_t((long long)d.N * (d.H / d.S) * (d.W / d.S), 256) * d.S * d.S;
 }
@@ -101,6 +119,12 @@ int mdt_thin_tconv(const void* G16, const float* Wf, ConvDesc d, const float* bi
   if (X && !part) return 1;
   const long long Mc = (long long)d.N * (d.H / d.S) * (d.W / d.S);
   const int gx = cdiv_t(Mc, 256);
+  if (tconv_patch_ok(d)) {
+    const ThinTconvArgs tp{reinterpret_cast<const __bf16*>(G16), Wf, d, bias, y32, X,
+                           reinterpret_cast<__bf16*>(dlog16), recon, part, gpart, gx};
+    hipLaunchKernelGGL((thin_tconv_patch_k<32, 64>), dim3(d.N * (d.OH / 4)), dim3(256), 0, s, tp);
+    return (int)hipGetLastError();
+  }
   if (tconv4_ok(d)) {  // one thread per input position: all four parity classes
     const ThinTconvArgs t4{reinterpret_cast<const __bf16*>(G16), Wf, d, bias, y32, X,
                            reinterpret_cast<__bf16*>(dlog16), recon, part, gpart, gx};

@@ -15,12 +15,12 @@
 #include "../kernels/conv_igemm.h"
 
 extern "C" {
-int mdt_igemm_plan(int mode, mdt::ConvDesc d, int allow_split, int* info);
+int mdt_igemm_plan(int mode, mdt::ConvDesc d, int allow_split, int* info, int fwd);
 void mdt_dconv_stamps(unsigned long long* p);
 int mdt_wgrad_plan(mdt::ConvDesc d, int* info);
 int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, mdt::ConvDesc d, const float* bias, int relu,
               void* y16, float* y32, const void* omask, float* colsum, float* ws, int skip_combine, hipStream_t s,
-              const mdt::APro* pro);
+              const mdt::APro* pro, int fwd);
 int mdt_wgrad(const void* G16, const void* X, int x_is_f32, mdt::ConvDesc d, float* out, hipStream_t s);
 int mdt_colsum(const void* G16, int M, int N, int rows_per, float* slab, hipStream_t s);
 int mdt_gather_rows(const float* X, const int* idx, const void* st, int B, int M, int P, float* xb, hipStream_t s);
@@ -111,9 +111,11 @@ static void check_min(const c10::optional<at::Tensor>& t, int64_t n, const char*
   if (t.has_value() && t->defined()) TORCH_CHECK(t->numel() >= n, w, " too small: ", t->numel(), " < ", n);
 }
 
-std::vector<int64_t> igemm_plan(int64_t mode, const std::vector<int64_t>& dv, bool allow_split) {
+// fwd: the forward-pass call of this geometry (may select the direct kernel
+// where the backward-data call of the same geometry keeps the fusable one)
+std::vector<int64_t> igemm_plan(int64_t mode, const std::vector<int64_t>& dv, bool allow_split, bool fwd) {
   int info[12];
-  rc(mdt_igemm_plan((int)mode, desc(dv), allow_split ? 1 : 0, info), "igemm_plan (unsupported geometry)");
+  rc(mdt_igemm_plan((int)mode, desc(dv), allow_split ? 1 : 0, info, fwd ? 1 : 0), "igemm_plan (unsupported geometry)");
   return std::vector<int64_t>(info, info + 12);
 }
 
@@ -130,14 +132,15 @@ void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::
            const c10::optional<at::Tensor>& y32, const c10::optional<at::Tensor>& omask,
            const c10::optional<at::Tensor>& colsum, const c10::optional<at::Tensor>& ws, Job* job, bool combine,
            const c10::optional<at::Tensor>& a_slab, int64_t a_ks, const c10::optional<at::Tensor>& a_bias,
-           bool a_relu, const c10::optional<at::Tensor>& a_out16) {
+           bool a_relu, const c10::optional<at::Tensor>& a_out16, bool fwd) {
   const ConvDesc d = desc(dv);
   TORCH_CHECK(A.is_cuda() && A.is_contiguous(), "A must be contiguous CUDA");
   const bool f32 = A.scalar_type() == torch::kFloat32;
   TORCH_CHECK(f32 || A.scalar_type() == torch::kBFloat16, "A must be f32 or bf16");
   check_bf16(B16, "B16");
   int info[12];
-  rc(mdt_igemm_plan((int)mode, d, ws.has_value() && ws->defined() ? 1 : 0, info), "igemm_plan");
+  rc(mdt_igemm_plan((int)mode, d, ws.has_value() && ws->defined() ? 1 : 0, info, fwd ? 1 : 0), "igemm_plan");
+  TORCH_CHECK(!(fwd && job), "igemm: fwd calls have no job form");
   const int64_t classes = info[3], M = info[4], Ncols = info[5], K = info[6], ksplit = info[10];
   const int64_t rows_total = classes * M;
   const int64_t a_need = mode == kModeConv ? (int64_t)d.N * d.H * d.W * d.C : (int64_t)d.N * d.OH * d.OW * d.CO;
@@ -173,7 +176,7 @@ void igemm(int64_t mode, const at::Tensor& A, const at::Tensor& B16, const std::
   }
   rc(mdt_igemm((int)mode, A.data_ptr(), f32, B16.data_ptr(), d, (const float*)opt_ptr(bias), relu,
                const_cast<void*>(opt_ptr(y16)), (float*)opt_ptr(y32), opt_ptr(omask), (float*)opt_ptr(colsum),
-               (float*)opt_ptr(ws), combine ? 0 : 1, cur(), pro.slab ? &pro : nullptr),
+               (float*)opt_ptr(ws), combine ? 0 : 1, cur(), pro.slab ? &pro : nullptr, fwd ? 1 : 0),
      "igemm");
 }
 
@@ -651,7 +654,7 @@ class TrialStateBuf {
 
 void bind_conv(pybind11::module& m) {
   namespace py = pybind11;
-  m.def("igemm_plan", &igemm_plan);
+  m.def("igemm_plan", &igemm_plan, py::arg("mode"), py::arg("desc"), py::arg("allow_split"), py::arg("fwd") = false);
   m.def("dconv_stamps", [](const c10::optional<at::Tensor>& t) {
     // profiling: per-workgroup s_memrealtime stamps of the direct conv kernels ([grid][8] int64), None = off
     if (t.has_value() && t->defined()) {
@@ -679,7 +682,8 @@ void bind_conv(pybind11::module& m) {
         py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),
         py::arg("colsum") = py::none(), py::arg("ws") = py::none(), py::arg("job") = py::none(),
         py::arg("combine") = true, py::arg("a_slab") = py::none(), py::arg("a_ks") = 0,
-        py::arg("a_bias") = py::none(), py::arg("a_relu") = false, py::arg("a_out16") = py::none());
+        py::arg("a_bias") = py::none(), py::arg("a_relu") = false, py::arg("a_out16") = py::none(),
+        py::arg("fwd") = false);
   m.def("wgrad", &wgrad, py::arg("G16"), py::arg("X"), py::arg("desc"), py::arg("out"), py::arg("job") = py::none());
   m.def("colsum", &colsum, py::arg("G16"), py::arg("M"), py::arg("N"), py::arg("rows_per"), py::arg("slab"),
         py::arg("job") = py::none());

@@ -504,7 +504,7 @@ class ConvVaeTrainer:
         """Number of KLD partials the forward writes for a batch of M (one per
         block of the reparameterisation kernel that ends the encoder)."""
         head = [l for l in self.spec if l.name.startswith("enc")][-1]
-        ks = self.C.igemm_plan(0, self._desc(head, M), True)[10]
+        ks = self.C.igemm_plan(0, self._desc(head, M), True, fwd=True)[10]
         if ks > 1:
             return self.C.combine_reparam_blocks(ks, M, self.Z)
         return -(-M * self.Z // 256)
@@ -574,7 +574,7 @@ class ConvVaeTrainer:
             slabs[prev.name + ".bias"] = (t, rows * (ncols // prev.cout))
         for l in spec:  # forward split-K (deep, narrow conv-mode layers such as enc_head)
             if l.kind != "convT":
-                q = C.igemm_plan(0, self._desc(l, M), True)
+                q = C.igemm_plan(0, self._desc(l, M), True, fwd=True)
                 if q[10] > 1:
                     ws_need = max(ws_need, q[10] * q[4] * q[5])
         # the layer feeding the encoder head, when it runs split-K: its combine
@@ -584,7 +584,7 @@ class ConvVaeTrainer:
         if len(enc) >= 3 and os.getenv("MDT_CONV_APRO", "1") != "0":
             src = enc[-2]
             if not (src is spec[0] and self._thin_first) and src.kind == "conv" and src.cout % 8 == 0:
-                q = C.igemm_plan(0, self._desc(src, M), True)
+                q = C.igemm_plan(0, self._desc(src, M), True, fwd=True)
                 if q[10] > 1:
                     ks_a = q[10]
                     ws_a = torch.empty(ks_a * q[4] * q[5], **f32)
@@ -675,9 +675,9 @@ class ConvVaeTrainer:
         elif l is self.spec[-1] and self._thin_last:
             self.C.thin_tconv(h, self._wf32(l), d, self._b(l), y32=o32)
         elif l.kind == "convT":
-            self.C.igemm(1, h, self._wt(l), d, self._b(l), l.relu, o16, o32)
+            self.C.igemm(1, h, self._wt(l), d, self._b(l), l.relu, o16, o32, fwd=True)
         else:
-            self.C.igemm(0, h, self._w(l), d, self._b(l), l.relu, o16, o32, ws=ws, **pro)
+            self.C.igemm(0, h, self._w(l), d, self._b(l), l.relu, o16, o32, ws=ws, fwd=True, **pro)
 
     def _forward_hip(self, M, state, stream, want_recon=False, train=True, src=None):
         """Forward of one batch. ``src = (X, idx)``: the batch is gathered from
@@ -717,16 +717,17 @@ class ConvVaeTrainer:
             if not last and p["ws_a"] is not None and l is enc[-2]:
                 # split-K partials only; the head's A staging combines them (+bias, ReLU)
                 # and writes this layer's activations for the backward
-                C.igemm(0, h, self._w(l), self._desc(l, M), None, False, None, None, ws=p["ws_a"], combine=False)
+                C.igemm(0, h, self._w(l), self._desc(l, M), None, False, None, None, ws=p["ws_a"], combine=False,
+                        fwd=True)
                 pro = dict(a_slab=p["ws_a"], a_ks=p["ks_a"], a_bias=self._b(l), a_relu=l.relu,
                            a_out16=self.acts[l.name])
                 h = self.acts[l.name]
                 continue
             if last:
-                q = C.igemm_plan(0, self._desc(l, M), True)
+                q = C.igemm_plan(0, self._desc(l, M), True, fwd=True)
                 if q[10] > 1:  # split-K head: combine fused with the reparameterisation
                     C.igemm(0, h, self._w(l), self._desc(l, M), self._b(l), False, None, self.mulv, ws=p["ws"],
-                            combine=False, **pro)
+                            combine=False, fwd=True, **pro)
                     C.combine_reparam(p["ws"], q[10], self._b(l), self.mulv, self.eps, self.z16, None, M, self.Z,
                                       state, hp, stream, self.kld_part)
                     break

@@ -10,7 +10,7 @@ that step only (A/B switches such as MDT_CONV_F28=0, MDT_CONV_DIRECT=0):
 
   test[:PATH[:KEXPR]]                     pytest (default ``tests -m gpu``), one process
   bench[:MODEL[:B[:STEPS[:WARMUP]]]]      bench.py -> bench_<i>.json + a summary line
-  driver                                  the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
+  driver[:ARG:ARG...]                     the driver's command: bench.py --gpus 1 --steps 20 --warmup 5 [ARGS]
   launches[:IMAGE[:B]]                    bench/conv_kernels.py (every launch of a step, alone)
   f28phases | f28parts | dconv[:B]        in-kernel stamp / per-launch tools of the fused kernels
   prof[:MODEL[:B]]                        rocprofv3 --kernel-trace --stats of a short bench run
@@ -72,7 +72,7 @@ def command(kind, args, out, i):
     if kind == "bench":
         return [PY] + bench_args(*args), ROOT, os.path.join(out, f"{i:02d}_bench.json")
     if kind == "driver":
-        return [PY, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "20", "--warmup", "5"], ROOT, \
+        return [PY, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "20", "--warmup", "5"] + args, ROOT, \
             os.path.join(out, f"{i:02d}_driver.json")
     if kind == "launches":
         image, b = (args + ["128", "64"])[:2] if args else ("128", "64")

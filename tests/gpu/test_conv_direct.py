@@ -35,7 +35,8 @@ def _parity_B(Wc):
 
 # (mode, H, C, OH, CO) in conv view: mode 0 = conv (A = H x H x C), mode 1 =
 # transposed conv (A = OH x OH x CO, output H x H x C)
-CASES = [(0, 64, 32, 32, 64), (0, 32, 64, 16, 128), (1, 32, 64, 16, 128), (1, 64, 32, 32, 64)]
+CASES = [(0, 64, 32, 32, 64), (0, 32, 64, 16, 128), (1, 32, 64, 16, 128), (1, 64, 32, 32, 64),
+         (0, 16, 128, 8, 256), (1, 16, 128, 8, 256)]
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"mode{c[0]}_{c[1]}x{c[2]}_{c[3]}x{c[4]}")
@@ -48,7 +49,7 @@ def test_direct_conv_matches_torch(case, epi, native_ext):
     g = torch.Generator(device="cpu").manual_seed(11 + mode + H)
     Wc = (torch.randn(CO, C, 4, 4, generator=g) * 0.05).bfloat16().float().to(dev)
     d = [N, H, H, C, OH, OH, CO, 4, 4, 2, 1]
-    info = C_.igemm_plan(mode, d, False)
+    info = C_.igemm_plan(mode, d, False, fwd=True)
     assert info[0] >= 100, f"direct kernel not selected: {info}"
     if mode == 0:
         A = torch.randn(N, C, H, H, generator=g).bfloat16().float().to(dev)
@@ -74,7 +75,7 @@ def test_direct_conv_matches_torch(case, epi, native_ext):
         mask = (torch.rand(ref.shape, generator=g) > 0.4).bfloat16().to(dev)
         ref = ref * mask.float()
         cs = torch.full((info[11] * ncols,), float("nan"), device=dev)
-    C_.igemm(mode, A16, B16, d, bias, relu, y16, y32, mask, cs)
+    C_.igemm(mode, A16, B16, d, bias, relu, y16, y32, mask, cs, fwd=True)
     torch.cuda.synchronize()
     r = ref.flatten()
     err = float((y32 - r).abs().max() / r.abs().max())
@@ -85,3 +86,37 @@ def test_direct_conv_matches_torch(case, epi, native_ext):
         tot = cs.view(info[11], ncols).double().sum(0)
         torch.testing.assert_close(tot, ref.reshape(-1, ncols).double().sum(0), rtol=1e-5,
                                    atol=1e-5 * float(ref.abs().sum(0).max()))
+
+
+def test_thin_tconv_patch_matches_torch(native_ext):
+    """Last 128x128 decoder layer (convT 32 -> 1, 64^2 -> 128^2) on the
+    halo-patch kernel with the fused BCE: logits vs conv_transpose2d, the
+    loss / dlogits-sum partials vs their definitions."""
+    C_ = native_ext
+    dev = torch.device("cuda")
+    N = 3
+    g = torch.Generator(device="cpu").manual_seed(5)
+    d = [N, 128, 128, 1, 64, 64, 32, 4, 4, 2, 1]
+    nb = C_.thin_blocks(True, d)
+    assert nb == N * 16, nb  # one workgroup per 4 class-grid rows: the patch kernel
+    G = torch.randn(N, 32, 64, 64, generator=g).bfloat16().float().to(dev)
+    Wc = (torch.randn(32, 1, 4, 4, generator=g) * 0.1).to(dev)  # conv view [CO][C][kh][kw]
+    bias = torch.tensor([0.05], device=dev)
+    X = torch.rand(N, 128 * 128, generator=g).to(dev)
+    G16 = G.permute(0, 2, 3, 1).contiguous().bfloat16()
+    Wf = Wc.permute(0, 2, 3, 1).contiguous().flatten()  # [CO][4][4][1]
+    y32 = torch.empty(N * 128 * 128, device=dev)
+    dlog = torch.empty(N * 128 * 128, dtype=torch.bfloat16, device=dev)
+    recon = torch.empty(N * 128 * 128, device=dev)
+    part = torch.full((nb,), float("nan"), device=dev)
+    gpart = torch.full((nb,), float("nan"), device=dev)
+    C_.thin_tconv(G16, Wf, d, bias, y32=y32, X=X, dlog16=dlog, recon=recon, part=part, gpart=gpart)
+    torch.cuda.synchronize()
+    t = (F.conv_transpose2d(G, Wc, stride=2, padding=1) + bias).flatten()
+    torch.testing.assert_close(y32, t, rtol=1e-5, atol=1e-5)
+    p = torch.sigmoid(t)
+    torch.testing.assert_close(recon, p, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dlog.float(), (p - X.flatten()).bfloat16().float(), rtol=0, atol=1e-2)
+    bce = F.binary_cross_entropy_with_logits(t, X.flatten(), reduction="sum")
+    torch.testing.assert_close(part.double().sum(), bce.double(), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gpart.double().sum(), (p - X.flatten()).double().sum(), rtol=1e-4, atol=1e-2)
