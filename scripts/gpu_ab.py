@@ -63,7 +63,7 @@ def command(kind, args, out, i):
     log = os.path.join(out, f"{i:02d}_{kind}.log")
     if kind == "test":
         path = args[0] if args else "tests"
-        argv = [PY, "-u", "-m", "pytest", path, "-x", "-q", "--timeout", "150", "--timeout-method", "thread"]
+        argv = [PY, "-u", "-m", "pytest", path, "-x", "-q", "-s", "--timeout", "150", "--timeout-method", "thread"]
         if not args:
             argv += ["-m", "gpu"]
         if len(args) > 1:
