@@ -356,20 +356,23 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
   __syncthreads();
 
   stamp(a.stamps, 1);
-  // ---- P1: enc1 (1 -> 32, 28x28 -> 14x14, VALU), ReLU
-  if (tid < 196) {
-    const int oy = tid / 14, ox = tid - 14 * (tid / 14);
-    float acc[32];
+  // ---- P1: enc1 (1 -> 32, 28x28 -> 14x14, VALU), ReLU. Two threads per
+  // output pixel (16 channels each): 392 of the 512 threads instead of 196
+  // with a 512-FMA chain each.
+  if (tid < 392) {
+    const int pix = tid >> 1, hc = tid & 1;
+    const int oy = pix / 14, ox = pix - 14 * (pix / 14);
+    float acc[16];
 #pragma unroll
-    for (int c = 0; c < 32; ++c) acc[c] = W.b1[c];
-#pragma unroll 2
+    for (int c = 0; c < 16; ++c) acc[c] = W.b1[16 * hc + c];
+#pragma unroll 4
     for (int t = 0; t < 16; ++t) {
       const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
       const bool ok = (unsigned)iy < 28u && (unsigned)ix < 28u;
       const float x = ok ? Xs[iy * 28 + ix] : 0.f;
 #pragma unroll
-      for (int c4 = 0; c4 < 8; ++c4) {
-        const float4 wv = reinterpret_cast<const float4*>(W1s + t * 32)[c4];
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const float4 wv = reinterpret_cast<const float4*>(W1s + t * 32 + 16 * hc)[c4];
         acc[4 * c4 + 0] = fmaf(x, wv.x, acc[4 * c4 + 0]);
         acc[4 * c4 + 1] = fmaf(x, wv.y, acc[4 * c4 + 1]);
         acc[4 * c4 + 2] = fmaf(x, wv.z, acc[4 * c4 + 2]);
@@ -377,12 +380,13 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
       }
     }
 #pragma unroll
-    for (int ch = 0; ch < 4; ++ch) {
+    for (int h = 0; h < 2; ++h) {
+      const int ch = 2 * hc + h;
       bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (__bf16)fmaxf(acc[8 * ch + e], 0.f);
-      *reinterpret_cast<bf16x8*>(A1s + img14(tid, ch)) = o;
-      if (a.train) *reinterpret_cast<bf16x8*>(a.a1 + ((size_t)n * 196 + tid) * 32 + 8 * ch) = o;
+      for (int e = 0; e < 8; ++e) o[e] = (__bf16)fmaxf(acc[8 * h + e], 0.f);
+      *reinterpret_cast<bf16x8*>(A1s + img14(pix, ch)) = o;
+      if (a.train) *reinterpret_cast<bf16x8*>(a.a1 + ((size_t)n * 196 + pix) * 32 + 8 * ch) = o;
     }
   }
   __syncthreads();
@@ -631,54 +635,53 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
   }
 
   stamp(a.stamps, 1);
-  // ---- Q1: dec2 backward-data (conv 1 -> 32 on the dlogits, 28 -> 14) x dec1 ReLU mask
-  {
-    float acc[32];
+  // ---- Q1: dec2 backward-data (conv 1 -> 32 on the dlogits, 28 -> 14) x dec1 ReLU mask.
+  // Two threads per pixel (16 channels each), as in P1.
+  if (tid < 392) {
+    const int pix = tid >> 1, hc = tid & 1;
+    const int oy = pix / 14, ox = pix - 14 * (pix / 14);
+    float acc[16];
 #pragma unroll
-    for (int c = 0; c < 32; ++c) acc[c] = 0.f;
-    if (tid < 196) {
-      const int oy = tid / 14, ox = tid - 14 * (tid / 14);
-      // the dec1 ReLU mask, loaded before the FMAs so its latency overlaps them
-      bf16x8 mk[4];
+    for (int c = 0; c < 16; ++c) acc[c] = 0.f;
+    // the dec1 ReLU mask, loaded before the FMAs so its latency overlaps them
+    bf16x8 mk[2];
 #pragma unroll
-      for (int ch = 0; ch < 4; ++ch)
-        mk[ch] = MERGED ? reinterpret_cast<const bf16x8*>(lds + L::D1 + tid * 64)[ch]
-                        : reinterpret_cast<const bf16x8*>(a.d1 + ((size_t)n * 196 + tid) * 32)[ch];
-#pragma unroll 2
-      for (int t = 0; t < 16; ++t) {
-        const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
-        const bool ok = (unsigned)iy < 28u && (unsigned)ix < 28u;
-        const float g = ok ? Gs[iy * 28 + ix] : 0.f;
+    for (int h = 0; h < 2; ++h)
+      mk[h] = MERGED ? reinterpret_cast<const bf16x8*>(lds + L::D1 + pix * 64)[2 * hc + h]
+                     : reinterpret_cast<const bf16x8*>(a.d1 + ((size_t)n * 196 + pix) * 32)[2 * hc + h];
+#pragma unroll 4
+    for (int t = 0; t < 16; ++t) {
+      const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
+      const bool ok = (unsigned)iy < 28u && (unsigned)ix < 28u;
+      const float g = ok ? Gs[iy * 28 + ix] : 0.f;
 #pragma unroll
-        for (int c4 = 0; c4 < 8; ++c4) {
-          const float4 wv = reinterpret_cast<const float4*>(W4s + t * 32)[c4];
-          acc[4 * c4 + 0] = fmaf(g, wv.x, acc[4 * c4 + 0]);
-          acc[4 * c4 + 1] = fmaf(g, wv.y, acc[4 * c4 + 1]);
-          acc[4 * c4 + 2] = fmaf(g, wv.z, acc[4 * c4 + 2]);
-          acc[4 * c4 + 3] = fmaf(g, wv.w, acc[4 * c4 + 3]);
-        }
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const float4 wv = reinterpret_cast<const float4*>(W4s + t * 32 + 16 * hc)[c4];
+        acc[4 * c4 + 0] = fmaf(g, wv.x, acc[4 * c4 + 0]);
+        acc[4 * c4 + 1] = fmaf(g, wv.y, acc[4 * c4 + 1]);
+        acc[4 * c4 + 2] = fmaf(g, wv.z, acc[4 * c4 + 2]);
+        acc[4 * c4 + 3] = fmaf(g, wv.w, acc[4 * c4 + 3]);
       }
+    }
 #pragma unroll
-      for (int ch = 0; ch < 4; ++ch) {
-        const bf16x8 m = mk[ch];
-        bf16x8 o;
+    for (int h = 0; h < 2; ++h) {
+      const int ch = 2 * hc + h;
+      const bf16x8 m = mk[h];
+      bf16x8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v = (float)m[e] > 0.f ? acc[8 * ch + e] : 0.f;
-          acc[8 * ch + e] = v;
-          o[e] = (__bf16)v;
-        }
-        *reinterpret_cast<bf16x8*>(GD1s + img14(tid, ch)) = o;
-        *reinterpret_cast<bf16x8*>(a.gd1 + ((size_t)n * 196 + tid) * 32 + 8 * ch) = o;
+      for (int e = 0; e < 8; ++e) {
+        const float v = (float)m[e] > 0.f ? acc[8 * h + e] : 0.f;
+        acc[8 * h + e] = v;
+        o[e] = (__bf16)v;
       }
+      *reinterpret_cast<bf16x8*>(GD1s + img14(pix, ch)) = o;
+      *reinterpret_cast<bf16x8*>(a.gd1 + ((size_t)n * 196 + pix) * 32 + 8 * ch) = o;
     }
     // dec1 bias partials: transpose the f32 values through LDS, then 8 lanes
     // per channel sum strided pixels and combine in a fixed order (a wave_sum
     // per channel was 192 dependent cross-lane steps per wave: ~5 us)
-    if (tid < 196) {
 #pragma unroll
-      for (int c = 0; c < 32; ++c) CSB[c * 197 + tid] = acc[c];
-    }
+    for (int c = 0; c < 16; ++c) CSB[(16 * hc + c) * 197 + pix] = acc[c];
   }
   __syncthreads();
   if (tid < 256) {
