@@ -148,6 +148,25 @@ __device__ __forceinline__ void stream2(Load ld, Use use) {
   }
 }
 
+// stream2 whose first CH loads were issued earlier (during a previous phase).
+template <int CH, int NCH, class Load, class Use>
+__device__ __forceinline__ void stream2_pre(const bf16x8 (&first)[CH], Load ld, Use use) {
+  bf16x8 bc[CH], bn[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) bc[i] = first[i];
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+    if (c + 1 < NCH) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) bn[i] = ld((c + 1) * CH + i);
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) use(c * CH + i, bc[i]);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) bc[i] = bn[i];
+  }
+}
+
 // Conv-layout [64][16][32] bf16 weight staged in LDS: row co = 1 KB, 16-B
 // chunk (tap, ch) of row co at slot (tap*4 + ch) ^ (co & 15), so the 16 rows a
 // B-fragment read touches land on 16 different bank groups.
@@ -392,6 +411,14 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
   __syncthreads();
 
   stamp(a.stamps, 2);
+  // the head's first weight row per wave (P3) is loaded now: its latency
+  // hides under the enc2 MFMAs instead of opening P3
+  bf16x8 wh0[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int k = 512 * i + 8 * lane;
+    wh0[i] = *reinterpret_cast<const bf16x8*>(W.Wh + (size_t)w * kFlat + (k < kFlat ? k : 0));
+  }
   // ---- P2: enc2 (32 -> 64, 14x14 -> 7x7, MFMA), ReLU
   conv14to7(A1s, [&](int j, int t) { return conv_bfrag(W3s, j, t, lane); }, [&](int, int col) { return W.b2[col]; },
             [&](int p, int col, float v, float bias) {
@@ -426,7 +453,8 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
       }
     };
     bf16x8 vc[7], vn[7];
-    ld_row(w, vc);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) vc[i] = wh0[i];
 #pragma unroll 1
     for (int c = 0; c < 8; ++c) {
       if (c + 1 < 8) ld_row(w + 8 * (c + 1), vn);
@@ -444,6 +472,15 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
       for (int i = 0; i < 7; ++i) vc[i] = vn[i];
     }
   }
+  // P5's first 13 dec_fc weight loads, in flight across the barrier and P4
+  const __bf16* wp5 = W.Wd + (size_t)(lane & 15) * 32 + 8 * (lane >> 4);
+  auto wd5_ld = [&](int i) {
+    const int t = w + 8 * i;
+    return *reinterpret_cast<const bf16x8*>(wp5 + (size_t)(t < 196 ? t : 0) * 512);
+  };
+  bf16x8 wd5[13];
+#pragma unroll
+  for (int i = 0; i < 13; ++i) wd5[i] = wd5_ld(i);
   __syncthreads();
 
   stamp(a.stamps, 4);
@@ -478,13 +515,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
   // ---- P5: dec_fc (32 -> 3136, MFMA K = 32), ReLU. Wave w: n-tiles w + 8i.
   {
     const bf16x8 av = (lane & 15) == 0 ? *reinterpret_cast<const bf16x8*>(Zs + 8 * (lane >> 4)) : zero8();
-    const __bf16* wp = W.Wd + (size_t)(lane & 15) * 32 + 8 * (lane >> 4);
     // n-tiles t = w + 8i (i < 25, t < 196): 2 chunks of 13 loads
-    stream2<13, 2>(
-        [&](int i) {
-          const int t = w + 8 * i;
-          return *reinterpret_cast<const bf16x8*>(wp + (size_t)(t < 196 ? t : 0) * 512);
-        },
+    stream2_pre<13, 2>(
+        wd5, wd5_ld,
         [&](int i, const bf16x8& b) {
           const int t = w + 8 * i;
           if (t < 196) {
@@ -695,6 +728,14 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
   }
 
   stamp(a.stamps, 2);
+  // Q3's first 13 weight loads, in flight during the Q2 MFMAs
+  auto wd_ld = [&](int it) {
+    const int jj = it * 128 + w * 16 + (lane >> 2);
+    return *reinterpret_cast<const bf16x8*>(W.Wd + (size_t)(jj < kFlat ? jj : 0) * 32 + 8 * (lane & 3));
+  };
+  bf16x8 wd0[13];
+#pragma unroll
+  for (int i = 0; i < 13; ++i) wd0[i] = wd_ld(i);
   // ---- Q2: dec1 backward-data (conv 32 -> 64 with the convT weights, 14 -> 7) x dec_fc ReLU mask
   conv14to7(GD1s,
             [&](int j, int t) {
@@ -727,11 +768,8 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = 0.f;
     // 25 row groups of 128 (3136 rows): 2 chunks of 13 loads
-    stream2<13, 2>(
-        [&](int it) {
-          const int jj = it * 128 + w * 16 + jr;
-          return *reinterpret_cast<const bf16x8*>(W.Wd + (size_t)(jj < kFlat ? jj : 0) * 32 + 8 * c8);
-        },
+    stream2_pre<13, 2>(
+        wd0, wd_ld,
         [&](int it, const bf16x8& wv) {
           const int jj = it * 128 + w * 16 + jr;
           if (jj < kFlat) {
@@ -754,6 +792,12 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
       for (int e = 0; e < 8; ++e) DZR[w * 32 + 8 * lane + e] = acc[e];
     }
   }
+  // Q5's first 16 head-weight loads, in flight across the barrier and Q4
+  const int k05 = 8 * (tid < kFlat / 8 ? tid : 0);
+  auto wh_ld = [&](int o) { return *reinterpret_cast<const bf16x8*>(W.Wh + (size_t)o * kFlat + k05); };
+  bf16x8 wh5[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) wh5[i] = wh_ld(i);
   __syncthreads();
   stamp(a.stamps, 4);
   // ---- Q4: reparameterisation backward -> d[mu | logvar]
@@ -784,7 +828,7 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = 0.f;
     // 64 weight rows: 4 chunks of 16 loads
-    stream2<16, 4>([&](int o) { return *reinterpret_cast<const bf16x8*>(W.Wh + (size_t)o * kFlat + k0); },
+    stream2_pre<16, 4>(wh5, wh_ld,
                    [&](int o, const bf16x8& wv) {
                      const float dm = DMs[o];
 #pragma unroll
