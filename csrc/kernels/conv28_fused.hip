@@ -109,6 +109,19 @@ struct BwdArgs {
 // 14x14x32 bf16 LDS image, 64-B pixel rows: 16-B chunk ch of pixel p at slot
 // ch ^ ((p >> 1) & 3) -- the stride-2 im2col gathers of 16 lanes then spread
 // over all four chunk slots of a bank row instead of hitting one.
+// Workgroup barrier for the phase hand-offs: LDS writes visible, global
+// stores NOT waited for. __syncthreads() waits vmcnt(0), i.e. for the
+// acknowledgement of every global store of the phase (the activations and
+// gradients the weight-gradient launch reads later), which put an L2 write
+// round trip on every phase boundary. Inside these kernels every cross-thread
+// hand-off goes through LDS; a thread re-reading global data reads its own
+// earlier stores (P4 -> Q4), which program order covers.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Phase timestamp (100 MHz s_memrealtime) of workgroup blockIdx.x, slot k.
 __device__ __forceinline__ void stamp(unsigned long long* st, int k) {
   if (st && threadIdx.x == 0) st[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memrealtime();
@@ -317,6 +330,7 @@ struct FwdLayout {
   static constexpr int X = kFX, W1 = kFW1, W4 = kFW4, A1 = kFA1, A2 = kFA2, D0 = kFD0, H = kFH, Z = kFZ;
   static constexpr int Red = kFRed, Scr = kFScr, IMG = kFW3, Dummy = kFDummy, Bd = kFBd;
   static constexpr int G = -1;  // dlogits stay in global memory only
+  static constexpr int D1 = kFA1;
   static constexpr int LDS = kFLds;
 };
 
@@ -332,7 +346,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
   __bf16* Zs = reinterpret_cast<__bf16*>(lds + L::Z);
   float* Scr = reinterpret_cast<float*>(lds + L::Scr);
   uint8_t* W3s = lds + L::IMG;
-  __bf16* D1s = reinterpret_cast<__bf16*>(lds + L::A1);  // aliases A1s (dead after enc2)
+  __bf16* D1s = reinterpret_cast<__bf16*>(lds + L::D1);  // FwdLayout: aliases A1s (dead after enc2)
 
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -408,7 +422,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
       if (a.train) *reinterpret_cast<bf16x8*>(a.a1 + ((size_t)n * 196 + pix) * 32 + 8 * ch) = o;
     }
   }
-  __syncthreads();
+  lds_barrier();
 
   stamp(a.stamps, 2);
   // the head's first weight row per wave (P3) is loaded now: its latency
@@ -426,7 +440,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
     A2s[p * 64 + col] = o;
     if (a.train) a.a2[(size_t)n * kFlat + p * 64 + col] = o;
   });
-  __syncthreads();
+  lds_barrier();
 
   TapImageRegs w3r;
   w3r.load(W.W3);  // dec1 tap images: in flight during P3-P5, written after P5
@@ -481,7 +495,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
   bf16x8 wd5[13];
 #pragma unroll
   for (int i = 0; i < 13; ++i) wd5[i] = wd5_ld(i);
-  __syncthreads();
+  lds_barrier();
 
   stamp(a.stamps, 4);
   // ---- P4: reparameterisation (Philox eps) + KLD
@@ -499,6 +513,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
       const float zz = mu + ep * sd;
       kl = 1.f + lv - mu * mu - sd * sd;
       Zs[c] = (__bf16)zz;
+      reinterpret_cast<float*>(lds + L::Red)[c] = ep;  // the merged step's Q4 (Red is free after P3)
       if (a.train) {
         a.mulv[(size_t)n * 64 + c] = mu;
         a.mulv[(size_t)n * 64 + 32 + c] = lv;
@@ -509,7 +524,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
     kl = wave_sum(kl);
     if (tid == 0) Scr[0] = -0.5f * kl;
   }
-  __syncthreads();
+  lds_barrier();
 
   stamp(a.stamps, 5);
   // ---- P5: dec_fc (32 -> 3136, MFMA K = 32), ReLU. Wave w: n-tiles w + 8i.
@@ -532,7 +547,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
         });
   }
   w3r.store(W3s);
-  __syncthreads();
+  lds_barrier();
 
   stamp(a.stamps, 6);
   // ---- P6: dec1 (convT 64 -> 32, 7x7 -> 14x14, MFMA), ReLU
@@ -545,7 +560,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
       return 0.f;
     }, cs);
   }
-  __syncthreads();
+  lds_barrier();
 
   stamp(a.stamps, 7);
   // ---- P7: dec2 (convT 32 -> 1, 14x14 -> 28x28, VALU) + BCE + dlogits
@@ -590,7 +605,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, uint8_t* lds) {
     Scr[8 + w] = loss;
     Scr[16 + w] = gsum;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) {
     float sl = 0.f, sg = 0.f;
 #pragma unroll
@@ -629,7 +644,7 @@ static_assert(kBGD1 % 16 == 0 && kBGD0 % 16 == 0 && kBGA2 % 16 == 0 && kBGA2F % 
 struct BwdLayout {
   static constexpr int G = kBG, W4 = kBW4, GD1 = kBGD1, GD0 = kBGD0, DM = kBDM, DZR = kBDZR, GA2 = kBGA2;
   static constexpr int GA2F = kBGA2F, CS = kBCS, IMG = kBW2, CSB = kBCSB, LDS = kBLds;
-  static constexpr int D1 = -1, D0 = -1, A2 = -1;  // masks come from global memory
+  static constexpr int D1 = -1, D0 = -1, A2 = -1, A1 = -1, H = -1, Red = -1;  // from global memory
 };
 
 // MERGED: the backward runs in the forward's workgroup right after it (one
@@ -664,7 +679,7 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
       W4s[t * 32 + c] = W.W4f[tid];
     }
     stage_conv_image(W.W3, W2s);  // dec1 weights (conv layout) first; enc2's tap images after Q2
-    __syncthreads();
+    lds_barrier();
   }
 
   stamp(a.stamps, 1);
@@ -716,7 +731,7 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) CSB[(16 * hc + c) * 197 + pix] = acc[c];
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < 256) {
     const int c = tid >> 3, part = tid & 7;
     float s = 0.f;
@@ -756,7 +771,7 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
     a.gd0[e] = o;
     a.dbd_part[e] = g;
   });
-  __syncthreads();
+  lds_barrier();
 
   TapImageRegs w2r;
   w2r.load(W.W2);  // enc2 tap images: in flight during Q3-Q5, written before Q6
@@ -798,7 +813,7 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
   bf16x8 wh5[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) wh5[i] = wh_ld(i);
-  __syncthreads();
+  lds_barrier();
   stamp(a.stamps, 4);
   // ---- Q4: reparameterisation backward -> d[mu | logvar]
   if (tid < 32) {
@@ -807,10 +822,14 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) dz += DZR[i * 32 + c];
     const float beta = a.hp->kl_beta;
-    const float mu = a.mulv[(size_t)n * 64 + c], lv = a.mulv[(size_t)n * 64 + 32 + c];
+    // merged step: mu | logvar and eps from the forward's LDS (H, Red); else from memory
+    const float* Hm = reinterpret_cast<const float*>(lds + L::H);
+    const float mu = MERGED ? Hm[c] : a.mulv[(size_t)n * 64 + c];
+    const float lv = MERGED ? Hm[32 + c] : a.mulv[(size_t)n * 64 + 32 + c];
+    const float ep = MERGED ? reinterpret_cast<const float*>(lds + L::Red)[c] : a.eps[(size_t)n * 32 + c];
     const float sd = expf(0.5f * lv);
     const float dm = dz + beta * mu;
-    const float dl = 0.5f * dz * a.eps[(size_t)n * 32 + c] * sd + 0.5f * beta * (sd * sd - 1.f);
+    const float dl = 0.5f * dz * ep * sd + 0.5f * beta * (sd * sd - 1.f);
     DMs[c] = dm;
     DMs[32 + c] = dl;
     a.dmulv[(size_t)n * 64 + c] = dm;
@@ -818,7 +837,7 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
     a.dmulv16[(size_t)n * 64 + c] = (__bf16)dm;
     a.dmulv16[(size_t)n * 64 + 32 + c] = (__bf16)dl;
   }
-  __syncthreads();
+  lds_barrier();
 
   stamp(a.stamps, 5);
   // ---- Q5: head backward-data g = dmulv . Wh (VALU over 392 chunks of 8) x enc2 ReLU mask
@@ -847,7 +866,7 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
     *reinterpret_cast<bf16x8*>(a.ga2 + (size_t)n * kFlat + k0) = o;
   }
   w2r.store(W2s);
-  __syncthreads();
+  lds_barrier();
   if (tid < 64) {  // enc2 bias partials: sum over the 49 pixels in order
     float s = 0.f;
     for (int p = 0; p < 49; ++p) s += GA2F[p * 64 + tid];
@@ -858,7 +877,13 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
   // ---- Q6: enc2 backward-data (convT 64 -> 32 with the conv weights, 7 -> 14) x enc1 ReLU mask
   {
     float cs[2];
-    tconv7to14(GA2u, W2s, [&](int pix, int co) { return (float)a.a1[((size_t)n * 196 + pix) * 32 + co]; },
+    tconv7to14(GA2u, W2s,
+               [&](int pix, int co) {
+                 if constexpr (MERGED)  // enc1's output is still in LDS (img14)
+                   return (float)*reinterpret_cast<const __bf16*>(lds + L::A1 + img14(pix, co >> 3) + ((co & 7) << 1));
+                 else
+                   return (float)a.a1[((size_t)n * 196 + pix) * 32 + co];
+               },
                [&](int pix, int co, float v, float mask) {
       const size_t e = ((size_t)n * 196 + pix) * 32 + co;
       const float g = mask > 0.f ? v : 0.f;
@@ -870,7 +895,7 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds) {
       CS[w * 64 + 16 + lane] = cs[1];
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < 32) {
     float s = 0.f;
 #pragma unroll
@@ -898,10 +923,8 @@ struct StepLayout {
   static constexpr int DM = X;                   //   bwd d[mu|lv] (X dead after P7)
   static constexpr int DZR = X + 64 * 4;         //   bwd dz partials
   static constexpr int G = X + 784 * 4;          // f32 [784] dlogits (P7 -> Q1)
-  static constexpr int A1 = G + 784 * 4;         // bf16 img14: enc1 out, then dec1 out (Q1 mask)
-  static constexpr int D1 = A1;
-  static constexpr int GA2F = A1;                //   bwd f32 [3136] (A1/D1 dead after Q1)
-  static constexpr int A2 = A1 + kFlat * 4;      // bf16 [3136] enc2 out (P3 input, Q5 mask)
+  static constexpr int A1 = G + 784 * 4;         // bf16 img14: enc1 out (P2 input, Q6 mask)
+  static constexpr int A2 = A1 + 196 * 64;       // bf16 [3136] enc2 out (P3 input, Q5 mask)
   static constexpr int D0 = A2 + kFlat * 2;      // bf16 img49 dec_fc out (P6 input, Q2 mask)
   static constexpr int GA2 = D0;                 //   bwd img49 (D0 dead after Q2)
   static constexpr int H = D0 + kFlat * 2;       // f32 [64]
@@ -913,9 +936,11 @@ struct StepLayout {
   static constexpr int Bd = Dummy + 8192;        // f32 [3136] dec_fc bias (P5 only)
   static constexpr int GD1 = Bd;                 //   bwd bf16 img14
   static constexpr int CSB = Bd + kFlat * 4;     // f32 [32][197]
-  static constexpr int LDS = CSB + 32 * 197 * 4;
+  static constexpr int D1 = CSB + 32 * 197 * 4;  // bf16 [196][32] dec1 out (P7 input, Q1 mask)
+  static constexpr int GA2F = D1;                //   bwd f32 [3136] (D1 dead after Q1)
+  static constexpr int LDS = D1 + kFlat * 4;
   static_assert(W1 % 16 == 0 && X % 16 == 0 && G % 16 == 0 && A1 % 16 == 0 && A2 % 16 == 0 && D0 % 16 == 0 &&
-                    Dummy % 16 == 0 && Bd % 16 == 0 && CSB % 16 == 0 && LDS <= 160 * 1024,
+                    Dummy % 16 == 0 && Bd % 16 == 0 && CSB % 16 == 0 && D1 % 16 == 0 && LDS <= 160 * 1024,
                 "step LDS map");
   static_assert(196 * 64 <= kFlat * 4 && 64 * 4 + 256 * 4 <= 784 * 4 && kFlat * 2 <= 8192, "step LDS aliases");
 };
@@ -923,7 +948,7 @@ struct StepLayout {
 __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[StepLayout::LDS];
   fwd_body<StepLayout>(fa, lds);
-  __syncthreads();
+  lds_barrier();
   bwd_body<StepLayout, true>(ba, lds);
 }
 
