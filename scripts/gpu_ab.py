@@ -75,7 +75,8 @@ def command(kind, args, out, i):
         return [PY, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "20", "--warmup", "5"] + args, ROOT, \
             os.path.join(out, f"{i:02d}_driver.json")
     if kind == "launches":
-        image, b = (args + ["128", "64"])[:2] if args else ("128", "64")
+        image = args[0] if args else "128"
+        b = args[1] if len(args) > 1 else "64"
         return [PY, os.path.join(ROOT, "bench", "conv_kernels.py"), "--image", image, "--batch", b, "--reps", "20",
                 "--json", os.path.join(out, f"{i:02d}_launches.json")], ROOT, log
     if kind == "f28phases":
@@ -89,7 +90,8 @@ def command(kind, args, out, i):
         return [PY, os.path.join(ROOT, "bench", "dconv_stamps.py"), "--batch", b, "--json",
                 os.path.join(out, f"{i:02d}_dconv.json")], ROOT, log
     if kind == "prof":
-        model, b = (args + ["conv28", None])[:2]
+        model = args[0] if args else "conv28"
+        b = args[1] if len(args) > 1 else None
         d = os.path.join(out, f"{i:02d}_prof")
         return ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "prof", "--",
                 PY] + bench_args(model, b, "20", "5"), "/tmp", log
