@@ -59,6 +59,54 @@ def test_vae_hpo_packed_trials_gpu(tmp_path):
     assert (tmp_path / "results-t1-0" / "sample_2.png").exists()
 
 
+def _hpo(tmp_path, port, *args):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "vae-hpo.py"), "--ngroups", "1"] + list(args),
+                       capture_output=True, text=True, timeout=600, cwd=str(tmp_path), env=env)
+    text = r.stdout + r.stderr
+    assert r.returncode == 0, text[-4000:]
+    assert "FAILED" not in text, text[-4000:]
+    return text
+
+
+def _epoch_losses(text):
+    return {int(e): float(v) for e, v in re.findall(r"====> Epoch: (\d+) Average loss: (\d+\.\d+)", text)}
+
+
+def test_vae_hpo_conv28_ckpt_resume_gpu(tmp_path):
+    """The 28x28 conv VAE through vae-hpo on the fused HIP step: 2 epochs
+    straight vs 1 epoch + checkpoint + --resume for epoch 2. The resumed run
+    restores weights, Adam moments, step counter and data cursor, so its
+    epoch-2 loss matches the straight run's (same kernels, same order)."""
+    common = ["--model", "conv", "--train-samples", "8192", "--test-samples", "1024", "--no-results"]
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    straight = _hpo(tmp_path / "a", 29615, "--epochs", "2", *common)
+    _hpo(tmp_path / "b", 29616, "--epochs", "1", "--ckpt-dir", "ck", *common)
+    assert (tmp_path / "b" / "ck" / "trial-0" / "epoch-1.pt").exists()
+    resumed = _hpo(tmp_path / "b", 29617, "--epochs", "2", "--ckpt-dir", "ck", "--resume", *common)
+    assert "resumed trial 0" in resumed and 1 not in _epoch_losses(resumed)
+    la, lb = _epoch_losses(straight), _epoch_losses(resumed)
+    assert la[2] < la[1]
+    assert abs(la[2] - lb[2]) <= 1e-3 * la[2], (la, lb)
+    import torch
+
+    ck = torch.load(str(tmp_path / "b" / "ck" / "trial-0" / "epoch-2.pt"), weights_only=True)
+    assert ck["progress"]["epoch"] == 2 and ck["arch"]["kind"] == "conv"
+
+
+def test_vae_hpo_conv128_gpu(tmp_path):
+    """The 128x128 conv VAE (direct-conv + im2col kernels, graphs) through
+    vae-hpo for one short epoch: finite decreasing-per-log loss, PNGs, aggregate."""
+    text = _hpo(tmp_path, 29618, "--model", "conv", "--image-size", "128", "--epochs", "1",
+                "--batch-size", "64", "--train-samples", "2048", "--test-samples", "256", "--metrics-dir", "m")
+    agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
+    assert agg["samples"] == 2048 and agg["failed_trials"] == [] and agg["value"] > 1e3
+    logs = [float(x) for x in re.findall(r"Train Epoch: 1 .*Loss: (\d+\.\d+)", text)]
+    assert len(logs) >= 2 and logs[-1] < logs[0], logs
+    assert (tmp_path / "results-0" / "reconstruction_1.png").exists()
+
+
 def test_bench_trial_packing():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "50", "--warmup", "10",
                         "--trials-per-gpu", "2"],
