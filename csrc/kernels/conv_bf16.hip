@@ -150,13 +150,15 @@ __global__ void __launch_bounds__(256) wtrans_k(WtransArgs wa) {
 }
 
 __global__ void __launch_bounds__(256) combine_reparam_k(CombineReparamArgs a) {
-  __shared__ float red[2 * 256 + 16];
-  combine_reparam_body(a, red, blockIdx.x);
+  __shared__ __attribute__((aligned(16))) float red[1024 + 16];
+  if (combine_rows_ok(a.Z)) combine_reparam_rows_body(a, red, blockIdx.x);
+  else combine_reparam_body(a, red, blockIdx.x);
 }
 
 __global__ void __launch_bounds__(256) combine_reparam_bwd_k(CombineReparamBwdArgs a) {
-  __shared__ float red[256];
-  combine_reparam_bwd_body(a, red, blockIdx.x);
+  __shared__ __attribute__((aligned(16))) float red[1024];
+  if (combine_rows_ok(a.Z)) combine_reparam_bwd_rows_body(a, red, blockIdx.x);
+  else combine_reparam_bwd_body(a, red, blockIdx.x);
 }
 
 }  // namespace mdt

@@ -81,9 +81,48 @@ __host__ __device__ inline int splitk_rp(int ks) {
   while (rp < 64 && rp * 4 < ks) rp *= 2;
   return rp;
 }
+// Row form (the default where it applies: Z a power of two in [8, 512]): one
+// block per sample row. Its 2Z (forward) / Z (backward) slab columns are read
+// as float4s by Z/2 (Z/4) lanes per k-slice row -- every wave-instruction
+// covers whole 256-B+ row pieces -- with 256/lanes k-slices in flight, then a
+// fixed-order LDS combine. The element-strided form above reads 16 B of each
+// 64-B segment per wave-instruction (4x the slab bytes fetched: 16.6 MB for a
+// 4 MB slab at the 128x128 decoder Linear) and stays for other Z.
+__host__ __device__ inline bool combine_rows_ok(int Z) { return Z >= 8 && Z <= 512 && (Z & (Z - 1)) == 0; }
 __host__ __device__ inline int combine_reparam_blocks(int ks, int B, int Z) {
+  if (combine_rows_ok(Z)) return B;
   const int cnt = 256 / splitk_rp(ks);
   return (B * Z + cnt - 1) / cnt;
+}
+
+// sum_z slab[z][row0 + 4q .. +3] over k-slices z = rg, rg + RG, ... (RG =
+// 256 / LW row groups of LW float4 lanes) -> red[rg][4q .. 4q+3]; `W` = row
+// width in floats (4 LW), `MN` = slab row pitch in floats.
+__device__ __forceinline__ void combine_rows_partial(const float* slab, int ks, long long MN, long long row0, int W,
+                                                     float* red) {
+  const int LW = W >> 2, RG = 256 / LW;
+  const int t = threadIdx.x, q = t % LW, rg = t / LW;
+  float4 s = {0.f, 0.f, 0.f, 0.f};
+  const float4* p = reinterpret_cast<const float4*>(slab + row0) + q;
+  const long long pitch4 = MN >> 2;
+  auto add = [&](const float4& v) {
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  };
+  // 16 loads in flight per lane (64 KB per workgroup): the slab was written by
+  // the previous launch, so every load is a fabric round trip
+  int z = rg;
+  for (; z + 15 * RG < ks; z += 16 * RG) {
+    float4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = p[(long long)(z + u * RG) * pitch4];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) add(v[u]);
+  }
+  for (; z < ks; z += RG) add(p[(long long)z * pitch4]);
+  reinterpret_cast<float4*>(red)[rg * LW + q] = s;
 }
 
 // Encoder head: mulv = sum_z slab[z] + bias (f32 [B][2Z]); eps ~ N(0,1)
@@ -103,6 +142,45 @@ struct CombineReparamArgs {
   uint32_t stream;
   float* kld_part;
 };
+
+// `red` >= 1024 + 16 floats (16-B aligned)
+__device__ __forceinline__ void combine_reparam_rows_body(const CombineReparamArgs& a, float* red, int i) {
+  const int Z = a.Z, W = 2 * Z, RG = 1024 / W, t = threadIdx.x;
+  combine_rows_partial(a.slab, a.ks, (long long)a.B * W, (long long)i * W, W, red);
+  __syncthreads();
+  float kl = 0.f, mu = 0.f, lv = 0.f, ep = 0.f, zz = 0.f;
+  const bool own = t < Z;
+  if (own) {
+    const int c = t;
+    for (int r = 0; r < RG; ++r) {
+      mu += red[r * W + c];
+      lv += red[r * W + Z + c];
+    }
+    if (a.bias) {
+      mu += a.bias[c];
+      lv += a.bias[Z + c];
+    }
+    const long long stp = a.st->step - 1;
+    const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(i * Z + c), a.stream, (uint32_t)((unsigned long long)stp & 0xffffffffu),
+                                           (uint32_t)((unsigned long long)stp >> 32)},
+                                     a.hp->seed_lo, a.hp->seed_hi);
+    ep = normal_from_bits(bits.x, bits.y);
+    const float sd = expf(0.5f * lv);
+    zz = mu + ep * sd;
+    kl = 1.f + lv - mu * mu - sd * sd;
+  }
+  // the KLD block sum before the stores (see below)
+  const float s = block_sum(kl, red + 1024);
+  if (own) {
+    const int c = t, e = i * Z + c;
+    a.mulv[(size_t)i * W + c] = mu;
+    a.mulv[(size_t)i * W + Z + c] = lv;
+    a.eps[e] = ep;
+    a.z16[e] = (__bf16)zz;
+    if (a.z32) a.z32[e] = zz;
+  }
+  if (t == 0) a.kld_part[i] = -0.5f * s;
+}
 
 // `red` >= 2*256 + 16 floats
 __device__ __forceinline__ void combine_reparam_body(const CombineReparamArgs& a, float* red, int bid) {
@@ -166,6 +244,29 @@ struct CombineReparamBwdArgs {
   int B, Z;
   const HParams* hp;
 };
+
+// `red` >= 1024 floats (16-B aligned)
+__device__ __forceinline__ void combine_reparam_bwd_rows_body(const CombineReparamBwdArgs& a, float* red, int i) {
+  const int Z = a.Z, RG = 1024 / Z, t = threadIdx.x;
+  combine_rows_partial(a.slab, a.ks, (long long)a.B * Z, (long long)i * Z, Z, red);
+  __syncthreads();
+  if (t >= Z) return;
+  const int c = t, e = i * Z + c;
+  float g = 0.f;
+  for (int r = 0; r < RG; ++r) g += red[r * Z + c];
+  if (a.dz) a.dz[e] = g;
+  const float beta = a.hp->kl_beta;
+  const float mu = a.mulv[(size_t)i * 2 * Z + c], lv = a.mulv[(size_t)i * 2 * Z + Z + c];
+  const float sd = expf(0.5f * lv);
+  const float dm = g + beta * mu;
+  const float dl = 0.5f * g * a.eps[e] * sd + 0.5f * beta * (sd * sd - 1.f);
+  a.dmulv[(size_t)i * 2 * Z + c] = dm;
+  a.dmulv[(size_t)i * 2 * Z + Z + c] = dl;
+  if (a.dmulv16) {
+    a.dmulv16[(size_t)i * 2 * Z + c] = (__bf16)dm;
+    a.dmulv16[(size_t)i * 2 * Z + Z + c] = (__bf16)dl;
+  }
+}
 
 // `red` >= 256 floats
 __device__ __forceinline__ void combine_reparam_bwd_body(const CombineReparamBwdArgs& a, float* red, int bid) {

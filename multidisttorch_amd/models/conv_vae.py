@@ -1112,10 +1112,15 @@ class ConvVaeTrainer:
             side_cs = []
             if prev is not None:
                 omask = a_in if prev.relu else None
-                if l.name == "dec_fc":
-                    C.igemm(1, g, self._wt(l), d, None, False, None, self.dz, ws=p["ws"])
-                    C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M, self.Z,
-                                  st.hparams)
+                if l.name == "dec_fc":  # as in _backward_hip: the same reduction order
+                    ks = C.igemm_plan(1, d, True)[10]
+                    C.igemm(1, g, self._wt(l), d, None, False, None, self.dz, ws=p["ws"], combine=ks == 1)
+                    if ks > 1:
+                        C.combine_reparam_bwd(p["ws"], ks, self.mulv, self.eps, self.dmulv, self.dmulv16, self.dz,
+                                              M, self.Z, st.hparams)
+                    else:
+                        C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M, self.Z,
+                                      st.hparams)
                     gin = self.dmulv16
                     side_cs.append((gin, 2 * self.Z, p["colsum"][prev.name]))
                 elif i == len(spec) - 1 and self._thin_last:
