@@ -1203,9 +1203,20 @@ class ConvVaeTrainer:
                 self._replay(1, M)
         if self._wt_deferred() or self.f28:
             # the last step's transposed weight copies (deferred to the next
-            # step's first launch, or never needed by the fused 28x28 step):
-            # written here so w16t is current for eval / decode between calls
+            # step's first launch, or never needed by the fused 28x28 step) are
+            # stale now: eval / decode write them first (_ensure_wt)
+            self._wt_stale = True
+
+    _wt_stale = False
+
+    def _ensure_wt(self):
+        """Write the transposed weight copies (w16t) if training left them
+        stale. Only eval / decode read them outside a training step: a step of
+        the layer path writes its own in its first launch, and the fused 28x28
+        step never reads them."""
+        if self._wt_stale:
             self._wtrans_layers(1, len(self.spec))
+            self._wt_stale = False
 
     def prepare(self, batch_sizes, eval_rows=None):
         """Set-up work done once before timing starts: capture the step graphs
@@ -1260,6 +1271,7 @@ class ConvVaeTrainer:
 
     @torch.no_grad()
     def evaluate(self, X, idx, want_first_recon=True):
+        self._ensure_wt()
         idx = idx.to(device=self.device, dtype=torch.int32).contiguous()
         n = idx.numel()
         nb = -(-n // self.B)
@@ -1302,6 +1314,7 @@ class ConvVaeTrainer:
         if self.backend == "torch":
             t = self.model.decode_logits(zz)
             return torch.sigmoid(t).permute(0, 2, 3, 1).reshape(zz.shape[0], self.D)
+        self._ensure_wt()
         outs = []
         dec = [l for l in self.spec if l.name.startswith("dec")]
         for i in range(0, zz.shape[0], self.B):

@@ -22,6 +22,7 @@ def _layer_path(monkeypatch):
 def _wt_layers(tr):
     """Transposed weight copies of every layer that has a backward-data GEMM
     (the first layer's copy is never read, so the training step skips it)."""
+    tr._ensure_wt()
     return {l.name: tr._wt(l).clone() for l in tr.spec[1:]}
 
 
