@@ -38,20 +38,6 @@ namespace mdt {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// LDS-DMA (16 B per lane) issued through inline asm. The compiler's waitcnt
-// pass counts a global_load_lds built from __builtin_amdgcn_global_load_lds as
-// an out-of-order LGKM event, so with one in flight every later LDS fragment
-// read is followed by s_waitcnt lgkmcnt(0) -- the k loop then waits out the
-// full latency of the reads issued for the NEXT k-step before each MFMA. The
-// hardware tracks the DMA on vmcnt only (dc_wait_stages waits on it
-// explicitly); hidden in asm it leaves the LDS reads counted exactly
-// (lgkmcnt(N), one k-step of reads in flight). `lds_dst` must be wave-uniform.
-__device__ __forceinline__ void dc_glds16(const void* src, uint8_t* lds_dst) {
-  const uint32_t l = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_dst;
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-               ::"s"(__builtin_amdgcn_readfirstlane(l)), "v"(src) : "memory");
-}
-
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -171,7 +157,7 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
       ix = x - 1;
     }
     const bool ok = pix < CF::PR * PC && (unsigned)iy < (unsigned)WA && (unsigned)ix < (unsigned)WA;
-    dc_glds16(ok ? (const void*)(An + ((size_t)iy * WA + ix) * CA + 8 * c) : (const void*)g_zero16, patch + j * 1024);
+    glds16(ok ? (const void*)(An + ((size_t)iy * WA + ix) * CA + 8 * c) : (const void*)g_zero16, patch + j * 1024);
   }
   // ---- weight ring: stage st = k range [64 st, 64 st + 64) of BROWS rows
   auto issue_stage = [&](int st) {
@@ -185,7 +171,7 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
       size_t row;
       if constexpr (CF::CONV) row = (size_t)nb * CF::NB + r;
       else row = (size_t)(r / CF::NB) * CF::NCOLS + nb * CF::NB + (r % CF::NB);
-      dc_glds16(a.B + row * K + 64 * st + 8 * c, dst + j * 1024);
+      glds16(a.B + row * K + 64 * st + 8 * c, dst + j * 1024);
     }
   };
 #pragma unroll

@@ -512,9 +512,17 @@ __global__ void __launch_bounds__(256) igemm_fwd_k(IgArgs a) {
 // masked lanes fetch 16 zero bytes instead.
 static __device__ __attribute__((aligned(64))) uint8_t g_zero16[64];
 
+// Issued through inline asm: the compiler's waitcnt pass counts a
+// __builtin_amdgcn_global_load_lds as an out-of-order LGKM event, so with one
+// in flight every later LDS read is followed by s_waitcnt lgkmcnt(0) (a k loop
+// then waits out the reads issued for the NEXT k-step before each MFMA;
+// profiles/r2_dconv/waitcnt). The hardware counts the DMA on vmcnt only, and
+// every user waits for it explicitly (wait_tiles / dc_wait_stages) before a
+// barrier. `lds_base` must be wave-uniform.
 __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_base) {
-  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+  const uint32_t l = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_base;
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+               ::"s"(__builtin_amdgcn_readfirstlane(l)), "v"(src) : "memory");
 }
 
 // Counted wait on this wave's outstanding LDS-DMA loads: `n` newer tiles of
