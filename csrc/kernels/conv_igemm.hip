@@ -25,6 +25,7 @@
 
 #include "conv_igemm_dev.h"
 #include "conv_direct.h"
+#include "conv_dwgrad.h"
 
 namespace mdt {
 
@@ -205,9 +206,41 @@ bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p, bool al
   return true;
 }
 
+// Direct weight-gradient geometry (conv_dwgrad.h) of `d`: 0 = DwL1, 1 = DwL2,
+// -1 = none. MDT_DWGRAD=0 keeps every layer on the im2col kernel; DwL2 (the
+// 32x32x64 -> 16x16x128 layer) only with MDT_DWGRAD_L2=1: its [N][128][1024]
+// partial rows are 4x the im2col kernel's slab.
+int dwgrad_cfg(const ConvDesc& d) {
+  static const bool on = [] {
+    const char* e = getenv("MDT_DWGRAD");
+    return !(e && e[0] == '0');
+  }();
+  const char* e2 = getenv("MDT_DWGRAD_L2");  // read per plan (tests switch it inside one process)
+  const bool l2 = e2 && e2[0] == '1';
+  if (!on || d.S != 2 || d.P != 1 || d.KH != 4 || d.KW != 4 || d.H != d.W || d.OH != d.OW || d.OH * 2 != d.H)
+    return -1;
+  if (d.H == DwL1::H && d.C == DwL1::C && d.CO == DwL1::CO) return 0;
+  if (l2 && d.H == DwL2::H && d.C == DwL2::C && d.CO == DwL2::CO) return 1;
+  return -1;
+}
+
 bool plan_wgrad(const ConvDesc& d, WgradPlan* p) {
   WgradPlan q{};
   if (d.CO % 8) return false;
+  const int dw = dwgrad_cfg(d);
+  if (dw >= 0) {  // one partial row per image (the workgroups of its four kernel rows)
+    q.cfg = 100 + dw;
+    q.M = d.N * d.OH * d.OW;
+    q.K2 = d.KH * d.KW * d.C;
+    q.BM = d.CO;
+    q.BN = q.K2;
+    q.cotiles = q.ktiles = 1;
+    q.mtiles = d.N;
+    q.nsplit = d.N;
+    q.mt_per_split = 1;
+    *p = q;
+    return true;
+  }
   q.M = d.N * d.OH * d.OW;
   q.K2 = d.KH * d.KW * d.C;
   q.thin = (d.C % 8) != 0;
@@ -489,6 +522,14 @@ int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* o
   WgArgs a;
   WgradPlan q;
   if (build_wgrad(G16, X, d, out, &a, &q)) return 1;
+  if (q.cfg >= 100) {
+    if (x_is_f32) return 3;
+    const DwArgs da{reinterpret_cast<const __bf16*>(X), reinterpret_cast<const __bf16*>(G16), out, d.N};
+    if (q.cfg == 100) hipLaunchKernelGGL(dwgrad_k<DwL1>, dim3(d.N * 4), dim3(256), 0, s, da);
+    else if (q.cfg == 101) hipLaunchKernelGGL(dwgrad_k<DwL2>, dim3(d.N * 4), dim3(256), 0, s, da);
+    else return 2;
+    return (int)hipGetLastError();
+  }
   if (!q.thin && !use_glds()) {
     if (x_is_f32) return 3;
     switch (q.cfg) {

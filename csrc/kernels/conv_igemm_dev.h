@@ -1093,6 +1093,7 @@ using W5 = TileCfg<32, 16, 2, 1>;
 bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p, bool allow_direct = true,
               bool fwd = false);
 int direct_cfg(int mode, const ConvDesc& d, bool fwd);
+int dwgrad_cfg(const ConvDesc& d);
 bool plan_wgrad(const ConvDesc& d, WgradPlan* p);
 bool use_glds();
 // Kernel arguments of one forward-type GEMM; with split-K (q->ksplit > 1) `c`

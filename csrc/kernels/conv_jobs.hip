@@ -377,7 +377,8 @@ int mdt_job_wgrad(JobBlob* j, const void* G16, const void* X, int x_is_f32, Conv
   WgradPlan q;
   if (build_wgrad(G16, X, d, out, &a, &q)) return 1;
   memset(j, 0, sizeof(*j));
-  if (!q.thin) j->kind = (x_is_f32 || use_glds()) ? 0 : kJobWgrad + q.cfg;
+  if (q.cfg >= 100) j->kind = 0;  // direct weight gradient (conv_dwgrad.h): its own launch
+  else if (!q.thin) j->kind = (x_is_f32 || use_glds()) ? 0 : kJobWgrad + q.cfg;
   else j->kind = kJobWgradThin + (x_is_f32 ? 20 : 0) + q.cfg;
   j->nblk = q.cotiles * q.ktiles * q.nsplit;
   put_args(j, a);

@@ -120,3 +120,32 @@ def test_thin_tconv_patch_matches_torch(native_ext):
     bce = F.binary_cross_entropy_with_logits(t, X.flatten(), reduction="sum")
     torch.testing.assert_close(part.double().sum(), bce.double(), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(gpart.double().sum(), (p - X.flatten()).double().sum(), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("geom", [(64, 32, 64), (32, 64, 128)], ids=["64x32_to_64", "32x64_to_128"])
+def test_direct_wgrad_matches_torch(geom, native_ext, monkeypatch):
+    """Row-streamed direct weight gradient (conv_dwgrad.h): per-image partial
+    rows [N][CO][4][4][C] summed in order == conv2d_weight in fp32 (the kernel
+    accumulates bf16 products in f32; only the summation order differs)."""
+    C_ = native_ext
+    monkeypatch.setenv("MDT_DWGRAD_L2", "1")
+    H, C, CO = geom
+    OH = H // 2
+    dev = torch.device("cuda")
+    for N in (8, 5):  # XCD-grouped and plain workgroup order
+        d = [N, H, H, C, OH, OH, CO, 4, 4, 2, 1]
+        info = C_.wgrad_plan(d)
+        assert info[0] >= 100 and info[6] == N, info
+        g = torch.Generator(device="cpu").manual_seed(3 + N + H)
+        X = torch.randn(N, C, H, H, generator=g).bfloat16().float().to(dev)
+        G = torch.randn(N, CO, OH, OH, generator=g).bfloat16().float().to(dev)
+        out = torch.full((N * CO * 16 * C,), float("nan"), device=dev)
+        C_.wgrad(G.permute(0, 2, 3, 1).contiguous().bfloat16(), X.permute(0, 2, 3, 1).contiguous().bfloat16(), d,
+                 out)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all()
+        got = out.view(N, CO * 16 * C).double().sum(0)
+        ref = torch.nn.grad.conv2d_weight(X, (CO, C, 4, 4), G, stride=2, padding=1)  # [CO][C][4][4]
+        ref = ref.permute(0, 2, 3, 1).reshape(-1).double()
+        err = float((got - ref).abs().max() / ref.abs().max())
+        assert err < 1e-5, (N, err)
