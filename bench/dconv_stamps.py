@@ -75,6 +75,43 @@ def main():
             r[k] = (round(float(np.median(v)), 2), round(float(v.max()), 2))
         out[f"mode{mode}_{H}x{Cc}_{OH}x{CO}"] = r
         print(f"mode{mode} {H}x{Cc} <-> {OH}x{CO}: {r}", flush=True)
+    # direct weight gradient (conv_dwgrad.h): stamps 0 start, 1 stage 0 landed,
+    # 2 half the stages done, 3 k loop done, 4 partial row stored
+    for H, Cc, CO in ((64, 32, 64),):
+        OH = H // 2
+        d = [N, H, H, Cc, OH, OH, CO, 4, 4, 2, 1]
+        info = C.wgrad_plan(d)
+        if info[0] < 100:
+            continue
+        X = torch.randn(N * H * H * Cc, device=dev).bfloat16()
+        G = torch.randn(N * OH * OH * CO, device=dev).bfloat16()
+        o = torch.empty(N * CO * 16 * Cc, device=dev)
+        run = lambda: C.wgrad(G, X, d, o)
+        for _ in range(5):
+            run()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.reps):
+            run()
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) * 1e3 / a.reps
+        grid = N * 4
+        st = torch.zeros(grid * 8, dtype=torch.int64, device=dev)
+        C.dconv_stamps(st)
+        run()
+        torch.cuda.synchronize()
+        C.dconv_stamps(None)
+        t = st.view(grid, 8)[:, :5].cpu().numpy().astype(np.float64) * 0.01
+        ph = {"first_stage": t[:, 1] - t[:, 0], "first_half": t[:, 2] - t[:, 1], "second_half": t[:, 3] - t[:, 2],
+              "epi": t[:, 4] - t[:, 3]}
+        r = {"cfg": info[0], "grid": grid, "us": round(us, 2), "span_us": round(float(t[:, 4].max() - t[:, 0].min()), 2),
+             "start_skew_us": round(float(t[:, 0].max() - t[:, 0].min()), 2)}
+        for k, v in ph.items():
+            r[k] = (round(float(np.median(v)), 2), round(float(v.max()), 2))
+        out[f"dwgrad_{H}x{Cc}_{OH}x{CO}"] = r
+        print(f"dwgrad {H}x{Cc} -> {OH}x{CO}: {r}", flush=True)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)

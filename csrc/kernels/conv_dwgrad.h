@@ -35,6 +35,7 @@ struct DwArgs {
   const __bf16* G;  // NHWC [N][OH][OH][CO] (gradient of the conv output)
   float* out;       // [N][CO][16 C] partial rows
   int nimg;
+  unsigned long long* stamps;  // optional [grid][8] s_memrealtime (profiling, mdt_dconv_stamps)
 };
 
 template <int C_, int H_, int CO_, int RPS_, int S_>
@@ -118,6 +119,7 @@ __device__ __forceinline__ void dwgrad_body(const DwArgs& a, uint8_t* lds, int b
       glds16(src, dst + j * 1024);
     }
   };
+  dc_stamp(a.stamps, 0);
 #pragma unroll
   for (int s = 0; s < S; ++s) issue(s);
 
@@ -172,6 +174,8 @@ __device__ __forceinline__ void dwgrad_body(const DwArgs& a, uint8_t* lds, int b
     const int ahead = NST - 1 - st;
     dc_wait_stages<NIW, S - 2>(ahead < S - 2 ? ahead : S - 2);  // stage st has landed (this wave's part)
     stage_barrier();  // ... every wave's, and every wave is done with stage st-1's slot
+    if (st == 0) dc_stamp(a.stamps, 1);
+    if (st == NST / 2) dc_stamp(a.stamps, 2);
     if (st >= 1 && st - 1 + S < NST) issue(st - 1 + S);
     const uint8_t* base = lds + (st % S) * CF::STAGE;
 #pragma unroll
@@ -180,6 +184,7 @@ __device__ __forceinline__ void dwgrad_body(const DwArgs& a, uint8_t* lds, int b
       for (int k = 0; k < CF::KPR; ++k) kstep(base + r * CF::XROW, base + CF::GOFF + r * CF::GROW, 16 * k);
   }
 
+  dc_stamp(a.stamps, 3);
   // partial row n: [CO][ky*4 + kx][C]
   float* out = a.out + (size_t)n * CO * CF::K2 + (size_t)(ky * 4 + w) * C;
 #pragma unroll
@@ -191,6 +196,7 @@ __device__ __forceinline__ void dwgrad_body(const DwArgs& a, uint8_t* lds, int b
         const int co = fm * 32 + (v & 3) + 8 * (v >> 2) + 4 * half;
         out[(size_t)co * CF::K2 + fn * 32 + (lane & 31)] = acc[fm][fn][v];
       }
+  dc_stamp(a.stamps, 4);
 }
 
 template <class CF>
