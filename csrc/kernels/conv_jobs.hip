@@ -125,6 +125,22 @@ struct JobPackN {
   JobBlob j[kMaxMultiJobs];
   int start[kMaxMultiJobs + 1];
   int n;
+  // Optional in-launch hand-off from the weight-gradient jobs to a finalize
+  // job (the fused 28x28 step's launch 2): job `fin` (the LAST job, so its
+  // workgroups have the highest ids and are dispatched after every block
+  // they wait for) owns one finalize unit per block; a unit whose segment is
+  // a weight waits until every block of its layer's weight-gradient job has
+  // arrived on tickets[job], then runs the same finalize + Adam body as the
+  // stand-alone grad_finalize_k (bitwise identical result). The finalize of a
+  // layer thus overlaps the other layers' weight gradients instead of waiting
+  // for a kernel boundary behind the slowest one.
+  int fin;                     // finalize job index, -1: no hand-off
+  int first;                   // job every finalize unit waits for first (the loss / step-advance job
+                               // that writes the Adam bias-correction products), -1 none
+  int arrive[kMaxMultiJobs];   // 1: job i's blocks arrive on tickets[i]
+  int waiters[kMaxMultiJobs];  // finalize units that wait for job i
+  int* tickets;                // device int[2 * kMaxMultiJobs + 1]: arrivals, passed waiters, timeout flag
+  const int* unit_wait;        // per finalize unit: job index to wait for, -1 none
 };
 
 constexpr int kMultiLds = cmax(cmax(cmax(wgrad_lds_bytes<W0>(), wgrad_lds_bytes<W1>()),
@@ -167,13 +183,55 @@ __device__ __forceinline__ void run_multi_job(const JobBlob& j, uint8_t* lds, in
 // makes the compiler copy the whole 2.4 KB pack into per-lane scratch
 // (measured 2368 B/lane, the launch ~10x slower), and selecting it with
 // constant indices inlines every body eight times (1100+ SGPR spills).
+// Ticket wait of a finalize unit (thread 0 spins with acquire loads and
+// s_sleep back-off, bounded: tickets[2 * kMaxMultiJobs] = 1 flags a timeout
+// instead of hanging); the last waiter of job t resets its two counters for
+// the next launch (graph replays included).
+__device__ __forceinline__ void multi_wait1(const JobPackN* __restrict__ p, int t) {
+  int* tk = p->tickets;
+  const int need = p->j[t].nblk;
+  int it = 0;
+  // relaxed polls (an acquire load per poll invalidates this CU's caches every
+  // time -- measured 0.34 ms/step instead of 0.072 with ~100 polling units);
+  // the acquire is the single fence in multi_wait after the loop
+  while (__hip_atomic_load(tk + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+    if (++it > (1 << 20)) {
+      __hip_atomic_store(tk + 2 * kMaxMultiJobs, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (__hip_atomic_fetch_add(tk + kMaxMultiJobs + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+      p->waiters[t] - 1) {
+    __hip_atomic_store(tk + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(tk + kMaxMultiJobs + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ void multi_wait(const JobPackN* __restrict__ p, int t0, int t1) {
+  if (threadIdx.x == 0) {
+    if (t0 >= 0) multi_wait1(p, t0);
+    if (t1 >= 0) multi_wait1(p, t1);
+  }
+  __syncthreads();
+  __threadfence();  // acquire for every wave: the awaited jobs' stores are visible
+}
+
 __global__ void __launch_bounds__(256) jobs_multi_k(const JobPackN* __restrict__ p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kMultiLds];
   const int b = blockIdx.x;
   const int n = p->n;
   int i = 0;
   while (i + 1 < n && b >= p->start[i + 1]) ++i;
-  run_multi_job(p->j[i], lds, b - p->start[i]);
+  const int lb = b - p->start[i];
+  const int fin = p->fin;
+  if (i == fin) multi_wait(p, p->first, p->unit_wait[lb]);
+  run_multi_job(p->j[i], lds, lb);
+  if (fin >= 0 && i != fin && p->arrive[i]) {
+    __threadfence();  // every wave releases its slab stores (agent scope: other XCDs' L2s)
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(p->tickets + i, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 __host__ inline bool multi_kind_ok(int k) {
@@ -396,7 +454,7 @@ int mdt_job_thin_conv(JobBlob* j, const void* X, int x_is_f32, const float* Wf, 
   j->nblk = cdivj((long long)d.N * d.OH * d.OW, 256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
                         colsum, idx, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), B, xb,
-                        j->nblk};
+                        j->nblk, thin_conv_mfma_ok(d)};
   put_args(j, ta);
   return 0;
 }
@@ -498,10 +556,45 @@ int mdt_launch_tail(const JobBlob* wg, const JobBlob* fin0, const JobBlob* finr,
 // Returns the grid size, 0 for an unsupported kind, -1 for bad input.
 int mdt_jobs_multi_bytes() { return (int)sizeof(JobPackN); }
 
+int mdt_pack_jobs_multi_fin(const JobBlob* jobs, int n, void* dst, int fin, int first, const int* unit_wait_host,
+                            const int* unit_wait_dev, int* tickets);
+
 int mdt_pack_jobs_multi(const JobBlob* jobs, int n, void* dst) {
+  return mdt_pack_jobs_multi_fin(jobs, n, dst, -1, -1, nullptr, nullptr, nullptr);
+}
+
+// fin >= 0: job `fin` must be the last job and a finalize job with one unit
+// per block; unit_wait_host / unit_wait_dev (same contents, host copy for
+// validation) name per unit the weight-gradient job it waits for (-1 none);
+// first (>= 0): a job every unit waits for before its own (the loss / step
+// advance job whose state the Adam constants read); tickets: zeroed device
+// int[2 * kMaxMultiJobs + 1].
+int mdt_pack_jobs_multi_fin(const JobBlob* jobs, int n, void* dst, int fin, int first, const int* unit_wait_host,
+                            const int* unit_wait_dev, int* tickets) {
   if (n < 1 || n > kMaxMultiJobs) return -1;
   JobPackN p;
   memset(&p, 0, sizeof(p));
+  p.fin = -1;
+  p.first = -1;
+  if (fin >= 0) {
+    if (fin != n - 1 || jobs[fin].kind != kJobFinalize || !unit_wait_host || !unit_wait_dev || !tickets) return -1;
+    if (first >= fin || (first >= 0 && jobs[first].kind != kJobLossStep && jobs[first].kind != kJobLoss)) return -1;
+    if (first >= 0) p.waiters[first] = jobs[fin].nblk;
+    p.first = first;
+    for (int u = 0; u < jobs[fin].nblk; ++u) {
+      const int t = unit_wait_host[u];
+      if (t < -1 || t >= fin || (t >= 0 && t == first)) return -1;
+      if (t >= 0) {
+        const int k = jobs[t].kind;
+        if (!((k >= kJobWgrad && k <= kJobWgrad + 5) || (k >= kJobWgradThin && k <= kJobWgradThin + 25))) return -1;
+        p.waiters[t] += 1;
+      }
+    }
+    for (int i = 0; i < fin; ++i) p.arrive[i] = p.waiters[i] > 0;
+    p.fin = fin;
+    p.tickets = tickets;
+    p.unit_wait = unit_wait_dev;
+  }
   int grid = 0;
   for (int i = 0; i < n; ++i) {
     if (jobs[i].nblk <= 0) return -1;

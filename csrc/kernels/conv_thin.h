@@ -2,6 +2,8 @@
 // conv_thin.hip for the design). Included by conv_thin.hip (stand-alone
 // kernels) and conv_igemm.hip (horizontally fused job kernels).
 #pragma once
+#include <stdlib.h>
+
 #include "common.h"
 #include "conv_igemm.h"
 #include "vae_mlp.h"
@@ -47,14 +49,36 @@ struct ThinConvArgs {
   int B;
   float* xb;
   int nblk;
+  int mfma;            // 1: thin_conv_mfma_body (host: thin_conv_mfma_ok)
 };
+
+// Geometry of the MFMA form of thin_conv (the 128x128 model's enc1 and its
+// last layer's backward-data): CO = 32, k4 s2 p1, 64-wide output rows, four
+// output rows per 256-pixel workgroup. MDT_THIN_MFMA=0 keeps the VALU body.
+__host__ inline int thin_conv_mfma_ok(const ConvDesc& d) {
+  static const bool on = [] {
+    const char* e = getenv("MDT_THIN_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  return on && d.C == 1 && d.CO == 32 && d.KH == 4 && d.KW == 4 && d.S == 2 && d.P == 1 && d.OW == 64 &&
+         d.W == 2 * d.OW && d.H == 2 * d.OH && d.OH % 4 == 0;
+}
 
 // LDS: staged weights [TAPS][CO] + the colsum transpose (256 x (CO+1)).
 template <int CO, int K>
 constexpr int thin_conv_lds_bytes() { return (K * K * CO + 256 * (CO + 1)) * 4; }
 
+template <typename TIN>
+__device__ void thin_conv_mfma_body(const ThinConvArgs& ta, uint8_t* lds, int bid);
+
 template <int CO, int K, typename TIN>
 __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* lds, int bid) {
+  if constexpr (CO == 32 && K == 4) {
+    if (ta.mfma) {
+      thin_conv_mfma_body<TIN>(ta, lds, bid);
+      return;
+    }
+  }
   constexpr int TAPS = K * K;
   const ConvDesc& d = ta.d;
   const TIN* X = reinterpret_cast<const TIN*>(ta.X);
@@ -487,6 +511,317 @@ __device__ __forceinline__ void thin_tconv_patch_body(const ThinTconvArgs& ta, u
       const float gs = block_sum(gsum, scratch);
       if (threadIdx.x == 0) ta.gpart[bid] = gs;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA forms of the 128x128 edge layers (round 2). The VALU bodies above read
+// every weight as a wave-uniform ds_read_b128 broadcast: an LDS instruction
+// costs the same 8 clocks for one broadcast address as for 64 distinct ones,
+// so per output pixel they spent ~2x more LDS time on weights than on data and
+// ran LDS-bound at 16-23 us per 128x128 B=64 call. Here the weights are MFMA
+// A fragments held in VGPRs for the whole workgroup, the activations are the B
+// operand read once per tap from the LDS patch, and the f32 master weights are
+// split w = hi + lo (two bf16, |w - hi - lo| <= 2^-18 |w|) so the result
+// matches the f32-weight VALU kernels to ~1e-6 relative.
+__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
+  hi = (__bf16)v;
+  lo = (__bf16)(v - (float)hi);
+}
+
+// Transposed conv 32 -> 1 (k4 s2 p1, 64^2 -> 128^2) + fused BCE, MFMA form.
+// Same grid / partial layout as thin_tconv_patch_body<32, 64> (one workgroup =
+// one image's 4 class-grid rows, wave w = row j0 + w, four 16-pixel tiles).
+// GEMM per tile (v_mfma_f32_16x16x32_bf16): D[16 x 16 px] = A[16 x K] B[K x 16
+// px], K = 9 neighbours x 32 channels (one k-step per 3x3 neighbour); A rows
+// 0-3 = hi weights of parity class (ca, cb) = (r >> 1, r & 1), rows 4-7 = lo,
+// rows 8-11 = lo2 = bf16(w - hi - lo) (three bf16 terms: the f32 weight to
+// ~2^-26), rows 12-15 zero; B = the bf16 activations of
+// the tile's 16 pixels at that neighbour straight from the swizzled patch.
+// Rows 0-3 + 4-7 + 8-11 (lanes l, l^16, l^32) are the four outputs of each
+// pixel; they go through a wave-private LDS row pair so the BCE epilogue runs
+// one float4 of an output row per lane.
+constexpr int kTcMfmaPatch = 6 * 66 * 64;  // (R + 2) x (WS + 2) pixels x 64 B
+constexpr int thin_tconv_mfma_lds_bytes() { return kTcMfmaPatch + 16 * 32 * 4 + 4 * 256 * 4 + 16 * 4; }
+
+__device__ __forceinline__ void thin_tconv_mfma_body(const ThinTconvArgs& ta, uint8_t* lds, int bid) {
+  constexpr int R = 4, WS = 64, PC = WS + 2, PB = 64, CO = 32;
+  const ConvDesc& d = ta.d;
+  const int rbn = d.OH / R;
+  const int n = bid / rbn, j0 = (bid - n * rbn) * R;
+  uint8_t* patch = lds;
+  float* wl = reinterpret_cast<float*>(lds + kTcMfmaPatch);  // [16 taps][32 ch]
+  float* obuf = wl + 16 * CO;                                  // [4 waves][2][128]
+  float* scratch = obuf + 4 * 256;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const __bf16* Gn = ta.G + (size_t)n * d.OH * d.OW * CO;
+  // this lane's epilogue pixels: output row 2 j + u, columns c4 .. c4 + 3;
+  // the BCE target is loaded first so its latency overlaps everything below
+  const int u = lane >> 5, c4 = (lane & 31) * 4;
+  const size_t e_out = ((size_t)n * d.H + 2 * (j0 + w) + u) * d.W + c4;
+  float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ta.X) x4 = *reinterpret_cast<const float4*>(ta.X + e_out);
+  // patch fill, unrolled: every 16-B load is issued before the first LDS
+  // store waits (a rolled loop paid one HBM round trip per iteration)
+  constexpr int NFILL = (R + 2) * PC * 4, NIT = (NFILL + 255) / 256;
+  bf16x8 fv[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + it * 256;
+    const int pix = e >> 2, q = e & 3;
+    const int y = pix / PC, x = pix - y * PC;
+    const int gy = j0 - 1 + y, gx = x - 1;
+    const bool ok = e < NFILL && (unsigned)gy < (unsigned)d.OH && (unsigned)gx < (unsigned)d.OW;
+    fv[it] = *reinterpret_cast<const bf16x8*>(Gn + (ok ? ((size_t)gy * d.OW + gx) * CO + 8 * q : 0));
+    if (!ok) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) fv[it][k] = (__bf16)0.f;
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + it * 256;
+    const int pix = e >> 2, q = e & 3;
+    const int y = pix / PC, x = pix - y * PC;
+    if (e < NFILL) *reinterpret_cast<bf16x8*>(patch + pix * PB + 16 * (q ^ ((x >> 2) & 3))) = fv[it];
+  }
+  for (int e = tid; e < 16 * CO; e += 256) {  // Wf [ch][ky][kx] -> wl[tap][ch]
+    const int c = e >> 4, tap = e & 15;
+    wl[tap * CO + c] = ta.Wf[e];
+  }
+  __syncthreads();
+  // A fragments: lane row m = lane & 15, channels 8 kq .. 8 kq + 7
+  const int m = lane & 15, kq = lane >> 4;
+  bf16x8 af[9];
+#pragma unroll
+  for (int nb = 0; nb < 9; ++nb) {
+    const int r = nb / 3, c = nb - 3 * (nb / 3);
+    const int cls = m & 3, ca = cls >> 1, cb = cls & 1;
+    const int ty = 2 - ca - r, tx = 2 - cb - c;
+    const bool ok = m < 12 && (unsigned)ty < 2u && (unsigned)tx < 2u;
+    const int tap = ok ? (ca + 2 * ty) * 4 + cb + 2 * tx : 0;
+    const float4 w0 = *reinterpret_cast<const float4*>(wl + tap * CO + 8 * kq);
+    const float4 w1 = *reinterpret_cast<const float4*>(wl + tap * CO + 8 * kq + 4);
+    const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 hi, lo;
+      split_bf16(wv[e], hi, lo);
+      const __bf16 lo2 = (__bf16)(wv[e] - (float)hi - (float)lo);
+      af[nb][e] = ok ? (m < 4 ? hi : (m < 8 ? lo : lo2)) : (__bf16)0.f;
+    }
+  }
+  const float b0 = ta.bias ? ta.bias[0] : 0.f;
+  float* ob = obuf + w * 256;
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    const int x0 = 16 * t + (lane & 15);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nb = 0; nb < 9; ++nb) {
+      const int r = nb / 3, c = nb - 3 * (nb / 3);
+      const int x = x0 + c;
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(patch + ((w + r) * PC + x) * PB + 16 * (kq ^ ((x >> 2) & 3)));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nb], bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {  // rows r + 4 r' (hi, lo, lo2): lanes l, l ^ 16, l ^ 32
+      acc[rr] += __shfl_xor(acc[rr], 16, 64);
+      acc[rr] += __shfl_xor(acc[rr], 32, 64);
+    }
+    if (lane < 16) {  // class (ca, cb) -> output row 1 - ca, column 2 i + 1 - cb
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) ob[(1 - (rr >> 1)) * 128 + 2 * x0 + 1 - (rr & 1)] = acc[rr] + b0;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const float4 tv4 = *reinterpret_cast<const float4*>(ob + u * 128 + c4);
+  const size_t e = e_out;
+  if (ta.y32) *reinterpret_cast<float4*>(ta.y32 + e) = tv4;
+  if (!ta.X) return;
+  const float tv[4] = {tv4.x, tv4.y, tv4.z, tv4.w}, xv[4] = {x4.x, x4.y, x4.z, x4.w};
+  float pv[4], gv[4], loss = 0.f, gsum = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float tq = tv[q], xq = xv[q];
+    const float p = 1.f / (1.f + expf(-tq));
+    pv[q] = p;
+    gv[q] = p - xq;
+    const float sp_pos = fmaxf(tq, 0.f) + log1pf(expf(-fabsf(tq)));
+    loss += xq * fminf(sp_pos - tq, 100.f) + (1.f - xq) * fminf(sp_pos, 100.f);
+    gsum += gv[q];
+  }
+  if (ta.dlog) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 g4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g4[q] = (__bf16)gv[q];
+    *reinterpret_cast<bf16x4*>(ta.dlog + e) = g4;
+  }
+  if (ta.recon) *reinterpret_cast<float4*>(ta.recon + e) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+  const float sl = block_sum(loss, scratch);
+  if (threadIdx.x == 0) ta.part[bid] = sl;
+  if (ta.gpart) {
+    __syncthreads();
+    const float gs = block_sum(gsum, scratch);
+    if (threadIdx.x == 0) ta.gpart[bid] = gs;
+  }
+}
+
+// Conv 1 -> 32 (k4 s2 p1, 64-wide output rows), MFMA form of thin_conv_body:
+// the 128x128 model's first layer (f32 input gathered from the dataset, bias,
+// ReLU) and its last layer's backward-data (bf16 dlogits, ReLU-backward mask,
+// bias-gradient column sums). Workgroup = 4 output rows (256 pixels: the same
+// blocks, hence the same colsum rows, as the VALU body), wave w = row oy0 + w,
+// four 16-pixel tiles. D[32 co x 16 px] = A[co][k] B[k][px] with k = 16 taps
+// of x_hi then 16 taps of x_lo (x = x_hi + x_lo, two bf16; x_lo = 0 for bf16
+// input) and A = [W_hi | W_hi], [W_lo | W_lo], [W_lo2 | W_lo2] (three bf16
+// terms of the f32 weight): the f32 product to ~2^-17 of |x w| (the x split;
+// exact for bf16 input). A rows are ordered co = 8 (m >> 2) + 4 mt + (m & 3), so lane (q, px)
+// ends with channels 8q .. 8q + 7 of its pixel: one 16-B NHWC store.
+constexpr int kTcPitch = 132;  // patch row pitch (floats): column ix at ix + 1
+template <typename TIN>
+__device__ void thin_conv_mfma_body(const ThinConvArgs& ta, uint8_t* lds, int bid) {
+  const ConvDesc& d = ta.d;
+  const TIN* X = reinterpret_cast<const TIN*>(ta.X);
+  float* patch = reinterpret_cast<float*>(lds);  // [10][kTcPitch] f32
+  float* red = patch + 10 * kTcPitch;            // [4][32]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rbn = d.OH / 4;
+  const int n = bid / rbn, oy0 = (bid - n * rbn) * 4;
+  const int* rows = ta.idx ? ta.idx + (size_t)ta.st->cursor * ta.B : nullptr;
+  const TIN* img = X + (size_t)(rows ? rows[n] : n) * d.H * d.W;
+  if (ta.xb) {
+    const int p4 = (d.H * d.W) >> 2;
+    const long long tot = (long long)d.N * p4;
+    for (long long e = (long long)bid * blockDim.x + tid; e < tot; e += (long long)ta.nblk * blockDim.x) {
+      const int i = (int)(e / p4), c = (int)(e - (long long)i * p4);
+      reinterpret_cast<float4*>(ta.xb + (size_t)i * d.H * d.W)[c] =
+          reinterpret_cast<const float4*>(X + (size_t)(rows ? rows[i] : i) * d.H * d.W)[c];
+    }
+  }
+  if (ta.hp && bid == 0 && tid == 0) {
+    TrainState* st = ta.st;
+    st->step = st->step + 1;
+    st->b1pow *= ta.hp->beta1_d;
+    st->b2pow *= ta.hp->beta2_d;
+  }
+  // input rows 2 oy0 - 1 .. 2 oy0 + 8, columns -1 .. 128 (zero padding
+  // stored; thin_conv_mfma_ok fixes W = 128), unrolled so every load is in
+  // flight before the first LDS store waits
+  constexpr int WP = 130, NFILL = 10 * WP, NIT = (NFILL + 255) / 256;
+  float fv[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + it * 256;
+    const int y = e / WP, xx = e - y * WP;
+    const int iy = 2 * oy0 - 1 + y, ix = xx - 1;
+    const bool ok = e < NFILL && (unsigned)iy < (unsigned)d.H && (unsigned)ix < 128u;
+    const float v = (float)img[ok ? iy * 128 + ix : 0];
+    fv[it] = ok ? v : 0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + it * 256;
+    const int y = e / WP, xx = e - y * WP;
+    if (e < NFILL) patch[y * kTcPitch + xx] = fv[it];
+  }
+  // A fragments (weights), lane row m = lane & 15, taps 8 (kq & 1) .. + 7
+  const int m = lane & 15, kq = lane >> 4, q = kq;
+  bf16x8 ahi[2], alo[2], alo2[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int co = 8 * (m >> 2) + 4 * mt + (m & 3);
+    const float4 w0 = *reinterpret_cast<const float4*>(ta.Wf + co * 16 + 8 * (kq & 1));
+    const float4 w1 = *reinterpret_cast<const float4*>(ta.Wf + co * 16 + 8 * (kq & 1) + 4);
+    const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 hi, lo;
+      split_bf16(wv[e], hi, lo);
+      ahi[mt][e] = hi;
+      alo[mt][e] = lo;
+      alo2[mt][e] = (__bf16)(wv[e] - (float)hi - (float)lo);
+    }
+  }
+  float bv[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) bv[c] = ta.bias ? ta.bias[8 * q + c] : 0.f;
+  __syncthreads();
+  const int oy = oy0 + w;
+  float cs[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) cs[c] = 0.f;
+  bf16x8 mks[4];
+  if (ta.omask) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      mks[t] = *reinterpret_cast<const bf16x8*>(ta.omask + (((size_t)n * d.OH + oy) * d.OW + 16 * t + (lane & 15)) *
+                                                               32 + 8 * q);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ox = 16 * t + (lane & 15);
+    const size_t pix = ((size_t)n * d.OH + oy) * d.OW + ox;
+    const bf16x8 mk = mks[t];
+    bf16x8 b;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const float* pr = patch + (2 * w + 2 * (kq & 1) + r) * kTcPitch + 2 * ox;
+      const float2 u0 = *reinterpret_cast<const float2*>(pr), u1 = *reinterpret_cast<const float2*>(pr + 2);
+      const float xv[4] = {u0.x, u0.y, u1.x, u1.y};
+#pragma unroll
+      for (int kx = 0; kx < 4; ++kx) {
+        __bf16 hi, lo;
+        split_bf16(xv[kx], hi, lo);
+        b[4 * r + kx] = kq < 2 ? hi : lo;
+      }
+    }
+    f32x4 acc[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[mt], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[mt], b, acc[mt], 0, 0, 0);
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo2[mt], b, acc[mt], 0, 0, 0);
+    }
+    float v[8];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) v[4 * mt + rr] = acc[mt][rr] + bv[4 * mt + rr];
+    if (ta.relu) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = fmaxf(v[c], 0.f);
+    }
+    if (ta.omask) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = (float)mk[c] > 0.f ? v[c] : 0.f;
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      o[c] = (__bf16)v[c];
+      cs[c] += v[c];
+    }
+    *reinterpret_cast<bf16x8*>(ta.y16 + pix * 32 + 8 * q) = o;
+  }
+  if (ta.colsum) {  // column sums: 16 pixel lanes, then the 4 waves in order
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float s = cs[c];
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 4, 64);
+      s += __shfl_xor(s, 8, 64);
+      cs[c] = s;
+    }
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) red[w * 32 + 8 * q + c] = cs[c];
+    }
+    __syncthreads();
+    if (tid < 32) ta.colsum[(size_t)bid * 32 + tid] = red[tid] + red[32 + tid] + red[64 + tid] + red[96 + tid];
   }
 }
 

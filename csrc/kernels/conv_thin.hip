@@ -38,6 +38,11 @@ __global__ void __launch_bounds__(256) thin_tconv_patch_k(ThinTconvArgs ta) {
   thin_tconv_patch_body<CO, WS>(ta, lds, blockIdx.x);
 }
 
+__global__ void __launch_bounds__(256) thin_tconv_mfma_k(ThinTconvArgs ta) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[thin_tconv_mfma_lds_bytes()];
+  thin_tconv_mfma_body(ta, lds, blockIdx.x);
+}
+
 template <int CO, int K, int S>
 __global__ void __launch_bounds__(256) thin_tconv_k(ThinTconvArgs ta) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[thin_tconv_lds_bytes<CO, K, S>()];
@@ -63,7 +68,7 @@ int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, cons
   dim3 grid(cdiv_t(M, 256)), blk(256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
                         colsum, idx, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), B, xb,
-                        (int)grid.x};
+                        (int)grid.x, thin_conv_mfma_ok(d)};
 #define THIN(CO_)                                                                     \
   {                                                                                   \
     if (x_is_f32)                                                                     \
@@ -106,6 +111,16 @@ static bool tconv_patch_ok(const ConvDesc& d) {
          d.H == 2 * d.OH && d.OW == 64;
 }
 
+// MFMA form of the patch kernel (thin_tconv_mfma_body, same grid and
+// partials); MDT_THIN_MFMA=0 keeps the VALU patch kernel.
+static bool thin_mfma_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDT_THIN_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int mdt_thin_blocks(int tconv, ConvDesc d) {
   if (!tconv) return cdiv_t((long long)d.N * d.OH * d.OW, 256);
   if (tconv_patch_ok(d)) return d.N * (d.OH / 4);
@@ -122,7 +137,10 @@ int mdt_thin_tconv(const void* G16, const float* Wf, ConvDesc d, const float* bi
   if (tconv_patch_ok(d)) {
     const ThinTconvArgs tp{reinterpret_cast<const __bf16*>(G16), Wf, d, bias, y32, X,
                            reinterpret_cast<__bf16*>(dlog16), recon, part, gpart, gx};
-    hipLaunchKernelGGL((thin_tconv_patch_k<32, 64>), dim3(d.N * (d.OH / 4)), dim3(256), 0, s, tp);
+    if (thin_mfma_on())
+      hipLaunchKernelGGL(thin_tconv_mfma_k, dim3(d.N * (d.OH / 4)), dim3(256), 0, s, tp);
+    else
+      hipLaunchKernelGGL((thin_tconv_patch_k<32, 64>), dim3(d.N * (d.OH / 4)), dim3(256), 0, s, tp);
     return (int)hipGetLastError();
   }
   if (tconv4_ok(d)) {  // one thread per input position: all four parity classes

@@ -65,6 +65,8 @@ int mdt_job_loss(mdt::JobBlob* j, const float* bce_part, int nb, const float* kl
 int mdt_launch_jobs(const mdt::JobBlob* jobs, int n, hipStream_t s);
 int mdt_jobs_multi_bytes();
 int mdt_pack_jobs_multi(const mdt::JobBlob* jobs, int n, void* dst);
+int mdt_pack_jobs_multi_fin(const mdt::JobBlob* jobs, int n, void* dst, int fin, int first,
+                            const int* unit_wait_host, const int* unit_wait_dev, int* tickets);
 int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s);
 int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train, hipStream_t s);
 int mdt_f28_backward(const long long* p, int M, hipStream_t s);
@@ -354,7 +356,13 @@ bool launch_jobs(const std::vector<Job*>& jobs) {
 // Pack recorded jobs (any supported kinds, up to 8) into a job table for ONE
 // jobs_multi_k launch: returns (uint8 CPU tensor image, grid). The caller keeps
 // the table in device memory for the lifetime of the plan (graph replays).
-std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs) {
+// fin >= 0 (the last job, a finalize job): in-launch weight-gradient ->
+// finalize hand-off (conv_jobs.hip JobPackN); unit_wait = device int32 [units]
+// (job index each finalize unit waits for, -1 none), tickets = zeroed device
+// int32 [17] owned by the caller for the lifetime of the pack.
+std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs, int64_t fin, int64_t first,
+                                                const c10::optional<at::Tensor>& unit_wait,
+                                                const c10::optional<at::Tensor>& tickets) {
   TORCH_CHECK(!jobs.empty() && jobs.size() <= 8, "pack_jobs_multi takes 1..8 jobs");
   std::vector<JobBlob> v;
   for (auto* j : jobs) {
@@ -363,7 +371,22 @@ std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs) {
     v.push_back(j->main);
   }
   auto img = torch::zeros({(int64_t)mdt_jobs_multi_bytes()}, torch::kUInt8);
-  const int grid = mdt_pack_jobs_multi(v.data(), (int)v.size(), img.data_ptr());
+  int grid;
+  if (fin >= 0) {
+    TORCH_CHECK(unit_wait.has_value() && tickets.has_value(), "pack_jobs_multi: fin needs unit_wait and tickets");
+    const at::Tensor& uw = *unit_wait;
+    const at::Tensor& tk = *tickets;
+    TORCH_CHECK(uw.is_cuda() && uw.scalar_type() == torch::kInt32 && uw.is_contiguous() && uw.dim() == 1 &&
+                    uw.numel() == v[fin].nblk, "pack_jobs_multi: unit_wait must be device int32 [finalize units]");
+    TORCH_CHECK(tk.is_cuda() && tk.scalar_type() == torch::kInt32 && tk.is_contiguous() && tk.numel() >= 17,
+                "pack_jobs_multi: tickets must be device int32 [>= 17]");
+    auto uw_host = uw.cpu();
+    grid = mdt_pack_jobs_multi_fin(v.data(), (int)v.size(), img.data_ptr(), (int)fin, (int)first,
+                                   uw_host.data_ptr<int>(),
+                                   uw.data_ptr<int>(), tk.data_ptr<int>());
+  } else {
+    grid = mdt_pack_jobs_multi(v.data(), (int)v.size(), img.data_ptr());
+  }
   TORCH_CHECK(grid > 0, "pack_jobs_multi: unsupported job kind or bad job (", grid, ")");
   return {img, (int64_t)grid};
 }
@@ -670,7 +693,9 @@ void bind_conv(pybind11::module& m) {
       .def_property_readonly("kind", &Job::kind)
       .def_property_readonly("has_post", &Job::has_post);
   m.def("launch_jobs", &launch_jobs);
-  m.def("pack_jobs_multi", &pack_jobs_multi);
+  m.def("pack_jobs_multi", &pack_jobs_multi, py::arg("jobs"), py::arg("fin") = -1, py::arg("first") = -1,
+        py::arg("unit_wait") = py::none(),
+        py::arg("tickets") = py::none());
   m.def("launch_jobs_multi", &launch_jobs_multi);
   m.def("f28_forward", &f28_forward, py::arg("tensors"), py::arg("B"), py::arg("M"), py::arg("stream"),
         py::arg("train"));

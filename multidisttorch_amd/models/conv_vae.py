@@ -267,6 +267,15 @@ class ConvVaeTrainer:
         self.f28_skip_adam = False  # tests: leave the reduced gradients in `grads`, no update
         # forward and backward of the fused step in one launch (MDT_F28_MERGE=0: two)
         self.f28_merge = os.getenv("MDT_F28_MERGE", "1") != "0"
+        # finalize + Adam as the last job of the weight-gradient launch, each
+        # unit released by its layer's ticket (conv_jobs.hip JobPackN): 2
+        # launches per step instead of 3. Bitwise-tested but measured 4x
+        # SLOWER (0.31 vs 0.072 ms/step, profiles/r2_fin): every cross-XCD
+        # hand-off needs an agent-scope release (L2 write-back) per
+        # weight-gradient block and an acquire (L2 invalidate) per finalize
+        # unit, which evicts the L2 working set of the blocks still running.
+        # Opt-in: MDT_F28_FIN=1.
+        self.f28_fin = os.getenv("MDT_F28_FIN", "0") == "1"
         # profiling: int64 [B*16] tensors (fwd, bwd) receiving per-workgroup
         # phase-end s_memrealtime stamps (obs/f28_phases.py); None = off
         self.f28_stamps = (None, None)
@@ -1038,6 +1047,20 @@ class ConvVaeTrainer:
         p = dict(fwd=fwd, bwd=bwd, jobs=jobs, jobs_pack=pack.to(dev), jobs_grid=grid, slabs=slabs,
                  segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
                  nunits=len(units))
+        if self.f28_fin:
+            # weight-gradient jobs 0..5 (srcs order), loss/step job 6, finalize
+            # job 7: a weight unit waits for its layer's job, every unit for the
+            # step-advance job (the Adam bias corrections it writes)
+            jf = C.Job()
+            C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
+                            len(units), st.train_state, st.hparams, True, job=jf)
+            names = list(srcs)
+            uw = [names.index(self.spec[si // 2].name) if si % 2 == 0 else -1 for si, _s, _c in units]
+            p["unit_wait"] = torch.tensor(uw, dtype=torch.int32, device=dev)
+            p["tickets"] = torch.zeros(17, dtype=torch.int32, device=dev)
+            packf, gridf = C.pack_jobs_multi(jobs + [jf], fin=len(jobs), first=len(jobs) - 1,
+                                             unit_wait=p["unit_wait"], tickets=p["tickets"])
+            p.update(jf=jf, fin_pack=packf.to(dev), fin_grid=gridf)
         self._plans28[M] = p
         return p
 
@@ -1052,8 +1075,11 @@ class ConvVaeTrainer:
         else:
             C.f28_forward(p["fwd"], self.B, M, self.rng_stream, True)
             C.f28_backward(p["bwd"], M)
-        C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
         red = self.reducer
+        if self.f28_fin and red is None and not self.f28_skip_adam:
+            C.launch_jobs_multi(p["fin_pack"], p["fin_grid"])
+            return
+        C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
         C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
                         p["nunits"], st.train_state, st.hparams, red is None and not self.f28_skip_adam)
         if red is not None:
