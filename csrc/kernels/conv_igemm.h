@@ -114,6 +114,7 @@ enum JobKindBase : int {
   kJobIgemm = 1000,      // + mode*100 + cfg  (bf16, vector gathers)
   kJobWgrad = 2000,      // + cfg              (bf16, vector gathers)
   kJobWgradThin = 2050,  // + 20*f32 + cfg     (per-element gathers)
+  kJobThinWgM = 2100,    // + f32               (MFMA single-channel weight gradient, conv_thin_wg.h)
   kJobThinConv = 3000,   // + CO + 100*f32
   kJobThinTconv = 4000,  // + CO
   kJobColsum = 5000,

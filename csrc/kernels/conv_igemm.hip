@@ -26,6 +26,7 @@
 #include "conv_igemm_dev.h"
 #include "conv_direct.h"
 #include "conv_dwgrad.h"
+#include "conv_thin_wg.h"
 
 namespace mdt {
 
@@ -227,6 +228,20 @@ int dwgrad_cfg(const ConvDesc& d) {
 bool plan_wgrad(const ConvDesc& d, WgradPlan* p) {
   WgradPlan q{};
   if (d.CO % 8) return false;
+  if (thin_wgrad_mfma_ok(d)) {  // conv_thin_wg.h: one partial row per 4 output rows
+    q.cfg = 110;
+    q.thin = true;
+    q.M = d.N * d.OH * d.OW;
+    q.K2 = d.KH * d.KW * d.C;
+    q.BM = d.CO;
+    q.BN = q.K2;
+    q.cotiles = q.ktiles = 1;
+    q.mtiles = d.N * d.OH / 4;
+    q.nsplit = q.mtiles;
+    q.mt_per_split = 1;
+    *p = q;
+    return true;
+  }
   const int dw = dwgrad_cfg(d);
   if (dw >= 0) {  // one partial row per image (the workgroups of its four kernel rows)
     q.cfg = 100 + dw;
@@ -348,6 +363,12 @@ int build_wgrad(const void* G16, const void* X, ConvDesc d, float* out, WgArgs* 
   *pa = a;
   *pq = q;
   return 0;
+}
+
+template <typename XT>
+__global__ void __launch_bounds__(256) thin_wgrad_k(WgArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[thin_wgrad_mfma_lds_bytes()];
+  thin_wgrad_mfma_body<XT>(a, lds, blockIdx.x);
 }
 
 static unsigned long long* g_dc_stamps = nullptr;
@@ -522,6 +543,11 @@ int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* o
   WgArgs a;
   WgradPlan q;
   if (build_wgrad(G16, X, d, out, &a, &q)) return 1;
+  if (q.cfg == 110) {
+    if (x_is_f32) hipLaunchKernelGGL(thin_wgrad_k<float>, dim3(q.nsplit), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(thin_wgrad_k<__bf16>, dim3(q.nsplit), dim3(256), 0, s, a);
+    return (int)hipGetLastError();
+  }
   if (q.cfg >= 100) {
     if (x_is_f32) return 3;
     const DwArgs da{reinterpret_cast<const __bf16*>(X), reinterpret_cast<const __bf16*>(G16), out, d.N, g_dc_stamps};

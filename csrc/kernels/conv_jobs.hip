@@ -24,6 +24,7 @@
 #include "conv_igemm_dev.h"
 #include "conv_small.h"
 #include "conv_thin.h"
+#include "conv_thin_wg.h"
 
 namespace mdt {
 using namespace tiles;
@@ -68,6 +69,14 @@ struct JWgThin {
   static constexpr int ID = kJobWgradThin + (sizeof(XT) == 4 ? 20 : 0) + CFG, LDS = wgrad_lds_bytes<TC>();
   static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
     wgrad_body<XT, false, TC>(job_args<WgArgs>(j), lds, b, j.nblk);
+  }
+};
+
+template <typename XT>
+struct JThinWg {
+  static constexpr int ID = kJobThinWgM + (sizeof(XT) == 4 ? 1 : 0), LDS = thin_wgrad_mfma_lds_bytes();
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    thin_wgrad_mfma_body<XT>(job_args<WgArgs>(j), lds, b);
   }
 };
 
@@ -326,6 +335,8 @@ using WgT5 = JWgThin<__bf16, 5, W5>;
 using WgT5f = JWgThin<float, 5, W5>;
 using ThinC32 = JThinConv<32, __bf16>;
 using ThinC32f = JThinConv<32, float>;
+using TwB = JThinWg<__bf16>;
+using TwF = JThinWg<float>;
 using Wg0 = JWg<0, W0>;
 using Wg1 = JWg<1, W1>;
 using IgC1 = JIg<kModeConv, 1, F1>;
@@ -343,6 +354,9 @@ const Combo kCombos[] = {
     // last layer: thin weight gradient || thin backward-data || loss reduction
     COMBO3(WgT5, ThinC32, JLoss),
     COMBO2(WgT5, ThinC32),
+    COMBO3(TwB, ThinC32, JLoss),
+    COMBO2(TwB, ThinC32),
+    COMBO2(TwF, JFinalize),
     // transposed-conv layers: conv-mode backward-data || weight gradient
     COMBO2(IgC5, Wg0),
     COMBO2(IgC1, Wg0),
@@ -435,7 +449,8 @@ int mdt_job_wgrad(JobBlob* j, const void* G16, const void* X, int x_is_f32, Conv
   WgradPlan q;
   if (build_wgrad(G16, X, d, out, &a, &q)) return 1;
   memset(j, 0, sizeof(*j));
-  if (q.cfg >= 100) j->kind = 0;  // direct weight gradient (conv_dwgrad.h): its own launch
+  if (q.cfg == 110) j->kind = kJobThinWgM + (x_is_f32 ? 1 : 0);  // MFMA thin weight gradient
+  else if (q.cfg >= 100) j->kind = 0;  // direct weight gradient (conv_dwgrad.h): its own launch
   else if (!q.thin) j->kind = (x_is_f32 || use_glds()) ? 0 : kJobWgrad + q.cfg;
   else j->kind = kJobWgradThin + (x_is_f32 ? 20 : 0) + q.cfg;
   j->nblk = q.cotiles * q.ktiles * q.nsplit;

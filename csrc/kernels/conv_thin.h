@@ -54,15 +54,29 @@ struct ThinConvArgs {
 
 // Geometry of the MFMA form of thin_conv (the 128x128 model's enc1 and its
 // last layer's backward-data): CO = 32, k4 s2 p1, 64-wide output rows, four
-// output rows per 256-pixel workgroup. MDT_THIN_MFMA=0 keeps the VALU body.
-__host__ inline int thin_conv_mfma_ok(const ConvDesc& d) {
-  static const bool on = [] {
+// output rows per 256-pixel workgroup (bit 1 of MDT_THIN_MFMA below).
+// MDT_THIN_MFMA: bit mask of the MFMA edge-layer forms in use: 1 thin conv
+// (enc1 forward, last layer backward-data), 2 transposed conv + BCE, 4 weight
+// gradients; 0 keeps every VALU / im2col body. Default 6: bits 2 and 4 leave
+// the model-level gradients bit-for-bit as close to the bf16-emulating f64
+// reference as the VALU kernels (profiles/r2_thin/ab_mask); bit 1 is 6.6 us
+// faster per 128x128 step but its MFMA accumulation flips more bf16
+// roundings of enc1's activations (worst gradient deviation 0.0158 -> 0.0201).
+__host__ inline int thin_mfma_mask() {
+  static const int m = [] {
     const char* e = getenv("MDT_THIN_MFMA");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : 6;
   }();
-  return on && d.C == 1 && d.CO == 32 && d.KH == 4 && d.KW == 4 && d.S == 2 && d.P == 1 && d.OW == 64 &&
+  return m;
+}
+
+__host__ inline bool thin_mfma_geom(const ConvDesc& d) {
+  return d.C == 1 && d.CO == 32 && d.KH == 4 && d.KW == 4 && d.S == 2 && d.P == 1 && d.OW == 64 &&
          d.W == 2 * d.OW && d.H == 2 * d.OH && d.OH % 4 == 0;
 }
+
+__host__ inline int thin_conv_mfma_ok(const ConvDesc& d) { return (thin_mfma_mask() & 1) && thin_mfma_geom(d); }
+
 
 // LDS: staged weights [TAPS][CO] + the colsum transpose (256 x (CO+1)).
 template <int CO, int K>
@@ -542,17 +556,20 @@ __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
 // pixel; they go through a wave-private LDS row pair so the BCE epilogue runs
 // one float4 of an output row per lane.
 constexpr int kTcMfmaPatch = 6 * 66 * 64;  // (R + 2) x (WS + 2) pixels x 64 B
-constexpr int thin_tconv_mfma_lds_bytes() { return kTcMfmaPatch + 16 * 32 * 4 + 4 * 256 * 4 + 16 * 4; }
+constexpr int kTcMfmaAux = 16 * 32 * 4 + 9 * 64 * 16;  // wl [16][32] f32 + A fragments [9][64 lanes] (obuf aliases)
+constexpr int thin_tconv_mfma_lds_bytes() { return kTcMfmaPatch + kTcMfmaAux + 16 * 4; }
 
 __device__ __forceinline__ void thin_tconv_mfma_body(const ThinTconvArgs& ta, uint8_t* lds, int bid) {
   constexpr int R = 4, WS = 64, PC = WS + 2, PB = 64, CO = 32;
+  static_assert(4 * 256 * 4 <= kTcMfmaAux, "obuf alias");
   const ConvDesc& d = ta.d;
   const int rbn = d.OH / R;
   const int n = bid / rbn, j0 = (bid - n * rbn) * R;
   uint8_t* patch = lds;
-  float* wl = reinterpret_cast<float*>(lds + kTcMfmaPatch);  // [16 taps][32 ch]
-  float* obuf = wl + 16 * CO;                                  // [4 waves][2][128]
-  float* scratch = obuf + 4 * 256;
+  float* wl = reinterpret_cast<float*>(lds + kTcMfmaPatch);                 // [16 taps][32 ch]
+  bf16x8* afr = reinterpret_cast<bf16x8*>(lds + kTcMfmaPatch + 16 * CO * 4);  // [9][64]
+  float* obuf = reinterpret_cast<float*>(lds + kTcMfmaPatch);               // [4 waves][2][128], after the A loads
+  float* scratch = reinterpret_cast<float*>(lds + kTcMfmaPatch + kTcMfmaAux);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const __bf16* Gn = ta.G + (size_t)n * d.OH * d.OW * CO;
   // this lane's epilogue pixels: output row 2 j + u, columns c4 .. c4 + 3;
@@ -590,27 +607,36 @@ __device__ __forceinline__ void thin_tconv_mfma_body(const ThinTconvArgs& ta, ui
     wl[tap * CO + c] = ta.Wf[e];
   }
   __syncthreads();
-  // A fragments: lane row m = lane & 15, channels 8 kq .. 8 kq + 7
-  const int m = lane & 15, kq = lane >> 4;
-  bf16x8 af[9];
-#pragma unroll
-  for (int nb = 0; nb < 9; ++nb) {
+  // A fragments, built ONCE per workgroup (each slot = one lane's 8 values of
+  // one neighbour step; per-lane builds cost ~1.1k VALU per wave and 8-way
+  // bank conflicts on the tap-strided weight reads): lane row m = lane & 15
+  // (class m & 3, term m >> 2: hi / lo / lo2 / zero), channels 8 kq .. + 7
+  for (int sl = tid; sl < 9 * 64; sl += 256) {
+    const int nb = sl >> 6, l = sl & 63, m = l & 15, kq = l >> 4;
     const int r = nb / 3, c = nb - 3 * (nb / 3);
-    const int cls = m & 3, ca = cls >> 1, cb = cls & 1;
+    const int ca = (m >> 1) & 1, cb = m & 1, term = m >> 2;
     const int ty = 2 - ca - r, tx = 2 - cb - c;
-    const bool ok = m < 12 && (unsigned)ty < 2u && (unsigned)tx < 2u;
+    const bool ok = term < 3 && (unsigned)ty < 2u && (unsigned)tx < 2u;
     const int tap = ok ? (ca + 2 * ty) * 4 + cb + 2 * tx : 0;
     const float4 w0 = *reinterpret_cast<const float4*>(wl + tap * CO + 8 * kq);
     const float4 w1 = *reinterpret_cast<const float4*>(wl + tap * CO + 8 * kq + 4);
     const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    bf16x8 a;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       __bf16 hi, lo;
       split_bf16(wv[e], hi, lo);
       const __bf16 lo2 = (__bf16)(wv[e] - (float)hi - (float)lo);
-      af[nb][e] = ok ? (m < 4 ? hi : (m < 8 ? lo : lo2)) : (__bf16)0.f;
+      a[e] = ok ? (term == 0 ? hi : (term == 1 ? lo : lo2)) : (__bf16)0.f;
     }
+    afr[sl] = a;
   }
+  __syncthreads();
+  const int kq = lane >> 4;
+  bf16x8 af[9];
+#pragma unroll
+  for (int nb = 0; nb < 9; ++nb) af[nb] = afr[nb * 64 + lane];
+  __syncthreads();  // obuf aliases wl / afr
   const float b0 = ta.bias ? ta.bias[0] : 0.f;
   float* ob = obuf + w * 256;
 #pragma unroll 1
@@ -625,9 +651,9 @@ __device__ __forceinline__ void thin_tconv_mfma_body(const ThinTconvArgs& ta, ui
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nb], bv, acc, 0, 0, 0);
     }
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {  // rows r + 4 r' (hi, lo, lo2): lanes l, l ^ 16, l ^ 32
-      acc[rr] += __shfl_xor(acc[rr], 16, 64);
-      acc[rr] += __shfl_xor(acc[rr], 32, 64);
+    for (int rr = 0; rr < 4; ++rr) {  // rows r + 4 r' (hi, lo, lo2) in lanes l, l + 16, l + 32: hi + (lo + lo2)
+      const float lo = __shfl(acc[rr], (lane & 15) + 16, 64), lo2 = __shfl(acc[rr], (lane & 15) + 32, 64);
+      acc[rr] += lo + lo2;
     }
     if (lane < 16) {  // class (ca, cb) -> output row 1 - ca, column 2 i + 1 - cb
 #pragma unroll
@@ -675,10 +701,13 @@ __device__ __forceinline__ void thin_tconv_mfma_body(const ThinTconvArgs& ta, ui
 // bias-gradient column sums). Workgroup = 4 output rows (256 pixels: the same
 // blocks, hence the same colsum rows, as the VALU body), wave w = row oy0 + w,
 // four 16-pixel tiles. D[32 co x 16 px] = A[co][k] B[k][px] with k = 16 taps
-// of x_hi then 16 taps of x_lo (x = x_hi + x_lo, two bf16; x_lo = 0 for bf16
-// input) and A = [W_hi | W_hi], [W_lo | W_lo], [W_lo2 | W_lo2] (three bf16
-// terms of the f32 weight): the f32 product to ~2^-17 of |x w| (the x split;
-// exact for bf16 input). A rows are ordered co = 8 (m >> 2) + 4 mt + (m & 3), so lane (q, px)
+// of x_hi then 16 taps of x_lo, plus [x_lo2 | 0] for f32 input (x = x_hi +
+// x_lo + x_lo2, three bf16; bf16 input is exact in x_hi) and A = [W_hi |
+// W_hi], [W_lo | W_lo], [W_lo2 | W_lo2] (three bf16 terms of the f32
+// weight): the f32 product to ~2^-24 of |x w| -- the same bf16 rounding
+// decisions downstream as an f32 kernel (a two-term x split flipped ~0.2 %
+// of the enc1 activations' bf16 roundings and doubled the model-level
+// gradient deviation from the bf16-emulating reference). A rows are ordered co = 8 (m >> 2) + 4 mt + (m & 3), so lane (q, px)
 // ends with channels 8q .. 8q + 7 of its pixel: one 16-B NHWC store.
 constexpr int kTcPitch = 132;  // patch row pitch (floats): column ix at ix + 1
 template <typename TIN>
@@ -692,15 +721,8 @@ __device__ void thin_conv_mfma_body(const ThinConvArgs& ta, uint8_t* lds, int bi
   const int n = bid / rbn, oy0 = (bid - n * rbn) * 4;
   const int* rows = ta.idx ? ta.idx + (size_t)ta.st->cursor * ta.B : nullptr;
   const TIN* img = X + (size_t)(rows ? rows[n] : n) * d.H * d.W;
-  if (ta.xb) {
-    const int p4 = (d.H * d.W) >> 2;
-    const long long tot = (long long)d.N * p4;
-    for (long long e = (long long)bid * blockDim.x + tid; e < tot; e += (long long)ta.nblk * blockDim.x) {
-      const int i = (int)(e / p4), c = (int)(e - (long long)i * p4);
-      reinterpret_cast<float4*>(ta.xb + (size_t)i * d.H * d.W)[c] =
-          reinterpret_cast<const float4*>(X + (size_t)(rows ? rows[i] : i) * d.H * d.W)[c];
-    }
-  }
+  // (the gathered rows xb -- BCE target, weight-gradient input -- are written
+  // from the patch below: this workgroup's own 8 input rows, no second read)
   if (ta.hp && bid == 0 && tid == 0) {
     TrainState* st = ta.st;
     st->step = st->step + 1;
@@ -726,6 +748,9 @@ __device__ void thin_conv_mfma_body(const ThinConvArgs& ta, uint8_t* lds, int bi
     const int e = tid + it * 256;
     const int y = e / WP, xx = e - y * WP;
     if (e < NFILL) patch[y * kTcPitch + xx] = fv[it];
+    // rows 2 oy0 .. 2 oy0 + 7 (patch rows 1..8) belong to this workgroup
+    if (ta.xb && e < NFILL && y >= 1 && y <= 8 && xx >= 1 && xx <= 128)
+      ta.xb[((size_t)n * d.H + 2 * oy0 - 1 + y) * 128 + xx - 1] = fv[it];
   }
   // A fragments (weights), lane row m = lane & 15, taps 8 (kq & 1) .. + 7
   const int m = lane & 15, kq = lane >> 4, q = kq;
@@ -765,7 +790,7 @@ __device__ void thin_conv_mfma_body(const ThinConvArgs& ta, uint8_t* lds, int bi
     const int ox = 16 * t + (lane & 15);
     const size_t pix = ((size_t)n * d.OH + oy) * d.OW + ox;
     const bf16x8 mk = mks[t];
-    bf16x8 b;
+    bf16x8 b, b2;  // b = [x_hi | x_lo] by k half; b2 = [x_lo2 | 0] (f32 input: x to ~2^-24)
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const float* pr = patch + (2 * w + 2 * (kq & 1) + r) * kTcPitch + 2 * ox;
@@ -776,14 +801,19 @@ __device__ void thin_conv_mfma_body(const ThinConvArgs& ta, uint8_t* lds, int bi
         __bf16 hi, lo;
         split_bf16(xv[kx], hi, lo);
         b[4 * r + kx] = kq < 2 ? hi : lo;
+        b2[4 * r + kx] = kq < 2 ? (__bf16)(xv[kx] - (float)hi - (float)lo) : (__bf16)0.f;
       }
     }
     f32x4 acc[2];
+    // smallest terms first, the hi x hi products last: the small partial sum
+    // enters the final MFMA as its accumulator instead of being added to an
+    // already large one
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[mt], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo2[mt], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[mt], b, acc[mt], 0, 0, 0);
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo2[mt], b, acc[mt], 0, 0, 0);
+      if constexpr (sizeof(TIN) == 4) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[mt], b2, acc[mt], 0, 0, 0);
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[mt], b, acc[mt], 0, 0, 0);
     }
     float v[8];
 #pragma unroll

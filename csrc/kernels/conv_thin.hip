@@ -112,14 +112,8 @@ static bool tconv_patch_ok(const ConvDesc& d) {
 }
 
 // MFMA form of the patch kernel (thin_tconv_mfma_body, same grid and
-// partials); MDT_THIN_MFMA=0 keeps the VALU patch kernel.
-static bool thin_mfma_on() {
-  static const bool on = [] {
-    const char* e = getenv("MDT_THIN_MFMA");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// partials): bit 2 of MDT_THIN_MFMA (conv_thin.h thin_mfma_mask).
+static bool thin_mfma_on() { return (thin_mfma_mask() & 2) != 0; }
 
 int mdt_thin_blocks(int tconv, ConvDesc d) {
   if (!tconv) return cdiv_t((long long)d.N * d.OH * d.OW, 256);

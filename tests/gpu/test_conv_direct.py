@@ -149,3 +149,38 @@ def test_direct_wgrad_matches_torch(geom, native_ext, monkeypatch):
         ref = ref.permute(0, 2, 3, 1).reshape(-1).double()
         err = float((got - ref).abs().max() / ref.abs().max())
         assert err < 1e-5, (N, err)
+
+
+@pytest.mark.parametrize("f32_x", [True, False], ids=["f32_input", "bf16_dlogits"])
+def test_thin_wgrad_mfma_matches_torch(f32_x, native_ext):
+    """MFMA weight gradient of the single-channel 128x128 edge layers
+    (conv_thin_wg.h): enc1 (X = f32 images) and the last layer's conv view
+    (X = bf16 dlogits). One [32][16] partial row per 4 output rows; their sum
+    equals conv2d_weight in f64 to the f32 accumulation (bf16 X exact; f32 X
+    in three bf16 terms)."""
+    C_ = native_ext
+    dev = torch.device("cuda")
+    N, H, OH, CO = 3, 128, 64, 32
+    d = [N, H, H, 1, OH, OH, CO, 4, 4, 2, 1]
+    info = C_.wgrad_plan(d)
+    assert info[0] == 110 and info[6] == N * OH // 4, info
+    g = torch.Generator(device="cpu").manual_seed(11)
+    X = torch.rand(N, 1, H, H, generator=g)
+    if not f32_x:
+        X = X - 0.5
+        X = X.bfloat16().float()
+    G = torch.randn(N, CO, OH, OH, generator=g).bfloat16().float()
+    Xd = (X.flatten(1).contiguous() if f32_x else X.flatten(1).bfloat16().contiguous()).to(dev)
+    G16 = G.permute(0, 2, 3, 1).contiguous().bfloat16().to(dev)
+    ns = info[6]
+    out = torch.full((ns * CO * 16,), float("nan"), device=dev)
+    C_.wgrad(G16, Xd, d, out)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    ref = torch.nn.grad.conv2d_weight(X.double(), (CO, 1, 4, 4), G.double(), stride=2, padding=1).reshape(-1)
+    mag = torch.nn.grad.conv2d_weight(X.double().abs(), (CO, 1, 4, 4), G.double().abs(), stride=2,
+                                      padding=1).reshape(-1)
+    tot = out.view(ns, CO * 16).double().sum(0).cpu()
+    err = (tot - ref).abs()
+    bound = mag * 2.0 ** -20
+    assert bool((err <= bound + 1e-6).all()), float((err / (mag + 1e-9)).max())

@@ -181,6 +181,8 @@ def test_grad_finalize_is_deterministic_and_fuses_adam(native_ext):
 @pytest.mark.parametrize("H", [28, 128])
 @pytest.mark.parametrize("f32_in", [True, False])
 def test_thin_conv_matches_conv2d(f32_in, H, native_ext):
+    # H = 128 exercises the MFMA form only with bit 1 of MDT_THIN_MFMA set
+    # (opt-in); otherwise the VALU body at both sizes
     """Single-input-channel conv (encoder conv 1 / last layer backward-data).
     H = 28 runs the VALU body, H = 128 the MFMA form (thin_conv_mfma_body:
     split hi/lo bf16 weights and inputs); the f32 column sums pin both to the
@@ -212,10 +214,10 @@ def test_thin_conv_matches_conv2d(f32_in, H, native_ext):
     assert _rel(y16.float().view(M, CO), ref.float()) < 1e-2
     # per element: within one bf16 rounding of the f64 result
     # per element: one bf16 rounding of the output plus the MFMA form's split
-    # error (x = x_hi + x_lo: <= 2^-17 of sum |x||w| per output)
+    # error (x and w in three bf16 terms: ~2^-24 of sum |x||w| per output)
     mag = nhwc(F.conv2d(nchw(x.float()).abs().double(), torch_weight(w).abs().double(), None, 2, 1)).reshape(M, CO)
     err = (y16.double().view(M, CO) - ref).abs()
-    bad = err > ref.abs() * 2.0 ** -8 + mag * 2.0 ** -16 + 1e-7
+    bad = err > ref.abs() * 2.0 ** -8 + mag * 2.0 ** -20 + 1e-7
     if bool(bad.any()):
         i = int((err / (ref.abs() + 1e-6)).argmax())
         print(f"thin_conv H={H} f32_in={f32_in}: {int(bad.sum())}/{bad.numel()} beyond one bf16 rounding; worst "
