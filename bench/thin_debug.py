@@ -33,6 +33,9 @@ def main():
         torch.cuda.synchronize()
         ref = nhwc(F.conv2d(nchw(x.float()).double(), torch_weight(w).double(), b.double(), 2, 1)).reshape(M, CO)
         y = y16.double().view(M, CO)
+        flips = int((y16.view(M, CO) != ref.float().bfloat16()).sum())
+        print(f"f32_in={f32_in}: bf16 outputs != bf16(f64 result): {flips}/{y.numel()} "
+              f"(MDT_THIN_MFMA={os.environ.get('MDT_THIN_MFMA', 'default')})")
         err = (y - ref).abs()
         bad = err > ref.abs() * 2.0 ** -8 + 1e-6
         print(f"f32_in={f32_in}: bad {int(bad.sum())}/{bad.numel()}, max err {float(err.max()):.3e}, "
