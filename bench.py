@@ -98,6 +98,15 @@ def main(argv=None):
 
     from multidisttorch_amd.runtime.bootstrap import _stdout_to_stderr
 
+    # One trial per rank (the headline K = N layout): the trial groups never
+    # communicate, so the device-bound world with one eager ncclCommSplit per
+    # group (the HPO runner's default, runtime/bootstrap.py) buys nothing here;
+    # the bench keeps the plain lazy RCCL world, whose single communicator the
+    # first timing barrier opens outside the timed region. An explicit
+    # MDT_EAGER_COMM still wins.
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if (a.ngroups is None or a.ngroups >= world_env) and "MDT_EAGER_COMM" not in os.environ:
+        os.environ["MDT_EAGER_COMM"] = "0"
     with _stdout_to_stderr():  # keep stdout for the single JSON line (gloo prints connect banners)
         world, rank = setup_ddp(verbose=False)
         K = a.ngroups or world
