@@ -469,7 +469,7 @@ int mdt_job_thin_conv(JobBlob* j, const void* X, int x_is_f32, const float* Wf, 
   j->nblk = cdivj((long long)d.N * d.OH * d.OW, 256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
                         colsum, idx, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), B, xb,
-                        j->nblk, thin_conv_mfma_ok(d)};
+                        j->nblk, thin_conv_mfma_ok(d, x_is_f32)};
   put_args(j, ta);
   return 0;
 }

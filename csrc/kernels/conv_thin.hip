@@ -68,7 +68,7 @@ int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, cons
   dim3 grid(cdiv_t(M, 256)), blk(256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
                         colsum, idx, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), B, xb,
-                        (int)grid.x, thin_conv_mfma_ok(d)};
+                        (int)grid.x, thin_conv_mfma_ok(d, x_is_f32)};
 #define THIN(CO_)                                                                     \
   {                                                                                   \
     if (x_is_f32)                                                                     \
