@@ -577,8 +577,11 @@ __device__ __forceinline__ void thin_tconv_mfma_body(const ThinTconvArgs& ta, ui
   float* scratch = reinterpret_cast<float*>(lds + kTcMfmaPatch + kTcMfmaAux);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const __bf16* Gn = ta.G + (size_t)n * d.OH * d.OW * CO;
+  // weights first: waiting for them (vmcnt counts in issue order) must not
+  // wait for the patch loads issued after them
+  const float wf0 = ta.Wf[tid], wf1 = ta.Wf[tid + 256];
   // this lane's epilogue pixels: output row 2 j + u, columns c4 .. c4 + 3;
-  // the BCE target is loaded first so its latency overlaps everything below
+  // the BCE target is loaded early so its latency overlaps everything below
   const int u = lane >> 5, c4 = (lane & 31) * 4;
   const size_t e_out = ((size_t)n * d.H + 2 * (j0 + w) + u) * d.W + c4;
   float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -600,18 +603,13 @@ __device__ __forceinline__ void thin_tconv_mfma_body(const ThinTconvArgs& ta, ui
       for (int k = 0; k < 8; ++k) fv[it][k] = (__bf16)0.f;
     }
   }
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int e = tid + it * 256;
-    const int pix = e >> 2, q = e & 3;
-    const int y = pix / PC, x = pix - y * PC;
-    if (e < NFILL) *reinterpret_cast<bf16x8*>(patch + pix * PB + 16 * (q ^ ((x >> 2) & 3))) = fv[it];
-  }
-  for (int e = tid; e < 16 * CO; e += 256) {  // Wf [ch][ky][kx] -> wl[tap][ch]
-    const int c = e >> 4, tap = e & 15;
-    wl[tap * CO + c] = ta.Wf[e];
-  }
-  __syncthreads();
+  // Wf [ch][ky][kx] -> wl[tap][ch]; the A fragments are built while the
+  // patch loads are still in flight (LDS-only barriers: __syncthreads()
+  // would also wait for them)
+  wl[(tid & 15) * CO + (tid >> 4)] = wf0;
+  wl[((tid + 256) & 15) * CO + ((tid + 256) >> 4)] = wf1;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   // A fragments, built ONCE per workgroup (each slot = one lane's 8 values of
   // one neighbour step; per-lane builds cost ~1.1k VALU per wave and 8-way
   // bank conflicts on the tap-strided weight reads): lane row m = lane & 15
@@ -636,12 +634,20 @@ __device__ __forceinline__ void thin_tconv_mfma_body(const ThinTconvArgs& ta, ui
     }
     afr[sl] = a;
   }
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   const int kq = lane >> 4;
   bf16x8 af[9];
 #pragma unroll
   for (int nb = 0; nb < 9; ++nb) af[nb] = afr[nb * 64 + lane];
-  __syncthreads();  // obuf aliases wl / afr
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + it * 256;
+    const int pix = e >> 2, q = e & 3;
+    const int y = pix / PC, x = pix - y * PC;
+    if (e < NFILL) *reinterpret_cast<bf16x8*>(patch + pix * PB + 16 * (q ^ ((x >> 2) & 3))) = fv[it];
+  }
+  __syncthreads();  // patch complete; obuf aliases wl / afr (every wave has read its fragments)
   const float b0 = ta.bias ? ta.bias[0] : 0.f;
   float* ob = obuf + w * 256;
 #pragma unroll 1
