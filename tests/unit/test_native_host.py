@@ -44,3 +44,25 @@ def test_conv_planners_consistent(image, M):
         assert all(v >= 0 for v in w)
     for ks in (1, 2, 8):
         assert C.combine_reparam_blocks(ks, M, 32) >= 1
+
+
+@pytest.mark.parametrize("M", [1, 7, 64, 128])
+def test_thin_mfma_wgrad_plan(M):
+    """The single-channel 128x128 layers (enc1, and the last layer in its conv
+    view) plan the MFMA weight gradient (conv_thin_wg.h, cfg 110): one partial
+    row per 4 output rows, i.e. M * 64 / 4 slabs of [32][16]; the 28x28 edge
+    layers keep the generic thin weight gradient."""
+    import os
+
+    C = native.require()
+    if os.environ.get("MDT_THIN_MFMA", "14") != "14":
+        pytest.skip("non-default MDT_THIN_MFMA mask")
+    for image in (28, 128):
+        for l, d in _descs(image, M):
+            if not (l.cin == 1 or l.cout == 1):
+                continue
+            info = C.wgrad_plan(d)
+            if image == 128:
+                assert info[0] == 110 and info[6] == M * 64 // 4 and info[1] == 32 and info[2] == 16, info
+            else:
+                assert info[0] != 110, info
