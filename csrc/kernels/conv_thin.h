@@ -49,7 +49,7 @@ struct ThinConvArgs {
   int B;
   float* xb;
   int nblk;
-  int mfma;            // 1: thin_conv_mfma_body (host: thin_conv_mfma_ok)
+  int mfma;            // 1: thin_conv_mfma_body (host: thin_conv_mfma_ok), 2: VALU with SGPR weights
 };
 
 // Geometry of the MFMA form of thin_conv (the 128x128 model's enc1 and its
@@ -57,8 +57,11 @@ struct ThinConvArgs {
 // output rows per 256-pixel workgroup (bit 1 of MDT_THIN_MFMA below).
 // MDT_THIN_MFMA: bit mask of the MFMA edge-layer forms in use: 1 thin conv
 // with f32 input (enc1 forward), 8 thin conv with bf16 input (last layer's
-// backward-data), 2 transposed conv + BCE, 4 weight gradients; 0 keeps every
-// VALU / im2col body. Default 14 (bits 2, 4, 8): they leave the model-level
+// backward-data), 2 transposed conv + BCE, 4 weight gradients, 16 VALU thin
+// conv with SGPR weights (any geometry, bitwise equal to the LDS form, but
+// measured slower: enc1 16.7 vs 15.2 us, conv28 layer path 0.1167 vs 0.1137
+// ms -- opt-in); 0 keeps every VALU / im2col body with LDS weights. Default
+// 14; bits 2, 4, 8: they leave the model-level
 // gradients exactly as close to the bf16-emulating f64 reference as the VALU
 // kernels (profiles/r2_thin/ab_mask); bit 1 is ~6 us faster per 128x128 step
 // and matches the f64 conv as closely as the VALU body on random inputs (same
@@ -77,9 +80,13 @@ __host__ inline bool thin_mfma_geom(const ConvDesc& d) {
          d.W == 2 * d.OW && d.H == 2 * d.OH && d.OH % 4 == 0;
 }
 
-// bit 1: f32 input (enc1 forward), bit 8: bf16 input (last layer's backward-data)
+// bit 1: f32 input (enc1 forward), bit 8: bf16 input (last layer's backward-data).
+// Returns the body selector of ThinConvArgs::mfma: 1 = MFMA form, 2 = VALU
+// body with the weights as SGPR operands (bit 16, default on), 0 = VALU body
+// with LDS-broadcast weights.
 __host__ inline int thin_conv_mfma_ok(const ConvDesc& d, int x_is_f32) {
-  return (thin_mfma_mask() & (x_is_f32 ? 1 : 8)) && thin_mfma_geom(d);
+  if ((thin_mfma_mask() & (x_is_f32 ? 1 : 8)) && thin_mfma_geom(d)) return 1;
+  return (thin_mfma_mask() & 16) ? 2 : 0;
 }
 
 
@@ -93,7 +100,7 @@ __device__ void thin_conv_mfma_body(const ThinConvArgs& ta, uint8_t* lds, int bi
 template <int CO, int K, typename TIN>
 __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* lds, int bid) {
   if constexpr (CO == 32 && K == 4) {
-    if (ta.mfma) {
+    if (ta.mfma == 1) {
       thin_conv_mfma_body<TIN>(ta, lds, bid);
       return;
     }
@@ -138,26 +145,40 @@ __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* 
     const float x = ld1(img + (ok ? iy * d.W + ix : 0));
     xin[t] = ok ? x : 0.f;
   }
-  // weights staged once per block in LDS as [tap][co]; the FMA loop reads
-  // them with wave-uniform (broadcast) ds_read_b128, 4 channels per read
-  for (int e = threadIdx.x; e < TAPS * CO; e += blockDim.x) {
-    const int c = e / TAPS, t = e - c * TAPS;
-    wl[t * CO + c] = Wf[e];
-  }
-  __syncthreads();
   float acc[CO];
 #pragma unroll
   for (int c = 0; c < CO; ++c) acc[c] = bias ? bias[c] : 0.f;
+  if (ta.mfma == 2) {
+    // weights as SGPR operands: the [co][16 taps] f32 rows are wave-uniform
+    // and read-only here, so they are read through the constant address
+    // space (s_load_dwordx16, one co row per load) instead of the LDS
+    // broadcasts below (an LDS instruction costs the same for one address as
+    // for 64). Same per-channel FMA chain over t = 0..15: bitwise identical.
+    typedef const __attribute__((address_space(4))) float cfloat;
+    const cfloat* Wk = (const cfloat*)Wf;
 #pragma unroll
-  for (int t = 0; t < TAPS; ++t) {
-    const float x = xin[t];
+    for (int c = 0; c < CO; ++c)
 #pragma unroll
-    for (int c4 = 0; c4 < CO / 4; ++c4) {
-      const float4 w = *reinterpret_cast<const float4*>(wl + t * CO + 4 * c4);
-      acc[4 * c4 + 0] = fmaf(x, w.x, acc[4 * c4 + 0]);
-      acc[4 * c4 + 1] = fmaf(x, w.y, acc[4 * c4 + 1]);
-      acc[4 * c4 + 2] = fmaf(x, w.z, acc[4 * c4 + 2]);
-      acc[4 * c4 + 3] = fmaf(x, w.w, acc[4 * c4 + 3]);
+      for (int t = 0; t < TAPS; ++t) acc[c] = fmaf(xin[t], Wk[c * TAPS + t], acc[c]);
+  } else {
+    // weights staged once per block in LDS as [tap][co]; the FMA loop reads
+    // them with wave-uniform (broadcast) ds_read_b128, 4 channels per read
+    for (int e = threadIdx.x; e < TAPS * CO; e += blockDim.x) {
+      const int c = e / TAPS, t = e - c * TAPS;
+      wl[t * CO + c] = Wf[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TAPS; ++t) {
+      const float x = xin[t];
+#pragma unroll
+      for (int c4 = 0; c4 < CO / 4; ++c4) {
+        const float4 w = *reinterpret_cast<const float4*>(wl + t * CO + 4 * c4);
+        acc[4 * c4 + 0] = fmaf(x, w.x, acc[4 * c4 + 0]);
+        acc[4 * c4 + 1] = fmaf(x, w.y, acc[4 * c4 + 1]);
+        acc[4 * c4 + 2] = fmaf(x, w.z, acc[4 * c4 + 2]);
+        acc[4 * c4 + 3] = fmaf(x, w.w, acc[4 * c4 + 3]);
+      }
     }
   }
   if (ta.relu) {
