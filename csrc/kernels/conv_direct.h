@@ -393,5 +393,10 @@ using DcS1b = DcCfg<0, 32, 64, 64, 64, 4, 2, 4, 0, 2, 3>;
 using DcS2b = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7>;
 using DcT2b = DcCfg<1, 128, 16, 64, 32, 4, 1, 3, 0, 0, 15>;
 using DcT3b = DcCfg<1, 64, 32, 32, 32, 4, 1, 3, 0, 1, 7>;
+// three-workgroups-per-CU variants (R = 2, shallower weight rings; MDT_DCONV_ALT=8,
+// the 32x32x64 -> 16x16x128 conv keeps its R = 4 tile)
+using DcS1c = DcCfg<0, 32, 64, 64, 64, 2, 2, 3, 0, 2, 3>;
+using DcT2c = DcCfg<1, 128, 16, 64, 32, 2, 1, 2, 0, 0, 15>;
+using DcT3c = DcCfg<1, 64, 32, 32, 32, 2, 1, 2, 0, 1, 7>;
 
 }  // namespace mdt

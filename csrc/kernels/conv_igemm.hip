@@ -58,7 +58,9 @@ template <class CF>
 constexpr DcInfo dc_info() { return DcInfo{CF::RB, CF::NBB, CF::MT, CF::NB}; }
 static const DcInfo kDcInfo[] = {dc_info<DcS1>(),  dc_info<DcS2>(),  dc_info<DcT2>(),  dc_info<DcT3>(),
                                   dc_info<DcS1b>(), dc_info<DcS2b>(), dc_info<DcT2b>(), dc_info<DcT3b>(),
-                                  dc_info<DcS3>(),  dc_info<DcT1>()};
+                                  dc_info<DcS3>(),  dc_info<DcT1>(),
+                                  dc_info<DcS1c>(), dc_info<DcS2b>() /* 11: unused */, dc_info<DcT2c>(),
+                                  dc_info<DcT3c>()};
 
 // the 16x16 <-> 8x8 geometries (MDT_DCONV_SMALL=0 keeps them on im2col)
 static bool direct_small() {
@@ -79,7 +81,7 @@ int direct_cfg(int mode, const ConvDesc& d, bool fwd) {
   // MDT_DCONV_ALT=0 selects the latter
   static const int alt = [] {
     const char* e = getenv("MDT_DCONV_ALT");
-    return e && e[0] == '0' ? 0 : 4;
+    return e && e[0] == '0' ? 0 : (e && e[0] == '8' ? 8 : 4);
   }();
   // MDT_DCONV_BWD=0: forward calls only (backward-data keeps the fusable im2col kernel)
   static const bool bwd = [] {
@@ -90,14 +92,14 @@ int direct_cfg(int mode, const ConvDesc& d, bool fwd) {
   if (!fwd && !bwd) return -1;
   if (d.H != d.W || d.OH != d.OW || d.H != 2 * d.OH) return -1;
   if (mode == kModeConv) {  // A = input (H, C), columns = CO
-    if (d.C == 32 && d.H == 64 && d.CO == 64) return 0 + alt;
-    if (d.C == 64 && d.H == 32 && d.CO == 128) return 1 + alt;
+    if (d.C == 32 && d.H == 64 && d.CO == 64) return alt == 8 ? 10 : 0 + alt;
+    if (d.C == 64 && d.H == 32 && d.CO == 128) return alt == 8 ? 5 : 1 + alt;
     // 16x16 -> 8x8: forward only; as a backward-data GEMM the im2col kernel
     // fuses with the weight gradient in one launch, which measured faster
     if (d.C == 128 && d.H == 16 && d.CO == 256 && fwd && direct_small()) return 8;
   } else {  // A = conv output (OH, CO), columns = C
-    if (d.CO == 128 && d.OH == 16 && d.C == 64) return 2 + alt;
-    if (d.CO == 64 && d.OH == 32 && d.C == 32) return 3 + alt;
+    if (d.CO == 128 && d.OH == 16 && d.C == 64) return alt == 8 ? 12 : 2 + alt;
+    if (d.CO == 64 && d.OH == 32 && d.C == 32) return alt == 8 ? 13 : 3 + alt;
     if (d.CO == 256 && d.OH == 8 && d.C == 128 && fwd && direct_small()) return 9;
   }
   return -1;
@@ -402,6 +404,9 @@ int launch_direct(int cfg, const void* A, const void* B16, const ConvDesc& d, co
     case 7: launch_dc<DcT3b>(a, s); break;
     case 8: launch_dc<DcS3>(a, s); break;
     case 9: launch_dc<DcT1>(a, s); break;
+    case 10: launch_dc<DcS1c>(a, s); break;
+    case 12: launch_dc<DcT2c>(a, s); break;
+    case 13: launch_dc<DcT3c>(a, s); break;
     default: return 2;
   }
   return (int)hipGetLastError();
