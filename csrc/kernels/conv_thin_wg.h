@@ -43,7 +43,7 @@ __device__ __forceinline__ void thin_wgrad_mfma_body(const WgArgs& a, uint8_t* l
   const int n = bid / rbn, oy = (bid - n * rbn) * 4 + w;
   uint8_t* img = lds + w * kTwWave;
   float* xs = reinterpret_cast<float*>(img + kTwImg);  // [ky][arr][68]: arr 0 = O'[px], 1 = E[px], 2 = O'[px+1], 3 = E[px+1]
-  const XT* X = reinterpret_cast<const XT*>(a.X) + (size_t)n * 128 * 128;
+  const XT* X = reinterpret_cast<const XT*>(a.X) + (size_t)n * d.H * 128;  // W = 128 (thin_mfma_geom)
   // ---- loads (all issued before the first LDS store): the G row (lane =
   // pixel, 64 B) and the four input rows (lane = column pair 2l, 2l + 1)
   const __bf16* Grow = a.G + (((size_t)n * d.OH + oy) * 64 + lane) * 32;
@@ -54,7 +54,7 @@ __device__ __forceinline__ void thin_wgrad_mfma_body(const WgArgs& a, uint8_t* l
 #pragma unroll
   for (int ky = 0; ky < 4; ++ky) {
     const int iy = 2 * oy - 1 + ky;
-    const bool ok = (unsigned)iy < 128u;
+    const bool ok = (unsigned)iy < (unsigned)d.H;
     const XT* p = X + (ok ? iy : 0) * 128 + 2 * lane;
     const float e = (float)p[0], o = (float)p[1];
     xe[ky] = ok ? e : 0.f;
