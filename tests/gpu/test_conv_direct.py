@@ -138,7 +138,7 @@ def test_direct_wgrad_matches_torch(geom, native_ext, monkeypatch):
         assert info[0] >= 100 and info[6] == N, info
         g = torch.Generator(device="cpu").manual_seed(3 + N + H)
         X = torch.randn(N, C, H, H, generator=g).bfloat16().float().to(dev)
-        G = torch.randn(N, CO, OH, OH, generator=g).bfloat16().float().to(dev)
+        G = torch.randn(N, CO, OH, OW, generator=g).bfloat16().float().to(dev)
         out = torch.full((N * CO * 16 * C,), float("nan"), device=dev)
         C_.wgrad(G.permute(0, 2, 3, 1).contiguous().bfloat16(), X.permute(0, 2, 3, 1).contiguous().bfloat16(), d,
                  out)
@@ -151,8 +151,9 @@ def test_direct_wgrad_matches_torch(geom, native_ext, monkeypatch):
         assert err < 1e-5, (N, err)
 
 
+@pytest.mark.parametrize("H", [128, 64], ids=["square", "h64"])
 @pytest.mark.parametrize("f32_x", [True, False], ids=["f32_input", "bf16_dlogits"])
-def test_thin_wgrad_mfma_matches_torch(f32_x, native_ext):
+def test_thin_wgrad_mfma_matches_torch(f32_x, H, native_ext):
     """MFMA weight gradient of the single-channel 128x128 edge layers
     (conv_thin_wg.h): enc1 (X = f32 images) and the last layer's conv view
     (X = bf16 dlogits). One [32][16] partial row per 4 output rows; their sum
@@ -160,16 +161,17 @@ def test_thin_wgrad_mfma_matches_torch(f32_x, native_ext):
     in three bf16 terms)."""
     C_ = native_ext
     dev = torch.device("cuda")
-    N, H, OH, CO = 3, 128, 64, 32
-    d = [N, H, H, 1, OH, OH, CO, 4, 4, 2, 1]
+    N, W, CO = 3, 128, 32
+    OH, OW = H // 2, W // 2
+    d = [N, H, W, 1, OH, OW, CO, 4, 4, 2, 1]
     info = C_.wgrad_plan(d)
     assert info[0] == 110 and info[6] == N * OH // 4, info
     g = torch.Generator(device="cpu").manual_seed(11)
-    X = torch.rand(N, 1, H, H, generator=g)
+    X = torch.rand(N, 1, H, W, generator=g)
     if not f32_x:
         X = X - 0.5
         X = X.bfloat16().float()
-    G = torch.randn(N, CO, OH, OH, generator=g).bfloat16().float()
+    G = torch.randn(N, CO, OH, OW, generator=g).bfloat16().float()
     Xd = (X.flatten(1).contiguous() if f32_x else X.flatten(1).bfloat16().contiguous()).to(dev)
     G16 = G.permute(0, 2, 3, 1).contiguous().bfloat16().to(dev)
     ns = info[6]
