@@ -138,7 +138,7 @@ def test_direct_wgrad_matches_torch(geom, native_ext, monkeypatch):
         assert info[0] >= 100 and info[6] == N, info
         g = torch.Generator(device="cpu").manual_seed(3 + N + H)
         X = torch.randn(N, C, H, H, generator=g).bfloat16().float().to(dev)
-        G = torch.randn(N, CO, OH, OW, generator=g).bfloat16().float().to(dev)
+        G = torch.randn(N, CO, OH, OH, generator=g).bfloat16().float().to(dev)
         out = torch.full((N * CO * 16 * C,), float("nan"), device=dev)
         C_.wgrad(G.permute(0, 2, 3, 1).contiguous().bfloat16(), X.permute(0, 2, 3, 1).contiguous().bfloat16(), d,
                  out)
