@@ -1,0 +1,749 @@
+// Two workgroups per sample for the fused 28x28 conv-VAE step (gfx950).
+//
+// Why: the solo step (conv28_fused.h) runs one 512-thread workgroup per
+// sample, so a B = 128 trial -- the headline config -- keeps 128 of the 256
+// CUs busy, and its per-sample Linear GEMVs re-stream 600 KB of weights per
+// CU per direction. Here a launch of 2M workgroups gives every sample a PAIR
+// (blocks n and n + M: with M % 8 == 0 round-robin dispatch puts both on one
+// XCD, which buys L2 sharing of the weight slices -- speed only, never
+// correctness). Each half does half of every heavy phase:
+//
+//   7x7 maps (enc2 out, dec_fc out, their gradients): split by PIXEL --
+//     role 0 owns pixels 0..23, role 1 pixels 24..48, i.e. the contiguous
+//     ranges [0, 1536) / [1536, 3136) of the flattened 3136-vectors, so the
+//     Linear weight streams (head rows, dec_fc rows) are contiguous slices;
+//   14x14 maps (dec1 out, enc1 grad): split by CHANNEL -- 16 of 32 each;
+//   enc1, reparam, BCE/dlogits (cheap, and needed whole): both, redundantly
+//     and bitwise identically (fixed (role 0 + role 1) summation order).
+//
+// Six hand-offs per step, each a data-tagged 8-byte granule sweep
+// (MI355X_MICROARCH.md "handoff-1to1"; cdna_hip_programming.md Guideline 16
+// R2: {tag, payload} in ONE agent-scope store, so the data is its own flag and
+// no release/acquire fence is needed):
+//   X1 head partial sums (64 f32, K split)    X4 gd1 channel half (3 KB bf16)
+//   X2 d0 pixel half (~3 KB bf16)             X5 dz partial sums (32 f32)
+//   X3 dec2 partial logits (784 f32)          X6 ga2 pixel half (~3 KB bf16)
+// The consumer clears every granule it read, so the slabs are all-zero
+// between launches (graph replays need no memset node); tags also carry the
+// step so a stale granule can never match.
+//
+// Pairing never assumes co-residency. Each workgroup takes a ticket on its
+// sample's word at entry; the first arriver (leader) claims the sample SOLO
+// with a CAS after P0 unless the partner has already taken the second ticket.
+// A solo leader runs the one-workgroup body; a partner that arrives after the
+// claim exits. So a launch that cannot hold all 2M workgroups at once (trial
+// packing, a busy device) degrades to the solo step instead of deadlocking.
+// Every sweep is bounded (s_memrealtime) and reports a timeout in `err`.
+//
+// Bias-gradient partials: per-channel sums over the 7x7 pixels (enc2 bias)
+// come out per half, so db2_part is [2][M][64] and the finalize sums 2M rows;
+// everything else each half writes into its own part of the solo layout.
+#pragma once
+#include "conv28_fused.h"
+
+namespace mdt {
+namespace f28 {
+
+struct PairCtl {
+  unsigned long long* xg;  // [M][2][kXW] exchange granules (all zero between launches)
+  int* pairw;              // [M] pairing words (0 between launches)
+  unsigned* err;           // [1] bit 0: an exchange sweep timed out
+  int M;
+  int pair;                // 1: grid = 2M (pairs), 0: grid = M (solo)
+  int delay_us;            // tests: workgroups >= M wait this long before their ticket (forces solo)
+};
+
+// granule offsets inside one (sample, role) slab
+constexpr int kX1 = 0, kX2 = 72, kX3 = kX2 + 800, kX4 = kX3 + 784, kX5 = kX4 + 1568, kX6 = kX5 + 32;
+constexpr int kXW = kX6 + 800;
+#ifdef MDT_F28_NOSTORE  // timing experiment only: no global stores of the backward's inputs
+constexpr bool kGS = false;
+#else
+constexpr bool kGS = true;
+#endif
+constexpr unsigned long long kSpinTicks = 25000000ull;  // 0.25 s of s_memrealtime (100 MHz)
+
+enum : int { kModeSolo = 0, kModeRole0 = 1, kModeRole1 = 2, kModeExit = 3 };
+
+using g64 = __attribute__((address_space(1))) unsigned long long;
+using g32i = __attribute__((address_space(1))) int;
+
+// `near`: both workgroups of the pair run on ONE XCD (their HW_REG_XCC_ID
+// match, exchanged in X1), so they share one L2: the granule goes out as an
+// sc0 store that stays in that L2 instead of an sc1 write-through to memory,
+// and the partner's sc1 (L1-bypassing) polls hit it there. Read from the
+// hardware at run time, not assumed from dispatch order: with different XCDs
+// every store stays agent scope.
+__device__ __forceinline__ void xput(unsigned long long* g, uint32_t tag, uint32_t v, bool near) {
+  const unsigned long long x = ((unsigned long long)tag << 32) | v;
+  if (near)
+    __hip_atomic_store((g64*)g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    __hip_atomic_store((g64*)g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Each lane waits for its N granules gi[k] (< 0: none) of slab `base` to
+// carry `tag`, returns their payloads in v and clears them. Wave-uniform loop.
+template <int N>
+__device__ __forceinline__ void xget(unsigned long long* base, const int (&gi)[N], uint32_t tag, uint32_t (&v)[N],
+                                     unsigned* err, bool near) {
+  uint32_t pend = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    v[k] = 0;
+    if (gi[k] >= 0) pend |= 1u << k;
+  }
+#ifdef MDT_F28_XNOWAIT  // timing experiment only: no hand-off wait (wrong numerics)
+  pend = 0;
+#endif
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned spin = 0;; ++spin) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (pend & (1u << k)) {
+        const unsigned long long x = __hip_atomic_load((g64*)(base + gi[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(x >> 32) == tag) {
+          v[k] = (uint32_t)x;
+          pend &= ~(1u << k);
+        }
+      }
+    }
+    if (!__any(pend != 0)) break;
+    if ((spin & 15) == 15 && __builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+      if (pend) atomicOr(err, 1u);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    if (gi[k] >= 0) {
+      if (near)
+        __hip_atomic_store((g64*)(base + gi[k]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else
+        __hip_atomic_store((g64*)(base + gi[k]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
+__device__ __forceinline__ uint32_t bf16bits(__bf16 h) { return (uint32_t)__builtin_bit_cast(uint16_t, h); }
+
+// conv14to7 restricted to output pixels [p0, p1) (<= 32 of them): 2 m-tiles
+// x 4 n-tiles, one item per wave.
+template <class BFrag, class Pre, class Epi>
+__device__ __forceinline__ void conv14to7_rows(const uint8_t* in_img, int p0, int p1, BFrag bfrag, Pre pre, Epi epi) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = w & 3, mt = w >> 2;
+  float pv[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int p = p0 + mt * 16 + 4 * (lane >> 4) + rr;
+    pv[rr] = p < p1 ? pre(p, 16 * j + (lane & 15)) : 0.f;
+  }
+  const int r = p0 + mt * 16 + (lane & 15);
+  const int oy = r / 7, ox = r - 7 * (r / 7);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
+    const bool ok = r < p1 && (unsigned)iy < 14u && (unsigned)ix < 14u;
+    const bf16x8 a = ok ? *reinterpret_cast<const bf16x8*>(in_img + img14(iy * 14 + ix, lane >> 4)) : zero8();
+    acc = mfma_bf16(a, bfrag(j, t), acc);
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int p = p0 + mt * 16 + 4 * (lane >> 4) + rr;
+    if (p < p1) epi(p, 16 * j + (lane & 15), acc[rr], pv[rr]);
+  }
+}
+
+// tconv7to14 restricted to output channels [16 nj, 16 nj + 16): 4 classes x
+// 4 m-tiles, two items per wave (classes w >> 2 and (w >> 2) + 2, m-tile
+// w & 3). Returns this lane's column (16 nj + (lane & 15)) sum of epi's values
+// over the wave's items.
+template <class Pre, class Epi>
+__device__ __forceinline__ float tconv7to14_half(const uint8_t* in, const uint8_t* wimg, int nj, Pre pre, Epi epi) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int mt = w & 3;
+  float pv[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = (w >> 2) + 2 * i;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r2 = mt * 16 + 4 * (lane >> 4) + rr;
+      const int jy2 = r2 / 7, jx2 = r2 - 7 * (r2 / 7);
+      pv[i][rr] = r2 < 49 ? pre((2 * jy2 + (q >> 1)) * 14 + 2 * jx2 + (q & 1), 16 * nj + (lane & 15)) : 0.f;
+    }
+  }
+  float cs = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = (w >> 2) + 2 * i;
+    const int a = q >> 1, b = q & 1;
+    const int r = mt * 16 + (lane & 15);
+    const int jy = r / 7, jx = r - 7 * (r / 7);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int ty = ks >> 2, tx = (ks >> 1) & 1, hh = ks & 1;
+      const int iy = jy + a - ty, ix = jx + b - tx;
+      const bool ok = r < 49 && (unsigned)iy < 7u && (unsigned)ix < 7u;
+      const bf16x8 av = ok ? *reinterpret_cast<const bf16x8*>(in + img49(iy * 7 + ix, 4 * hh + (lane >> 4))) : zero8();
+      const int tap = ((1 - a) + 2 * ty) * 4 + (1 - b) + 2 * tx;
+      const bf16x8 bv = tr_frag<32>(wimg + tap * 4096, 16 * nj, 32 * hh, lane);
+      acc = mfma_bf16(av, bv, acc);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r2 = mt * 16 + 4 * (lane >> 4) + rr;
+      if (r2 < 49) {
+        const int jy2 = r2 / 7, jx2 = r2 - 7 * (r2 / 7);
+        s += epi((2 * jy2 + a) * 14 + 2 * jx2 + b, 16 * nj + (lane & 15), acc[rr], pv[i][rr]);
+      }
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    cs += s;
+  }
+  return cs;
+}
+
+// P2 .. Q6 of one sample, role r (0/1) of its pair. LDS map: StepLayout (the
+// solo merged step's), every region used for the same thing.
+template <class L>
+__device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, uint8_t* lds, int n, int r,
+                                          const PairCtl& pc) {
+  float* Xs = reinterpret_cast<float*>(lds + L::X);
+  float* W4s = reinterpret_cast<float*>(lds + L::W4);
+  uint8_t* A1s = lds + L::A1;
+  __bf16* A2s = reinterpret_cast<__bf16*>(lds + L::A2);
+  uint8_t* D0u = lds + L::D0;  // img49
+  float* Hs = reinterpret_cast<float*>(lds + L::H);
+  __bf16* Zs = reinterpret_cast<__bf16*>(lds + L::Z);
+  float* Eps = reinterpret_cast<float*>(lds + L::Red);
+  float* Scr = reinterpret_cast<float*>(lds + L::Scr);
+  uint8_t* IMG = lds + L::IMG;
+  __bf16* D1s = reinterpret_cast<__bf16*>(lds + L::D1);
+  float* Gs = reinterpret_cast<float*>(lds + L::G);
+  const float* Bds = reinterpret_cast<const float*>(lds + L::Bd);
+  uint8_t* GD1s = lds + L::GD1;                                  // aliases Bd (dead after P5)
+  __bf16* GD0s = reinterpret_cast<__bf16*>(lds + L::GD0);        // aliases the DMA landing zone
+  float* DMs = reinterpret_cast<float*>(lds + L::DM);            // aliases X (dead after P7)
+  float* DZR = reinterpret_cast<float*>(lds + L::DZR);
+  uint8_t* GA2u = lds + L::GA2;                                  // img49, aliases D0 (dead after Q2)
+  float* GA2F = reinterpret_cast<float*>(lds + L::GA2F);         // aliases D1 (dead after Q1)
+  float* CS = reinterpret_cast<float*>(lds + L::CS);
+  float* CSB = reinterpret_cast<float*>(lds + L::CSB);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Weights& W = a.w;
+  const int M = pc.M;
+  const int p0 = r ? 24 : 0, p1 = r ? 49 : 24;  // own pixels of the 7x7 maps
+  const int q0 = r ? 0 : 24, q1 = r ? 24 : 49;  // the partner's
+  const int k0 = 64 * p0, klen = 64 * (p1 - p0);
+  const uint32_t tg = (uint32_t)a.st->step * 8u;  // tags tg + 1 .. tg + 6 (never 0: +1)
+  unsigned long long* xo = pc.xg + ((size_t)n * 2 + r) * kXW;        // own slab (written)
+  unsigned long long* xi = pc.xg + ((size_t)n * 2 + (r ^ 1)) * kXW;  // partner's (read, cleared)
+  const bool train = a.train != 0;
+  const float* Bias = reinterpret_cast<const float*>(lds + L::Bias);
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  if (tid == 0) xput(xo + kX1 + 64, tg + 1, xcc, false);  // X1 also carries this XCD's id
+
+  stamp(a.stamps, 2);
+  // P3's first two own-K weight rows per wave, in flight under P2
+  auto ld_rows = [&](int c2, bf16x8 (&v)[8]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = w + 16 * c2 + 8 * h, k = 512 * i + 8 * lane;
+        v[4 * h + i] = k < klen ? *reinterpret_cast<const bf16x8*>(W.Wh + (size_t)o * kFlat + k0 + k) : zero8();
+      }
+  };
+  bf16x8 wh0[8];
+  ld_rows(0, wh0);
+  // ---- P2: enc2 on own pixels, ReLU
+  conv14to7_rows(A1s, p0, p1, [&](int j, int t) { return conv_bfrag(IMG, j, t, lane); },
+                 [&](int, int col) { return Bias[kB2 + col]; }, [&](int p, int col, float v, float bias) {
+    const __bf16 o = (__bf16)fmaxf(v + bias, 0.f);
+    A2s[p * 64 + col] = o;
+    if (kGS && train) a.a2[(size_t)n * kFlat + p * 64 + col] = o;
+  });
+  lds_barrier();
+
+  TapImageRegs w3r;
+  w3r.load(W.W3);  // dec1 tap images: in flight during P3-P5
+  stamp(a.stamps, 3);
+  // ---- P3: head partial sums over own K (= own pixels). Wave w: rows
+  // w + 16 c2 and w + 16 c2 + 8 per step c2 (two rows of loads per step, the
+  // next step's in flight: the row loop is L2-latency bound, not bandwidth)
+  {
+    bf16x8 av[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = 512 * i + 8 * lane;
+      av[i] = k < klen ? *reinterpret_cast<const bf16x8*>(A2s + k0 + k) : zero8();
+    }
+    bf16x8 vc[8], vn[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vc[i] = wh0[i];
+#pragma unroll 1
+    for (int c2 = 0; c2 < 4; ++c2) {
+      if (c2 + 1 < 4) ld_rows(c2 + 1, vn);
+      float d[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float dq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16x8& wv = vc[4 * h + i];
+          if (512 * i + 8 * lane < klen) {
+            dq[0] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 0, 1),
+                                                    __builtin_shufflevector(wv, wv, 0, 1), dq[0], false);
+            dq[1] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 2, 3),
+                                                    __builtin_shufflevector(wv, wv, 2, 3), dq[1], false);
+            dq[2] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 4, 5),
+                                                    __builtin_shufflevector(wv, wv, 4, 5), dq[2], false);
+            dq[3] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 6, 7),
+                                                    __builtin_shufflevector(wv, wv, 6, 7), dq[3], false);
+          }
+        }
+        d[h] = (dq[0] + dq[1]) + (dq[2] + dq[3]);
+      }
+      d[0] = wave_sum(d[0]);
+      d[1] = wave_sum(d[1]);
+      if (lane == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int o = w + 16 * c2 + 8 * h;
+          Hs[o] = d[h];
+          xput(xo + kX1 + o, tg + 1, fbits(d[h]), false);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vc[i] = vn[i];
+    }
+  }
+  // P5's first dec_fc weight loads (own n-tiles t = 4 p0 + w + 8 i), in flight across P4
+  const int t0 = 4 * p0, t1 = 4 * p1;
+  const __bf16* wp5 = W.Wd + (size_t)(lane & 15) * 32 + 8 * (lane >> 4);
+  auto wd5_ld = [&](int i) {
+    const int t = t0 + w + 8 * i;
+    return *reinterpret_cast<const bf16x8*>(wp5 + (size_t)(t < t1 ? t : t0) * 512);
+  };
+  bf16x8 wd5[13];
+#pragma unroll
+  for (int i = 0; i < 13; ++i) wd5[i] = wd5_ld(i);
+  lds_barrier();
+
+  stamp(a.stamps, 4);
+  // ---- X1 + P4: mu | logvar = (role-0 part + role-1 part) + bias; reparam + KLD (both halves)
+  if (tid < 64) {
+    float kl = 0.f;
+    if (tid < 32) {
+      const int c = tid;
+      const int gi[2] = {kX1 + c, kX1 + 32 + c};
+      uint32_t pv[2];
+      xget<2>(xi, gi, tg + 1, pv, pc.err, false);
+      const float m0 = Hs[c], l0 = Hs[32 + c], mp = bitsf(pv[0]), lp = bitsf(pv[1]);
+      const float mu = (r ? mp + m0 : m0 + mp) + Bias[kBh + c];
+      const float lv = (r ? lp + l0 : l0 + lp) + Bias[kBh + 32 + c];
+      Hs[c] = mu;
+      Hs[32 + c] = lv;
+      const unsigned long long stp = (unsigned long long)a.st->step;
+      const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(n * 32 + c), a.stream, (uint32_t)(stp & 0xffffffffu),
+                                             (uint32_t)(stp >> 32)},
+                                       a.hp->seed_lo, a.hp->seed_hi);
+      const float ep = normal_from_bits(bits.x, bits.y);
+      const float sd = expf(0.5f * lv);
+      const float zz = mu + ep * sd;
+      kl = 1.f + lv - mu * mu - sd * sd;
+      Zs[c] = (__bf16)zz;
+      Eps[c] = ep;
+      if (kGS && train && r == 0) {
+        if (kGS) a.mulv[(size_t)n * 64 + c] = mu;
+        if (kGS) a.mulv[(size_t)n * 64 + 32 + c] = lv;
+        if (kGS) a.eps[(size_t)n * 32 + c] = ep;
+        if (kGS) a.z16[(size_t)n * 32 + c] = (__bf16)zz;
+      }
+    }
+    if (tid == 32) {
+      const int gi[1] = {kX1 + 64};
+      uint32_t pv[1];
+      xget<1>(xi, gi, tg + 1, pv, pc.err, false);
+      reinterpret_cast<int*>(Scr)[30] = pv[0] == xcc;
+    }
+    kl = wave_sum(kl);
+    if (tid == 0) Scr[0] = -0.5f * kl;
+  }
+  lds_barrier();
+  const bool near = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(Scr)[30]) != 0;
+  if (a.stamps && tid == 0) a.stamps[blockIdx.x * 16 + 15] |= (unsigned long long)near << 4;  // mode | near << 4
+
+  stamp(a.stamps, 5);
+  // ---- P5: dec_fc on own pixels (n-tiles [t0, t1)), ReLU; X2 publishes them
+  {
+    const bf16x8 av = (lane & 15) == 0 ? *reinterpret_cast<const bf16x8*>(Zs + 8 * (lane >> 4)) : zero8();
+    stream2_pre<13, 1>(wd5, wd5_ld, [&](int i, const bf16x8& bw) {
+      const int t = t0 + w + 8 * i;
+      if (t < t1) {
+        const f32x4 acc = mfma_bf16(av, bw, f32x4{0.f, 0.f, 0.f, 0.f});
+        const int jj = 16 * t + (lane & 15);
+        const __bf16 o = (__bf16)fmaxf(acc[0] + Bds[jj], 0.f);
+        const uint32_t ob = bf16bits(o), nb = (uint32_t)__shfl_xor((int)ob, 1, 64);
+        if (lane < 16) {
+          *reinterpret_cast<__bf16*>(D0u + img49e(jj >> 6, jj & 63)) = o;
+          if (kGS && train) a.d0[(size_t)n * kFlat + jj] = o;
+          if ((lane & 1) == 0) xput(xo + kX2 + ((jj - k0) >> 1), tg + 2, ob | (nb << 16), near);
+        }
+      }
+    });
+  }
+  w3r.store(IMG);
+  {  // X2: the partner's d0 pixels into the img49 image
+    const int cnt = 32 * (q1 - q0);
+    const int gi[2] = {tid < cnt ? kX2 + tid : -1, tid + 512 < cnt ? kX2 + tid + 512 : -1};
+    uint32_t pv[2];
+    xget<2>(xi, gi, tg + 2, pv, pc.err, near);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (gi[k] >= 0) {
+        const int jj = 64 * q0 + 2 * (gi[k] - kX2);
+        *reinterpret_cast<uint32_t*>(D0u + img49e(jj >> 6, jj & 63)) = pv[k];
+      }
+    }
+  }
+  lds_barrier();
+
+  stamp(a.stamps, 6);
+  // ---- P6: dec1 (convT 64 -> 32) on own channels [16 r, 16 r + 16), ReLU
+  tconv7to14_half(D0u, IMG, r, [&](int, int co) { return Bias[kB3 + co]; }, [&](int pix, int co, float v, float bias) {
+    const __bf16 o = (__bf16)fmaxf(v + bias, 0.f);
+    D1s[pix * 32 + co] = o;
+    if (kGS && train) a.d1[((size_t)n * 196 + pix) * 32 + co] = o;
+    return 0.f;
+  });
+  lds_barrier();
+
+  stamp(a.stamps, 7);
+  // ---- P7: dec2 partial logits over own channels, X3, then BCE + dlogits (both)
+  float loss = 0.f, gsum = 0.f;
+  {
+    float tp[2] = {0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int pix = tid + 512 * k;
+      if (pix < 784) {
+        const int oy = pix / 28, ox = pix - 28 * (pix / 28);
+        const int ca = oy & 1, cb = ox & 1, jy = oy >> 1, jx = ox >> 1;
+        float t = 0.f;
+#pragma unroll
+        for (int ty = 0; ty < 2; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 2; ++tx) {
+            const int iy = jy + ca - ty, ix = jx + cb - tx;
+            if ((unsigned)iy < 14u && (unsigned)ix < 14u) {
+              const int tap = ((1 - ca) + 2 * ty) * 4 + (1 - cb) + 2 * tx;
+              const bf16x8* dp = reinterpret_cast<const bf16x8*>(D1s + (iy * 14 + ix) * 32 + 16 * r);
+              const float4* wp = reinterpret_cast<const float4*>(W4s + tap * 32 + 16 * r);
+#pragma unroll
+              for (int ch = 0; ch < 2; ++ch) {
+                const bf16x8 dv = dp[ch];
+                const float4 w0 = wp[2 * ch], w1 = wp[2 * ch + 1];
+                t = fmaf((float)dv[0], w0.x, t); t = fmaf((float)dv[1], w0.y, t);
+                t = fmaf((float)dv[2], w0.z, t); t = fmaf((float)dv[3], w0.w, t);
+                t = fmaf((float)dv[4], w1.x, t); t = fmaf((float)dv[5], w1.y, t);
+                t = fmaf((float)dv[6], w1.z, t); t = fmaf((float)dv[7], w1.w, t);
+              }
+            }
+          }
+        tp[k] = t;
+        xput(xo + kX3 + pix, tg + 3, fbits(t), near);
+      }
+    }
+    const int gi[2] = {tid < 784 ? kX3 + tid : -1, tid + 512 < 784 ? kX3 + tid + 512 : -1};
+    uint32_t pv[2];
+    xget<2>(xi, gi, tg + 3, pv, pc.err, near);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int pix = tid + 512 * k;
+      if (pix < 784) {
+        const float pp = bitsf(pv[k]);
+        const float t = Bias[kB4] + (r ? pp + tp[k] : tp[k] + pp);
+        const float x = Xs[pix];
+        const float p = 1.f / (1.f + expf(-t));
+        const float g = p - x;
+        const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));
+        loss += x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
+        gsum += g;
+        Gs[pix] = g;
+        if (kGS && train && (pix >= 392) == (r == 1)) a.dlog[(size_t)n * 784 + pix] = g;
+        if (kGS && a.recon && (pix >= 392) == (r == 1)) a.recon[(size_t)n * 784 + pix] = p;
+      }
+    }
+  }
+  loss = wave_sum(loss);
+  gsum = wave_sum(gsum);
+  if (lane == 0) {
+    Scr[8 + w] = loss;
+    Scr[16 + w] = gsum;
+  }
+  lds_barrier();
+  if (tid == 0 && r == 0) {
+    float sl = 0.f, sg = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sl += Scr[8 + i];
+      sg += Scr[16 + i];
+    }
+    if (kGS) a.bce_part[n] = sl;
+    if (kGS) a.kld_part[n] = Scr[0];
+    if (kGS && a.db4_part) a.db4_part[n] = sg;
+  }
+
+  stamp(a.stamps, 8);
+  // ---- Q1: dec2 backward-data on own channels (8 per thread) x dec1 ReLU mask; X4 publishes gd1
+  if (tid < 392) {
+    const int pix = tid >> 1, h = tid & 1, cg = 2 * r + h;  // 8-channel chunk cg of 4
+    const int oy = pix / 14, ox = pix - 14 * (pix / 14);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    const bf16x8 m = reinterpret_cast<const bf16x8*>(lds + L::D1 + pix * 64)[cg];
+#pragma unroll 4
+    for (int t = 0; t < 16; ++t) {
+      const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
+      const bool ok = (unsigned)iy < 28u && (unsigned)ix < 28u;
+      const float g = ok ? Gs[iy * 28 + ix] : 0.f;
+      const float4 w0 = reinterpret_cast<const float4*>(W4s + t * 32 + 8 * cg)[0];
+      const float4 w1 = reinterpret_cast<const float4*>(W4s + t * 32 + 8 * cg)[1];
+      acc[0] = fmaf(g, w0.x, acc[0]); acc[1] = fmaf(g, w0.y, acc[1]);
+      acc[2] = fmaf(g, w0.z, acc[2]); acc[3] = fmaf(g, w0.w, acc[3]);
+      acc[4] = fmaf(g, w1.x, acc[4]); acc[5] = fmaf(g, w1.y, acc[5]);
+      acc[6] = fmaf(g, w1.z, acc[6]); acc[7] = fmaf(g, w1.w, acc[7]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (float)m[e] > 0.f ? acc[e] : 0.f;
+      o[e] = (__bf16)v;
+      CSB[(8 * h + e) * 197 + pix] = v;  // dec1 bias partials (own channel 8 h + e)
+    }
+    *reinterpret_cast<bf16x8*>(GD1s + img14(pix, cg)) = o;
+    if (kGS) *reinterpret_cast<bf16x8*>(b.gd1 + ((size_t)n * 196 + pix) * 32 + 8 * cg) = o;
+#pragma unroll
+    for (int e = 0; e < 8; e += 2)  // granule layout [4][392]: one wave store = 512 contiguous bytes
+      xput(xo + kX4 + (e >> 1) * 392 + tid, tg + 4, bf16bits(o[e]) | (bf16bits(o[e + 1]) << 16), near);
+  }
+  // Q3's first dec_fc weight loads (own rows), in flight during X4 and Q2
+  const int jr = lane >> 2;
+  auto wd_ld = [&](int it) {
+    const int jj = k0 + it * 128 + w * 16 + jr;
+    return *reinterpret_cast<const bf16x8*>(W.Wd + (size_t)(jj < k0 + klen ? jj : k0) * 32 + 8 * (lane & 3));
+  };
+  bf16x8 wd0[13];
+#pragma unroll
+  for (int i = 0; i < 13; ++i) wd0[i] = wd_ld(i);
+  lds_barrier();
+  if (tid < 128) {  // dec1 bias partials of own channels: 8 lanes per channel, fixed order
+    const int c = tid >> 3, part = tid & 7;
+    float s = 0.f;
+    for (int p = part; p < 196; p += 8) s += CSB[c * 197 + p];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (part == 0) b.db3_part[(size_t)n * 32 + 16 * r + c] = s;
+  }
+  {  // X4: the partner's gd1 channels into the img14 image
+    int gi[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) gi[k] = tid + 512 * k < 1568 ? kX4 + tid + 512 * k : -1;
+    uint32_t pv[4];
+    xget<4>(xi, gi, tg + 4, pv, pc.err, near);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (gi[k] >= 0) {
+        const int g = gi[k] - kX4, e2 = g / 392, t = g - 392 * e2;
+        const int pix = t >> 1, ch = 16 * (r ^ 1) + 8 * (t & 1) + 2 * e2;
+        *reinterpret_cast<uint32_t*>(GD1s + img14(pix, ch >> 3) + ((ch & 7) << 1)) = pv[k];
+      }
+    }
+  }
+  lds_barrier();
+
+  stamp(a.stamps, 9);
+  // ---- Q2: dec1 backward-data (conv 32 -> 64, B from dec1's tap images) on own pixels x dec_fc mask
+  conv14to7_rows(GD1s, p0, p1,
+                 [&](int j, int t) {
+                   return *reinterpret_cast<const bf16x8*>(IMG + t * 4096 + timg<32>(16 * j + (lane & 15), lane >> 4));
+                 },
+                 [&](int p, int col) { return (float)*reinterpret_cast<const __bf16*>(D0u + img49e(p, col)); },
+                 [&](int p, int col, float v, float mask) {
+    const size_t e = (size_t)n * kFlat + p * 64 + col;
+    const float g = mask > 0.f ? v : 0.f;
+    const __bf16 o = (__bf16)g;
+    GD0s[p * 64 + col] = o;
+    if (kGS) b.gd0[e] = o;
+    if (kGS) b.dbd_part[e] = g;
+  });
+  lds_barrier();
+
+  TapImageRegs w2r;
+  w2r.load(W.W2);  // enc2 tap images: in flight during Q3-Q5
+  stamp(a.stamps, 10);
+  // ---- Q3: dz partial over own dec_fc rows
+  {
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    stream2_pre<13, 1>(wd0, wd_ld, [&](int it, const bf16x8& wv) {
+      const int jj = k0 + it * 128 + w * 16 + jr;
+      if (jj < k0 + klen) {
+        const float g = (float)GD0s[jj];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(g, (float)wv[e], acc[e]);
+      }
+    });
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = acc[e];
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      acc[e] = v;
+    }
+    if (lane < 4) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) DZR[w * 32 + 8 * lane + e] = acc[e];
+    }
+  }
+  // Q5's first 16 head-weight loads: row group grp = tid >> 8 (rows 32 grp ..), own 8-chunk ck
+  const int nck = klen >> 3, grp = tid >> 8, ck = tid & 255;
+  const int kk = k0 + 8 * (ck < nck ? ck : 0);
+  auto wh_ld = [&](int i) { return *reinterpret_cast<const bf16x8*>(W.Wh + (size_t)(32 * grp + i) * kFlat + kk); };
+  bf16x8 wh5[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) wh5[i] = wh_ld(i);
+  lds_barrier();
+
+  stamp(a.stamps, 11);
+  // ---- X5 + Q4: dz = role-0 part + role-1 part; reparam backward (both halves)
+  if (tid < 32) {
+    const int c = tid;
+    float mine = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mine += DZR[i * 32 + c];
+    xput(xo + kX5 + c, tg + 5, fbits(mine), near);
+    const int gi[1] = {kX5 + c};
+    uint32_t pv[1];
+    xget<1>(xi, gi, tg + 5, pv, pc.err, near);
+    const float dz = r ? bitsf(pv[0]) + mine : mine + bitsf(pv[0]);
+    const float beta = a.hp->kl_beta;
+    const float mu = Hs[c], lv = Hs[32 + c], ep = Eps[c];
+    const float sd = expf(0.5f * lv);
+    const float dm = dz + beta * mu;
+    const float dl = 0.5f * dz * ep * sd + 0.5f * beta * (sd * sd - 1.f);
+    DMs[c] = dm;
+    DMs[32 + c] = dl;
+    if (r == 0) {
+      if (kGS) b.dmulv[(size_t)n * 64 + c] = dm;
+      if (kGS) b.dmulv[(size_t)n * 64 + 32 + c] = dl;
+      if (kGS) b.dmulv16[(size_t)n * 64 + c] = (__bf16)dm;
+      if (kGS) b.dmulv16[(size_t)n * 64 + 32 + c] = (__bf16)dl;
+    }
+  }
+  lds_barrier();
+
+  stamp(a.stamps, 12);
+  // ---- Q5: head backward-data on own K: two row groups of 32 per 8-chunk, combined in a fixed order
+  {
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    stream2_pre<16, 2>(wh5, wh_ld, [&](int i, const bf16x8& wv) {
+      const float dm = DMs[32 * grp + i];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf(dm, (float)wv[e], acc[e]);
+    });
+    if (grp == 1 && ck < nck) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) CSB[ck * 8 + e] = acc[e];
+    }
+    lds_barrier();
+    if (grp == 0 && ck < nck) {
+      const bf16x8 mk = *reinterpret_cast<const bf16x8*>(A2s + kk);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v0 = acc[e] + CSB[ck * 8 + e];
+        const float v = (float)mk[e] > 0.f ? v0 : 0.f;
+        o[e] = (__bf16)v;
+        GA2F[kk + e] = v;
+      }
+      *reinterpret_cast<bf16x8*>(GA2u + img49(kk >> 6, (kk >> 3) & 7)) = o;
+      if (kGS) *reinterpret_cast<bf16x8*>(b.ga2 + (size_t)n * kFlat + kk) = o;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2)  // granule layout [4][200] (8-chunk ck of the own range)
+        xput(xo + kX6 + (e >> 1) * 200 + ck, tg + 6, bf16bits(o[e]) | (bf16bits(o[e + 1]) << 16), near);
+    }
+  }
+  w2r.store(IMG);
+  {  // X6: the partner's ga2 pixels into the img49 image
+    const int nckp = 8 * (q1 - q0);  // the partner's 8-chunks
+    int gi[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int g = tid + 512 * k, e2 = g / 200, c = g - 200 * e2;
+      gi[k] = g < 800 && c < nckp ? kX6 + g : -1;
+    }
+    uint32_t pv[2];
+    xget<2>(xi, gi, tg + 6, pv, pc.err, near);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (gi[k] >= 0) {
+        const int g = gi[k] - kX6, e2 = g / 200, c = g - 200 * e2;
+        const int jj = 64 * q0 + 8 * c + 2 * e2;
+        *reinterpret_cast<uint32_t*>(GA2u + img49e(jj >> 6, jj & 63)) = pv[k];
+      }
+    }
+  }
+  lds_barrier();
+  if (tid < 64) {  // enc2 bias partials over own pixels, in order: row r of [2][M][64]
+    float s = 0.f;
+    for (int p = p0; p < p1; ++p) s += GA2F[p * 64 + tid];
+    if (kGS) b.db2_part[((size_t)r * M + n) * 64 + tid] = s;
+  }
+
+  stamp(a.stamps, 13);
+  // ---- Q6: enc2 backward-data (convT 64 -> 32 with the conv weights) on own channels x enc1 mask
+  {
+    const float cs = tconv7to14_half(GA2u, IMG, r,
+                                     [&](int pix, int co) {
+                                       return (float)*reinterpret_cast<const __bf16*>(A1s + img14(pix, co >> 3) +
+                                                                                      ((co & 7) << 1));
+                                     },
+                                     [&](int pix, int co, float v, float mask) {
+      const float g = mask > 0.f ? v : 0.f;
+      if (kGS) b.ga1[((size_t)n * 196 + pix) * 32 + co] = (__bf16)g;
+      return g;
+    });
+    if (lane < 16) CS[w * 16 + lane] = cs;
+  }
+  lds_barrier();
+  if (tid < 16) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += CS[i * 16 + tid];
+    if (kGS) b.db1_part[(size_t)n * 32 + 16 * r + tid] = s;
+  }
+  stamp(a.stamps, 14);
+}
+
+}  // namespace f28
+}  // namespace mdt

@@ -70,7 +70,9 @@ int mdt_pack_jobs_multi_fin(const mdt::JobBlob* jobs, int n, void* dst, int fin,
 int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s);
 int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train, hipStream_t s);
 int mdt_f28_backward(const long long* p, int M, hipStream_t s);
-int mdt_f28_step(const long long* pf, const long long* pb, int B, int M, unsigned stream, hipStream_t s);
+int mdt_f28_step(const long long* pf, const long long* pb, const long long* pp, int B, int M, unsigned stream,
+                 int pair, int delay_us, hipStream_t s);
+int mdt_f28_pair_words();
 int mdt_launch_job1(const mdt::JobBlob* j, hipStream_t s);
 int mdt_launch_tail(const mdt::JobBlob* wg, const mdt::JobBlob* fin0, const mdt::JobBlob* finr, int* ticket,
                     hipStream_t s);
@@ -455,7 +457,7 @@ std::vector<Slot> f28_fwd_slots(int64_t B, bool train) {
       {"mulv", 'f', 64, false, !train},    {"eps", 'f', 32, false, !train},   {"z16", 'b', 32, false, !train},
       {"d0", 'b', 3136, false, !train},    {"d1", 'b', 6272, false, !train},  {"dlog", 'f', 784, false, !train},
       {"recon", 'f', 784, false, true},    {"bce_part", 'f', 1, false, false}, {"kld_part", 'f', 1, false, false},
-      {"db4_part", 'f', 1, false, true},   {"stamps", 'l', 16, false, true}};
+      {"db4_part", 'f', 1, false, true},   {"stamps", 'l', 32, false, true}};
   slots.insert(slots.end(), rest.begin(), rest.end());
   return slots;
 }
@@ -469,8 +471,8 @@ std::vector<Slot> f28_bwd_slots() {
       {"dlog", 'f', 784, false, false},    {"gd1", 'b', 6272, false, false},   {"gd0", 'b', 3136, false, false},
       {"dbd_part", 'f', 3136, false, false}, {"dmulv", 'f', 64, false, false}, {"dmulv16", 'b', 64, false, false},
       {"ga2", 'b', 3136, false, false},    {"ga1", 'b', 6272, false, false},   {"db3_part", 'f', 32, false, false},
-      {"db2_part", 'f', 64, false, false}, {"db1_part", 'f', 32, false, false},
-      {"stamps", 'l', 16, false, true}};
+      {"db2_part", 'f', 128, false, false}, {"db1_part", 'f', 32, false, false},
+      {"stamps", 'l', 32, false, true}};
   slots.insert(slots.end(), rest.begin(), rest.end());
   return slots;
 }
@@ -489,14 +491,27 @@ void f28_backward(const std::vector<c10::optional<at::Tensor>>& t, int64_t M) {
   rc(mdt_f28_backward(p.data(), (int)M, cur()), "f28_backward");
 }
 
-// Forward + backward of one training step in ONE launch (f28_step_k).
+// Forward + backward of one training step in ONE launch (f28_step_k). With
+// `pair` (three tensors: exchange granules int64 [B][2][f28_pair_words()],
+// pairing words int32 [B], error word int32 [1], all zero-initialised) the
+// launch runs two workgroups per sample.
 void f28_step(const std::vector<c10::optional<at::Tensor>>& tf, const std::vector<c10::optional<at::Tensor>>& tb,
-              int64_t B, int64_t M, int64_t stream) {
+              int64_t B, int64_t M, int64_t stream, const std::vector<c10::optional<at::Tensor>>& pair,
+              int64_t pair_delay_us) {
   TORCH_CHECK(M > 0 && M <= B, "f28_step: bad M ", M, " for B ", B);
   const int dev = tf[0].has_value() ? (int)tf[0]->device().index() : 0;
   const auto pf = f28_ptrs(tf, f28_fwd_slots(B, true), M, dev);
   const auto pb = f28_ptrs(tb, f28_bwd_slots(), M, dev);
-  rc(mdt_f28_step(pf.data(), pb.data(), (int)B, (int)M, (unsigned)stream, cur()), "f28_step");
+  std::vector<long long> pp;
+  if (!pair.empty()) {
+    const std::vector<Slot> ps = {{"xchg", 'l', 2 * (int64_t)mdt_f28_pair_words(), false, false},
+                                  {"pairw", 'i', 1, false, false},
+                                  {"err", 'i', 1, true, false}};
+    pp = f28_ptrs(pair, ps, M, dev);
+  }
+  rc(mdt_f28_step(pf.data(), pb.data(), pp.empty() ? nullptr : pp.data(), (int)B, (int)M, (unsigned)stream,
+                  pp.empty() ? 0 : 1, (int)pair_delay_us, cur()),
+     "f28_step");
 }
 
 void step_begin(at::Tensor state, const at::Tensor& hparams) {
@@ -700,8 +715,10 @@ void bind_conv(pybind11::module& m) {
   m.def("f28_forward", &f28_forward, py::arg("tensors"), py::arg("B"), py::arg("M"), py::arg("stream"),
         py::arg("train"));
   m.def("f28_backward", &f28_backward, py::arg("tensors"), py::arg("M"));
+  m.def("f28_pair_words", &mdt_f28_pair_words);
   m.def("f28_step", &f28_step, py::arg("fwd_tensors"), py::arg("bwd_tensors"), py::arg("B"), py::arg("M"),
-        py::arg("stream"));
+        py::arg("stream"), py::arg("pair") = std::vector<c10::optional<at::Tensor>>{},
+        py::arg("pair_delay_us") = 0);
   m.def("launch_tail", &launch_tail);
   m.def("igemm", &igemm, py::arg("mode"), py::arg("A"), py::arg("B16"), py::arg("desc"), py::arg("bias"),
         py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),

@@ -31,8 +31,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "multidisttorch_amd")
 CSRC = os.path.join(ROOT, "csrc")
 SANITIZE = os.getenv("MDT_SANITIZE", "0") == "1"
-BUILD = os.path.join(ROOT, "build", "native_san" if SANITIZE else "native")
-OUT = os.path.join(ROOT, "build", "san", "_C.so") if SANITIZE else os.path.join(PKG, "_C.so")
+# MDT_BUILD_TAG=name: an A/B variant (e.g. with MDT_HIP_EXTRA_FLAGS=-D...) built
+# into variants/<name>/_C.so (objects in build/native_<name>); load it on the
+# GPU box with MDT_NATIVE_SO=variants/<name>/_C.so. The default build is untouched.
+TAG = os.getenv("MDT_BUILD_TAG", "")
+BUILD = os.path.join(ROOT, "build", "native_san" if SANITIZE else ("native_" + TAG if TAG else "native"))
+OUT = (os.path.join(ROOT, "build", "san", "_C.so") if SANITIZE else
+       os.path.join(ROOT, "variants", TAG, "_C.so") if TAG else os.path.join(PKG, "_C.so"))
 SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
 ARCH = os.environ.get("MDT_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")

@@ -267,6 +267,10 @@ class ConvVaeTrainer:
         self.f28_skip_adam = False  # tests: leave the reduced gradients in `grads`, no update
         # forward and backward of the fused step in one launch (MDT_F28_MERGE=0: two)
         self.f28_merge = os.getenv("MDT_F28_MERGE", "1") != "0"
+        # the merged step with two workgroups per sample (conv28_pair.h): a
+        # B = 128 trial fills all 256 CUs instead of 128. MDT_F28_PAIR=0 (A/B): one per sample
+        self.f28_pair = os.getenv("MDT_F28_PAIR", "1") != "0"
+        self.f28_pair_delay_us = 0  # tests: delay every partner workgroup (forces the solo fallback)
         # finalize + Adam as the last job of the weight-gradient launch, each
         # unit released by its layer's ticket (conv_jobs.hip JobPackN): 2
         # launches per step instead of 3. Bitwise-tested but measured 4x
@@ -500,7 +504,12 @@ class ConvVaeTrainer:
         if self.f28:
             self.dlog32 = torch.zeros(B * self.D, **f32)
             self.f28_part = torch.zeros(3 * B, **f32)                  # bce | kld | dec2-bias partials
-            self.f28_bias = torch.zeros(B * (3136 + 32 + 64 + 32), **f32)  # dec_fc | dec1 | enc2 | enc1
+            # bias partials: dec_fc [B][3136] | dec1 [B][32] | enc2 [2][B][64] (a row per pair half) | enc1 [B][32]
+            self.f28_bias = torch.zeros(B * (3136 + 32 + 128 + 32), **f32)
+            # paired step state: exchange granules, pairing words, error word (all zero between launches)
+            self.f28_xg = torch.zeros(B * 2 * self.C.f28_pair_words(), dtype=torch.int64, device=dev)
+            self.f28_pairw = torch.zeros(B, dtype=torch.int32, device=dev)
+            self.f28_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._cast_weights()
 
     def _n_bce(self, M):
@@ -1013,8 +1022,8 @@ class ConvVaeTrainer:
         bias = self.f28_bias
         dbd = bias.narrow(0, 0, B * 3136)
         db3 = bias.narrow(0, B * 3136, B * 32)
-        db2 = bias.narrow(0, B * 3168, B * 64)
-        db1 = bias.narrow(0, B * 3232, B * 32)
+        db2 = bias.narrow(0, B * 3168, 2 * B * 64)  # [2][M][64] for a batch of M
+        db1 = bias.narrow(0, B * 3296, B * 32)
         a1, a2, d0, d1 = self.acts["enc1"], self.acts["enc2"], self.acts["dec_fc"], self.acts["dec1"]
         gd1, gd0, ga2, ga1 = self.gacts["dec1"], self.gacts["dec_fc"], self.gacts["enc2"], self.gacts["enc1"]
         fwd = w + [X, idx, st.train_state, st.hparams, self.xb, a1, a2, self.mulv, self.eps, self.z16, d0, d1,
@@ -1038,9 +1047,9 @@ class ConvVaeTrainer:
         C.loss_finalize2(bce, M, kld, M, st.train_state, st.hparams, True, job=j, advance_step=True)
         jobs.append(j)
         # bias gradients: per-sample partial rows written by the fused kernels
-        for name, t, width in (("enc1", db1, 32), ("enc2", db2, 64), ("enc_head", self.dmulv, 64),
-                               ("dec_fc", dbd, 3136), ("dec1", db3, 32), ("dec2", db4, 1)):
-            slabs[name + ".bias"] = (t, M)
+        for name, t, rows in (("enc1", db1, M), ("enc2", db2, 2 * M), ("enc_head", self.dmulv, M),
+                              ("dec_fc", dbd, M), ("dec1", db3, M), ("dec2", db4, M)):
+            slabs[name + ".bias"] = (t, rows)
         segs = self._seg_rows(slabs)
         units, layer_units = self._finalize_units(segs)
         pack, grid = C.pack_jobs_multi(jobs)
@@ -1071,7 +1080,9 @@ class ConvVaeTrainer:
         Adam + bf16 cast)."""
         C, p, st = self.C, self._plan28(M), self.state
         if self.f28_merge:
-            C.f28_step(p["fwd"], p["bwd"], self.B, M, self.rng_stream)
+            C.f28_step(p["fwd"], p["bwd"], self.B, M, self.rng_stream,
+                       pair=[self.f28_xg, self.f28_pairw, self.f28_err] if self.f28_pair else [],
+                       pair_delay_us=self.f28_pair_delay_us)
         else:
             C.f28_forward(p["fwd"], self.B, M, self.rng_stream, True)
             C.f28_backward(p["bwd"], M)
