@@ -402,8 +402,12 @@ void launch_jobs_multi(const at::Tensor& dev_pack, int64_t grid) {
 
 // Fused 28x28 step launches (conv28_fused.hip). `t` lists the tensors in the
 // kernel's pointer-table order (None -> nullptr where optional); every tensor is
-// checked for device, contiguity, dtype and minimum size BEFORE the launch so
-// a shape mistake is a Python error, never an out-of-bounds access on the GPU.
+// checked for device, contiguity, dtype and minimum size BEFORE the launch, so
+// a wrong buffer is a Python error rather than an out-of-bounds access. Not
+// checkable here: the gathered rows X[idx[cursor * B + n]] depend on device
+// state (the cursor) and on the index VALUES; the trainer guarantees them
+// (bind_train_data pads idx to whole batches of in-range rows, set_cursor
+// keeps cursor < nbatches), and the checks below pin the shapes they assume.
 namespace {
 struct Slot {
   const char* name;
@@ -477,8 +481,16 @@ std::vector<Slot> f28_bwd_slots() {
   return slots;
 }
 
+// X is [rows][784] and idx whole batches of B (cursor * B + n indexes it).
+void f28_check_data(const std::vector<c10::optional<at::Tensor>>& t, int64_t B) {
+  TORCH_CHECK(t.size() > 13 && t[12].has_value() && t[13].has_value(), "f28: X and idx are required");
+  TORCH_CHECK(t[12]->numel() % 784 == 0, "f28: X must be [rows][784], has ", t[12]->numel(), " elements");
+  TORCH_CHECK(t[13]->numel() % B == 0, "f28: idx must hold whole batches of ", B, ", has ", t[13]->numel());
+}
+
 void f28_forward(const std::vector<c10::optional<at::Tensor>>& t, int64_t B, int64_t M, int64_t stream, bool train) {
   TORCH_CHECK(M > 0 && M <= B, "f28_forward: bad M ", M, " for B ", B);
+  f28_check_data(t, B);
   const int dev = t[0].has_value() ? (int)t[0]->device().index() : 0;
   const auto p = f28_ptrs(t, f28_fwd_slots(B, train), M, dev);
   rc(mdt_f28_forward(p.data(), (int)B, (int)M, (unsigned)stream, train ? 1 : 0, cur()), "f28_forward");
@@ -499,6 +511,7 @@ void f28_step(const std::vector<c10::optional<at::Tensor>>& tf, const std::vecto
               int64_t B, int64_t M, int64_t stream, const std::vector<c10::optional<at::Tensor>>& pair,
               int64_t pair_delay_us) {
   TORCH_CHECK(M > 0 && M <= B, "f28_step: bad M ", M, " for B ", B);
+  f28_check_data(tf, B);
   const int dev = tf[0].has_value() ? (int)tf[0]->device().index() : 0;
   const auto pf = f28_ptrs(tf, f28_fwd_slots(B, true), M, dev);
   const auto pb = f28_ptrs(tb, f28_bwd_slots(), M, dev);

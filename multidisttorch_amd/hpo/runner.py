@@ -40,7 +40,7 @@ from ..parallel.ddp import broadcast_params, make_arena_reducer
 from ..parallel.groups import print0
 from ..runtime.bootstrap import bound_device, global_barrier
 from ..runtime.faults import (InjectedFault, TrialTimeout, agree_healthy, fault_step, group_timeout_s, guarded,
-                              maybe_inject)
+                              heartbeat_s, maybe_inject, trial_watch)
 from ..utils.images import flush_images, save_image_async
 from .trial import TrialSpec
 
@@ -121,13 +121,35 @@ def _load_data(opts: RunOptions, device):
 LOSS_RING = 4096  # per-step loss history ring of the trainers (kLossHist, csrc/kernels/vae_mlp.h)
 
 
-def _launch_epoch(trainer, epoch: int, n_shard: int, opts: RunOptions, fault_at: Optional[int] = None):
+def _steps(trainer, n: int, B: int, events):
+    """``train_steps(n)``; with an ``events`` list, in chunks of about 64 steps
+    (a whole number of captured graphs) each followed by a recorded event, so
+    a waiter can tell a slow epoch that is still completing steps from a stuck
+    one."""
+    if events is None:
+        trainer.train_steps(n, B)
+        return
+    gs = max(1, int(getattr(trainer, "graph_steps", 1)))
+    chunk = gs * max(1, 64 // gs)
+    done = 0
+    while done < n:
+        k = min(chunk, n - done)
+        trainer.train_steps(k, B)
+        done += k
+        ev = torch.cuda.Event()
+        ev.record()
+        events.append(ev)
+
+
+def _launch_epoch(trainer, epoch: int, n_shard: int, opts: RunOptions, fault_at: Optional[int] = None,
+                  events=None):
     """Enqueue one epoch of steps on the current stream; returns (step counter
     before the epoch, {batch_idx: loss} of log lines whose ring slots were read
     early). No host sync unless the epoch is longer than the loss ring: then
     the ring is read after every LOSS_RING steps, before it wraps (batch sizes
     below 15 on a 60000-sample shard). ``fault_at`` (MDT_FAULT step=) stops
-    issuing steps at that optimizer step and raises, mid-epoch."""
+    issuing steps at that optimizer step and raises, mid-epoch. ``events``
+    (a list) receives progress events (see ``_steps``)."""
     B = opts.batch_size
     full, tail = n_shard // B, n_shard % B
     nb = full + (1 if tail else 0)
@@ -141,9 +163,9 @@ def _launch_epoch(trainer, epoch: int, n_shard: int, opts: RunOptions, fault_at:
         while c < full:
             n = min(full - c, LOSS_RING) if nb > LOSS_RING else full - c
             if stop is not None and c + n > stop:
-                trainer.train_steps(stop - c, B)
+                _steps(trainer, stop - c, B, events)
                 raise InjectedFault(f"injected fault at step {fault_at} (epoch {epoch})")
-            trainer.train_steps(n, B)
+            _steps(trainer, n, B, events)
             if nb > LOSS_RING:
                 hist = trainer.loss_history()
                 assert len(hist) == LOSS_RING
@@ -154,32 +176,60 @@ def _launch_epoch(trainer, epoch: int, n_shard: int, opts: RunOptions, fault_at:
         if tail:
             if stop is not None and stop == full:
                 raise InjectedFault(f"injected fault at step {fault_at} (epoch {epoch})")
-            trainer.train_steps(1, tail)
+            _steps(trainer, 1, tail, events)
     return step0, early
 
 
-def _wait_epoch(trainer, group, device):
-    """Bounded wait for this replica's enqueued epoch (groups > 1 on GPU).
+def _abort(group, device):
+    try:
+        be = group._get_backend(device)
+        if hasattr(be, "abort"):
+            be.abort()
+    except Exception:  # noqa: BLE001 - best effort, we are failing anyway
+        pass
+
+
+def _wait_epoch(trainer, group, device, events, watch=None):
+    """Wait for this replica's enqueued epoch (groups > 1 on GPU).
 
     The bucket collectives run inside replayed graphs, out of sight of
     ProcessGroupNCCL's watchdog: if a peer died mid-epoch they would never
-    complete. Poll the epoch's completion event; past ``MDT_GROUP_TIMEOUT_S``
-    abort the group's communicator (RCCL kernels observe the abort flag and
-    exit) and fail the trial."""
+    complete. So: poll the epoch's progress events; meanwhile beat on the
+    trial's ``TrialWatch`` and check the peers (a published failure or a
+    silent peer ends the wait within ~0.5 s / ``MDT_HEARTBEAT_S``); and if no
+    chunk of steps completes for ``MDT_GROUP_TIMEOUT_S`` the epoch is stuck.
+    Either way abort the group's communicator (RCCL kernels observe the abort
+    flag and exit) and fail the trial."""
     if device.type != "cuda" or group is None or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
     ev = torch.cuda.Event()
     ev.record()
-    deadline = time.monotonic() + group_timeout_s()
-    while not ev.query():
-        if time.monotonic() > deadline:
+    events.append(ev)
+    stall, hb = group_timeout_s(), heartbeat_s()
+    now = time.monotonic()
+    last_progress, next_beat, done = now, now, 0
+    if watch is not None:
+        watch.reset()
+    while True:
+        while done < len(events) and events[done].query():
+            done += 1
+            last_progress = time.monotonic()
+        if done == len(events):
+            break
+        now = time.monotonic()
+        if now - last_progress > stall:
+            _abort(group, device)
+            raise TrialTimeout(f"no step of the epoch completed for {stall:.0f} s (peer lost?)")
+        if watch is not None and now >= next_beat:
+            next_beat = now + 0.5
             try:
-                be = group._get_backend(device)
-                if hasattr(be, "abort"):
-                    be.abort()
-            except Exception:  # noqa: BLE001 - best effort, we are failing anyway
-                pass
-            raise TrialTimeout(f"epoch did not complete within {group_timeout_s():.0f} s (peer lost?)")
+                watch.beat()
+                msg = watch.check(hb)
+            except Exception as e:  # noqa: BLE001 - the store (on world rank 0) is unreachable
+                msg = f"control store unreachable: {type(e).__name__}: {e}"
+            if msg:
+                _abort(group, device)
+                raise TrialTimeout(msg)
         time.sleep(0.0005)
     red = getattr(trainer, "reducer", None)
     if red is not None and hasattr(red, "status") and int(red.status()) != 0:
@@ -187,14 +237,18 @@ def _wait_epoch(trainer, group, device):
 
 
 def _train_epoch(trainer, epoch: int, n_shard: int, n_dataset: int, opts: RunOptions, group,
-                 step0: Optional[int] = None, tag: str = "", fault_at: Optional[int] = None) -> float:
+                 step0: Optional[int] = None, tag: str = "", fault_at: Optional[int] = None, watch=None) -> float:
     B = opts.batch_size
     full, tail = n_shard // B, n_shard % B
     nb = full + (1 if tail else 0)
     early = {}
     if step0 is None:
-        step0, early = _launch_epoch(trainer, epoch, n_shard, opts, fault_at)
-        _wait_epoch(trainer, group, getattr(trainer, "device", torch.device("cpu")))
+        device = getattr(trainer, "device", torch.device("cpu"))
+        multi = device.type == "cuda" and group is not None and dist.is_initialized() and \
+            dist.get_world_size(group) > 1
+        events = [] if multi else None
+        step0, early = _launch_epoch(trainer, epoch, n_shard, opts, fault_at, events)
+        _wait_epoch(trainer, group, device, events, watch)
     elif nb > LOSS_RING:
         raise ValueError(f"{nb} batches per epoch exceed the {LOSS_RING}-entry loss ring of a packed trial; "
                          f"use a larger --batch-size or --trials-per-group 1")
@@ -266,19 +320,34 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
     if opts.ckpt_dir and opts.resume:
         # only group rank 0 writes checkpoints, so only it reads one; the
         # replicas receive weights, Adam moments, the step counter and the
-        # epoch to resume from (no shared filesystem needed)
-        prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer) if grank == 0 else None
+        # epoch to resume from (no shared filesystem needed). Rank 0's load
+        # outcome goes first, so a load error (arch mismatch, corrupt file)
+        # raises on every member together instead of stranding the replicas
+        # in the parameter broadcast.
+        prog, err = None, None
+        if grank == 0:
+            try:
+                prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer)
+            except Exception as e:  # noqa: BLE001 - re-raised below on every member
+                err = e
         if prog is not None:
             start_epoch = prog["epoch"] + 1
             print0(f"resumed trial {spec.group_id} from {prog['path']} (epoch {prog['epoch']})", process_group=group)
         if gsize > 1:
-            broadcast_params([trainer.params, trainer.exp_avg, trainer.exp_avg_sq], group)
-            meta = torch.tensor([start_epoch, trainer.step_count], dtype=torch.int64,
+            meta = torch.tensor([0 if err is None else 1, start_epoch, trainer.step_count], dtype=torch.int64,
                                 device=device if dist.get_backend(group) == "nccl" else "cpu")
             broadcast_params([meta], group)
-            start_epoch = int(meta[0].item())
-            trainer.set_step(int(meta[1].item()))
+            if int(meta[0].item()) != 0:
+                if err is not None:
+                    raise err
+                raise RuntimeError(f"trial {spec.group_id}: group rank 0 could not load its checkpoint; "
+                                   f"stopping every member")
+            broadcast_params([trainer.params, trainer.exp_avg, trainer.exp_avg_sq], group)
+            start_epoch = int(meta[1].item())
+            trainer.set_step(int(meta[2].item()))
             trainer.refresh_weights()
+        elif err is not None:
+            raise err
     metrics = TrialMetrics(opts.metrics_dir, spec.group_id, enabled=(grank == 0))
 
     idx = shard_indices(len(train), n_rep, spec.group_id)
@@ -299,9 +368,13 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
     failure = {}
     epochs_done = 0
 
+    watch = trial_watch(spec.group_id) if gsize > 1 else None
+
     def _fail(e):
         failure["error"] = f"{type(e).__name__}: {e}"
         metrics.log(event="trial_failed", error=failure["error"])
+        if watch is not None:  # peers waiting on their epoch see it within ~0.5 s
+            watch.fail(failure["error"])
 
     fault_at = fault_step(trial=spec.group_id, rank=world_rank)
     checked_in = False  # this member's "not ok" has been delivered to the group
@@ -313,7 +386,7 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
                 raise RuntimeError("a replica of this trial failed; stopping the trial on every member")
             maybe_inject(trial=spec.group_id, epoch=epoch, rank=world_rank)
             train_loss, test_loss = _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape,
-                                               gen, device, spec, grank, metrics, fault_at=fault_at)
+                                               gen, device, spec, grank, metrics, fault_at=fault_at, watch=watch)
             epochs_done += 1
         if not agree_healthy(spec.group_id, True):
             checked_in = True
@@ -330,10 +403,10 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
 
 
 def _run_epoch(trainer, epoch, n_shard, train, test, opts, group, rdir, shape, gen, device, spec, grank, metrics,
-               step0=None, t_train=None, tag="", fault_at=None):
+               step0=None, t_train=None, tag="", fault_at=None, watch=None):
     te = time.perf_counter()
     train_loss = _train_epoch(trainer, epoch, n_shard, len(train), opts, group, step0=step0, tag=tag,
-                              fault_at=fault_at)
+                              fault_at=fault_at, watch=watch)
     if t_train is None:
         t_train = time.perf_counter() - te
     phases = {}
@@ -405,6 +478,11 @@ def run_packed_trials(specs, group, opts: RunOptions, data=None, num_trials: Opt
                        metrics=TrialMetrics(opts.metrics_dir, spec.group_id, enabled=True),
                        gen=torch.Generator(device="cpu").manual_seed(spec.seed * 7919 + 17),
                        done=0, train_loss=float("nan"), test_loss=float("nan"), failure={}))
+    for t in tr:  # a packed epoch is enqueued whole: its losses must fit the ring (checked before any launch)
+        nb = -(-t["n_shard"] // opts.batch_size)
+        if nb > LOSS_RING:
+            raise ValueError(f"{nb} batches per epoch exceed the {LOSS_RING}-entry loss ring of a packed trial; "
+                             f"use a larger --batch-size or --trials-per-group 1")
     global_barrier()
     t0 = time.time()
     last = max(t["spec"].epochs for t in tr)

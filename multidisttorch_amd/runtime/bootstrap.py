@@ -96,12 +96,25 @@ def bound_device() -> torch.device:
     return torch.device("cpu")
 
 
-def _bind_local_device(info: _envmod.LaunchInfo) -> torch.device:
+def _bind_local_device(info: _envmod.LaunchInfo, backend: Optional[str] = None) -> torch.device:
     if not torch.cuda.is_available():
         return torch.device("cpu")
     ndev = torch.cuda.device_count()
     # If the launcher already isolated one GPU per process (jsrun resource
     # sets, --gpus-per-task, HIP_VISIBLE_DEVICES) ndev == 1 and this is cuda:0.
+    # ndev == 1 is the launcher-isolated layout (each rank sees its own GPU as
+    # cuda:0); with several visible GPUs, more local ranks than GPUs means sharing
+    shared = ndev > 1 and ((info.local_size is not None and info.local_size > ndev) or info.local_rank >= ndev)
+    if shared and backend == "nccl":
+        # more ranks than GPUs on this node: RCCL would later abort with
+        # "Duplicate GPU detected" inside the first collective; say so now
+        raise RuntimeError(
+            f"{info.local_size if info.local_size is not None else '>' + str(info.local_rank)} ranks on this node "
+            f"but {ndev} visible GPUs: RCCL needs one process per GPU (launch at most {ndev} ranks per node, or "
+            f"use DDP_BACKEND=gloo to share GPUs)")
+    if shared:
+        print(f"[mdt] warning: local rank {info.local_rank} shares a GPU ({ndev} visible); "
+              f"cuda:{info.local_rank % max(ndev, 1)}", file=sys.stderr, flush=True)
     idx = info.local_rank % max(ndev, 1)
     torch.cuda.set_device(idx)
     return torch.device("cuda", idx)
@@ -133,7 +146,7 @@ def setup_ddp(backend: Optional[str] = None, verbose: bool = True,
         if ifname is not None:
             os.environ["GLOO_SOCKET_IFNAME"] = ifname
 
-    _STATE["device"] = _bind_local_device(info) if bind_device else bound_device()
+    _STATE["device"] = _bind_local_device(info, backend) if bind_device else bound_device()
 
     if verbose:
         print("Distributed data parallel: %s master at %s:%s" % (backend, master_addr, master_port))

@@ -29,6 +29,7 @@ __all__ = [
     "init_comm_size_and_rank",
     "local_rank_from_env",
     "parse_slurm_nodelist",
+    "parse_slurm_tasks_per_node",
     "find_ifname",
     "discover_master",
 ]
@@ -71,10 +72,35 @@ def local_rank_from_env(env: Optional[Mapping[str, str]] = None,
     return 0
 
 
+def parse_slurm_tasks_per_node(spec: str) -> list:
+    """Expand SLURM's compressed per-node task counts (``SLURM_TASKS_PER_NODE``
+    / ``SLURM_STEP_TASKS_PER_NODE``): ``"8(x2)"`` -> [8, 8], ``"4,2"`` -> [4, 2],
+    ``"2(x3),1"`` -> [2, 2, 2, 1]. Raises ValueError on anything else."""
+    out = []
+    for part in spec.strip().split(","):
+        part = part.strip()
+        if not part:
+            raise ValueError(f"bad task count list {spec!r}")
+        if part.endswith(")") and "(x" in part:
+            n, rep = part[:-1].split("(x", 1)
+            out += [int(n)] * int(rep)
+        else:
+            out.append(int(part))
+    if not out or min(out) < 1:
+        raise ValueError(f"bad task count list {spec!r}")
+    return out
+
+
 def local_size_from_env(env: Optional[Mapping[str, str]] = None) -> Optional[int]:
     """Number of ranks on this node, when the launcher says (torchrun
     ``LOCAL_WORLD_SIZE``, Open MPI ``OMPI_COMM_WORLD_LOCAL_SIZE``, MPICH
-    ``MPI_LOCALNRANKS``, SLURM ``SLURM_NTASKS_PER_NODE``); None if unknown."""
+    ``MPI_LOCALNRANKS``, SLURM ``SLURM_NTASKS_PER_NODE`` or the per-node lists
+    ``SLURM_STEP_TASKS_PER_NODE`` / ``SLURM_TASKS_PER_NODE`` indexed by
+    ``SLURM_NODEID``, e.g. ``8(x2)``); None if unknown.
+
+    A plain ``srun`` exports only the lists (the reference's primary launcher
+    path, /root/reference/utils.py:17-20), so without them the device-bound
+    RCCL world (ncclCommSplit trial groups) would never turn on under SLURM."""
     e = _env(env)
     for key in ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "SLURM_NTASKS_PER_NODE"):
         v = e.get(key)
@@ -83,6 +109,19 @@ def local_size_from_env(env: Optional[Mapping[str, str]] = None) -> Optional[int
                 return int(v)
             except ValueError:  # e.g. SLURM's "8(x2)"
                 continue
+    for key in ("SLURM_STEP_TASKS_PER_NODE", "SLURM_TASKS_PER_NODE"):
+        v = e.get(key)
+        if v in (None, ""):
+            continue
+        try:
+            counts = parse_slurm_tasks_per_node(v)
+        except ValueError:
+            continue
+        node = e.get("SLURM_NODEID")
+        if node not in (None, "") and 0 <= int(node) < len(counts):
+            return counts[int(node)]
+        if len(set(counts)) == 1:  # same count on every node: the node id does not matter
+            return counts[0]
     return None
 
 

@@ -20,6 +20,13 @@ ranks, crash or hang everyone at the global barriers, and RCCL waits for the
   happened (Python error between epochs, a replica stuck in a collective that
   timed out and aborted its communicator) all members leave the trial at the
   same check and mark it failed; nobody blocks forever in graph replay.
+* **Heartbeat** — while a replica waits for its enqueued epoch it beats on
+  the c10d store and watches its peers (``TrialWatch``): a peer that raised
+  publishes a "failed" key (seen within ~0.5 s), a peer whose process died
+  stops beating (``MDT_HEARTBEAT_S``, default 30 s); either aborts the trial's
+  communicator at once instead of after the group timeout. The stall bound
+  (``MDT_GROUP_TIMEOUT_S``) counts from the last completed chunk of steps,
+  not from the start of the epoch, so a long healthy epoch never trips it.
 * **Injection** — ``MDT_FAULT`` triggers a deterministic failure for tests and
   drills: ``MDT_FAULT="trial=1,epoch=1"`` (before the epoch starts) or
   ``"rank=3,step=5"`` (mid-epoch: the rank stops issuing steps at optimizer
@@ -36,7 +43,8 @@ from contextlib import contextmanager
 from typing import Dict, Optional
 
 __all__ = ["InjectedFault", "TrialTimeout", "maybe_inject", "fault_step", "guarded", "group_timeout_s",
-           "parse_fault", "create_health_groups", "health_group", "agree_healthy"]
+           "heartbeat_s", "parse_fault", "create_health_groups", "health_group", "trial_watch", "agree_healthy",
+           "TrialWatch"]
 
 
 class InjectedFault(RuntimeError):
@@ -48,35 +56,99 @@ class TrialTimeout(RuntimeError):
 
 
 _HEALTH: Dict[int, object] = {}
+_WATCH: Dict[int, "TrialWatch"] = {}
+_GEN = [0]
+
+
+class TrialWatch:
+    """Host-side liveness of the replicas of one trial over the c10d store:
+    ``beat()`` advances this member's counter, ``fail(msg)`` publishes a
+    failure, ``check()`` reports a published failure or a peer whose counter
+    has not moved for ``silent_s`` seconds (``reset()`` restarts those clocks,
+    e.g. when a new epoch starts)."""
+
+    def __init__(self, store, rank: int, size: int):
+        self.store, self.rank, self.size = store, rank, size
+        self.beats = 0
+        self.seen: Dict[int, tuple] = {}
+
+    def beat(self):
+        self.beats += 1
+        self.store.set(f"hb/{self.rank}", str(self.beats))
+
+    def fail(self, msg: str):
+        try:
+            self.store.set("failed", f"rank {self.rank}: {msg}")
+        except Exception:  # noqa: BLE001 - the store may be gone with rank 0
+            pass
+
+    def reset(self):
+        self.seen.clear()
+
+    def check(self, silent_s: Optional[float] = None) -> Optional[str]:
+        import time
+
+        silent_s = heartbeat_s() if silent_s is None else silent_s
+        if self.store.check(["failed"]):
+            return "a replica failed (" + self.store.get("failed").decode(errors="replace") + ")"
+        now = time.monotonic()
+        for p in range(self.size):
+            if p == self.rank:
+                continue
+            key = f"hb/{p}"
+            v = self.store.get(key) if self.store.check([key]) else b""
+            old = self.seen.get(p)
+            if old is None or old[0] != v:
+                self.seen[p] = (v, now)
+            elif now - old[1] > silent_s:
+                return f"replica {p} of the trial sent no heartbeat for {now - old[1]:.0f} s (process lost?)"
+        return None
 
 
 def create_health_groups(num_groups: int, world_size: Optional[int] = None):
-    """World collective: one gloo group per trial group for health agreement.
+    """One gloo group per multi-rank trial for health agreement, plus its
+    ``TrialWatch``. Call on every rank (it is NOT a world collective).
 
-    Call on every rank, in the same order relative to other ``new_group``
-    calls (right after ``setup_ddp_groups`` / ``control_group``). Members keep
-    their own group's handle; ``health_group(g)`` returns it.
+    Built without ``dist.new_group``: on a device-bound RCCL world torch makes
+    every NON-member of a new group take part in a ``ncclCommSplit(NOCOLOR)``
+    of the world communicator -- for gloo groups too -- while the gloo group's
+    members make no split call, so an idle leftover rank (W % K != 0) would
+    issue one split more than the trial members and hang in it.
+    Here each member connects a ``ProcessGroupGloo`` of its own trial straight
+    through the default store (keys under a per-call prefix, the same
+    constructor ``new_group`` uses); non-members and idle ranks do nothing.
+    ``health_group(g)`` / ``trial_watch(g)`` return this member's handles.
     """
     import torch.distributed as dist
 
     from ..parallel.groups import GroupPlan
     from .bootstrap import _stdout_to_stderr
 
+    _HEALTH.clear()
+    _WATCH.clear()
     if not dist.is_initialized():
         return
+    _GEN[0] += 1
     W = world_size or dist.get_world_size()
     plan = GroupPlan(W, num_groups)
     me = dist.get_rank()
-    _HEALTH.clear()
+    g = plan.group_of(me)
+    if g is None or plan.ranks_per_group == 1:
+        return
+    ranks = plan.ranks(g)
+    store = dist.PrefixStore(f"mdt_health/{_GEN[0]}/{g}/", dist.distributed_c10d._get_default_store())
     with _stdout_to_stderr():  # gloo connect banners stay off stdout
-        for g in range(num_groups):
-            pg = dist.new_group(ranks=plan.ranks(g), backend="gloo", timeout=_dt.timedelta(hours=6))
-            if me in plan.ranks(g):
-                _HEALTH[g] = pg
+        _HEALTH[g] = dist.ProcessGroupGloo(dist.PrefixStore("pg/", store), me - ranks[0], len(ranks),
+                                           _dt.timedelta(hours=6))
+    _WATCH[g] = TrialWatch(dist.PrefixStore("watch/", store), me - ranks[0], len(ranks))
 
 
 def health_group(group_id: int):
     return _HEALTH.get(group_id)
+
+
+def trial_watch(group_id: int) -> Optional[TrialWatch]:
+    return _WATCH.get(group_id)
 
 
 def agree_healthy(group_id: int, ok: bool) -> bool:
@@ -88,10 +160,12 @@ def agree_healthy(group_id: int, ok: bool) -> bool:
     import torch
     import torch.distributed as dist
 
-    if dist.get_world_size(pg) == 1:
+    if pg.size() == 1:
         return ok
     t = torch.tensor([1 if ok else 0], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=pg)
+    opts = dist.AllreduceOptions()
+    opts.reduceOp = dist.ReduceOp.MIN
+    pg.allreduce([t], opts).wait()
     return bool(t.item())
 
 
@@ -133,6 +207,10 @@ def maybe_inject(**where):
 
 def group_timeout_s() -> float:
     return float(os.getenv("MDT_GROUP_TIMEOUT_S", "600"))
+
+
+def heartbeat_s() -> float:
+    return float(os.getenv("MDT_HEARTBEAT_S", "30"))
 
 
 @contextmanager

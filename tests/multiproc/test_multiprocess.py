@@ -278,3 +278,39 @@ def test_failure_inside_multi_rank_group(tmp_path):
     assert re.search(r"^\[0:0\] ====> Test set loss", text, re.M)
     agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
     assert agg["failed_trials"] == [1] and agg["trials"] == 2
+
+
+def test_health_groups_idle_rank_and_watch():
+    """W=5, K=2 (rank 4 idle): health groups come up without any world-
+    collective new_group (on a device-bound RCCL world that path made an idle
+    rank issue one ncclCommSplit more than the members: ADVICE r2), members
+    agree, and the store heartbeat reports a published failure and a silent
+    peer."""
+    rc, outs = _run([WORKER, "health", "2"], 5, "torchrun", timeout=120)
+    text = "\n".join(o or "" for o in outs)
+    assert rc == 0, text
+    res = {r["rank"]: r for r in _results(outs)}
+    assert sorted(res) == [0, 1, 2, 3, 4], text
+    assert res[4]["group"] is None and not res[4]["has_pg"]
+    for r in range(4):
+        assert res[r]["has_pg"] and res[r]["agree_all_ok"] is True and res[r]["agree_one_bad"] is False
+    for r in (0, 2):
+        assert "rank 1: boom" in res[r]["failure_seen"], res[r]
+        assert "sent no heartbeat" in res[r]["silence_seen"] and res[r]["silence_after_s"] < 5, res[r]
+
+
+def test_resume_arch_mismatch_fails_every_member_together(tmp_path):
+    """A 2-rank trial resuming from a checkpoint of another architecture: only
+    group rank 0 reads it, and its load error reaches the replica before the
+    parameter broadcast, so BOTH members raise (the replica used to
+    wait in the broadcast until the collective timeout)."""
+    rc, outs = _vae_hpo(tmp_path, 2, "--epochs", "1", "--ngroups", "1", "--ckpt-dir", "ck", "--no-results")
+    assert rc == 0, "\n".join(outs)
+    t0 = __import__("time").monotonic()
+    rc, outs = _vae_hpo(tmp_path, 2, "--model", "conv", "--epochs", "2", "--ngroups", "1", "--ckpt-dir", "ck",
+                        "--resume", "--no-results")
+    took = __import__("time").monotonic() - t0
+    text = "\n".join(o or "" for o in outs)
+    assert rc != 0, text
+    assert "could not load its checkpoint" in text, text[-3000:]
+    assert took < 120, took

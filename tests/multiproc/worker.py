@@ -154,6 +154,70 @@ def mode_autotune():
     dist.destroy_process_group()
 
 
+def mode_health(k):
+    """Health groups + trial watch on W ranks, K groups (leftover ranks idle):
+    built without any further ``dist.new_group`` (patched to raise), agreement
+    over each trial, a published failure and a silent peer are detected."""
+    import time
+
+    from multidisttorch_amd.runtime import faults
+    from multidisttorch_amd.runtime.bootstrap import global_barrier, setup_ddp
+    from multidisttorch_amd.parallel.groups import GroupPlan, setup_ddp_groups
+
+    ws, wr = setup_ddp(verbose=False)
+    setup_ddp_groups(k, verbose=False)
+    global_barrier()
+
+    def _no_new_group(*a, **kw):
+        raise AssertionError("create_health_groups must not call dist.new_group")
+
+    real = dist.new_group
+    dist.new_group = _no_new_group
+    try:
+        faults.create_health_groups(k)
+    finally:
+        dist.new_group = real
+    plan = GroupPlan(ws, k)
+    g = plan.group_of(wr)
+    res = dict(rank=wr, group=g, has_pg=faults.health_group(g) is not None if g is not None else False)
+    if g is not None and plan.ranks_per_group > 1:
+        grank = wr - plan.ranks(g)[0]
+        res["agree_all_ok"] = faults.agree_healthy(g, True)
+        res["agree_one_bad"] = faults.agree_healthy(g, grank != 1)
+        w = faults.trial_watch(g)
+        w.reset()
+        if grank == 0:
+            # peers beat for 1 s, then rank 1 publishes a failure
+            t0 = time.monotonic()
+            msg = None
+            while msg is None and time.monotonic() - t0 < 20:
+                w.beat()
+                msg = w.check(60.0)
+                time.sleep(0.05)
+            res["failure_seen"] = msg
+        else:
+            for _ in range(20):
+                w.beat()
+                time.sleep(0.05)
+            if grank == 1:
+                w.fail("boom")
+        faults.agree_healthy(g, True)  # resync before the silence check
+        if grank == 0:
+            # now nobody else beats: a 0.5 s heartbeat bound flags a silent peer
+            w2 = faults.TrialWatch(w.store, 0, w.size)
+            w2.store.delete_key("failed")
+            t0 = time.monotonic()
+            msg = None
+            while msg is None and time.monotonic() - t0 < 20:
+                msg = w2.check(0.5)
+                time.sleep(0.05)
+            res["silence_seen"] = msg
+            res["silence_after_s"] = round(time.monotonic() - t0, 2)
+    global_barrier()
+    out(**res)
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
     mode = sys.argv[1]
     if mode == "groups":
@@ -166,5 +230,7 @@ if __name__ == "__main__":
         mode_trainer_ddp()
     elif mode == "autotune":
         mode_autotune()
+    elif mode == "health":
+        mode_health(int(sys.argv[2]))
     else:
         raise SystemExit(f"unknown mode {mode}")

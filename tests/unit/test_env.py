@@ -78,3 +78,63 @@ def test_eager_device_bound_world_default(monkeypatch):
     assert not eager_comm_requested(info, 8)
     monkeypatch.setenv("MDT_EAGER_COMM", "1")
     assert eager_comm_requested(info2, 8)
+
+
+def test_slurm_tasks_per_node_forms():
+    """SLURM's compressed per-node task lists (srun exports no LOCAL_WORLD_SIZE)."""
+    from multidisttorch_amd.runtime import env as E
+
+    assert E.parse_slurm_tasks_per_node("8(x2)") == [8, 8]
+    assert E.parse_slurm_tasks_per_node("4,2") == [4, 2]
+    assert E.parse_slurm_tasks_per_node("2(x3),1") == [2, 2, 2, 1]
+    for bad in ("", "x", "0", "2(x0)"):
+        with pytest.raises(ValueError):
+            E.parse_slurm_tasks_per_node(bad)
+    base = {"SLURM_NPROCS": "10", "SLURM_PROCID": "9", "SLURM_LOCALID": "1"}
+    assert E.local_size_from_env(dict(base, SLURM_TASKS_PER_NODE="8(x2)")) == 8
+    assert E.local_size_from_env(dict(base, SLURM_TASKS_PER_NODE="8,2", SLURM_NODEID="1")) == 2
+    assert E.local_size_from_env(dict(base, SLURM_TASKS_PER_NODE="8,2")) is None  # which node? unknown
+    # the step's own list wins over the allocation's
+    assert E.local_size_from_env(dict(base, SLURM_TASKS_PER_NODE="8(x2)", SLURM_STEP_TASKS_PER_NODE="4(x2)")) == 4
+    assert E.local_size_from_env(dict(base, SLURM_NTASKS_PER_NODE="2", SLURM_TASKS_PER_NODE="8(x2)")) == 2
+
+
+def test_eager_split_chosen_under_emulated_srun(monkeypatch):
+    """A plain ``srun -N2 --ntasks-per-node 8`` environment (no LOCAL_WORLD_SIZE,
+    only SLURM's lists) on 8-GPU nodes selects the eager device-bound world."""
+    from multidisttorch_amd.runtime import env as E
+    from multidisttorch_amd.runtime.bootstrap import eager_comm_requested
+
+    monkeypatch.delenv("MDT_EAGER_COMM", raising=False)
+    srun = {"SLURM_NPROCS": "16", "SLURM_PROCID": "11", "SLURM_LOCALID": "3", "SLURM_NODEID": "1",
+            "SLURM_NODELIST": "node[01-02]", "SLURM_TASKS_PER_NODE": "8(x2)", "SLURM_STEP_TASKS_PER_NODE": "8(x2)"}
+    info = E.discover(srun, ndev=8)
+    assert info.launcher == "slurm" and info.local_rank == 3 and info.local_size == 8
+    assert eager_comm_requested(info, 8)
+    # 16 tasks crammed on one 8-GPU node: lazy path (and setup_ddp refuses RCCL)
+    info2 = E.discover(dict(srun, SLURM_TASKS_PER_NODE="16", SLURM_STEP_TASKS_PER_NODE="16", SLURM_NODEID="0"), ndev=8)
+    assert info2.local_size == 16 and not eager_comm_requested(info2, 8)
+
+
+def test_bind_refuses_more_rccl_ranks_than_gpus(monkeypatch):
+    """_bind_local_device fails loudly instead of wrapping local ranks onto
+    shared GPUs when the backend is RCCL (it would die later with 'Duplicate
+    GPU detected'); gloo may share (with a warning)."""
+    import torch
+
+    from multidisttorch_amd.runtime import bootstrap as B
+    from multidisttorch_amd.runtime import env as E
+
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda i: None)
+    info = E.discover({"WORLD_SIZE": "9", "RANK": "8", "LOCAL_RANK": "8", "LOCAL_WORLD_SIZE": "9"}, ndev=8)
+    with pytest.raises(RuntimeError, match="one process per GPU"):
+        B._bind_local_device(info, "nccl")
+    assert B._bind_local_device(info, "gloo") == torch.device("cuda", 0)
+    ok = E.discover({"WORLD_SIZE": "8", "RANK": "7", "LOCAL_RANK": "7", "LOCAL_WORLD_SIZE": "8"}, ndev=8)
+    assert B._bind_local_device(ok, "nccl") == torch.device("cuda", 7)
+    # launcher-isolated: one visible GPU per process, any local size
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    iso = E.discover({"WORLD_SIZE": "8", "RANK": "5", "LOCAL_RANK": "5", "LOCAL_WORLD_SIZE": "8"}, ndev=1)
+    assert B._bind_local_device(iso, "nccl") == torch.device("cuda", 0)
