@@ -346,6 +346,7 @@ struct FwdLayout {
 // phase waits on a global bias load (vmcnt is in order: such a load also
 // waits for every store the wave issued before it)
 constexpr int kB1 = 0, kB2 = 32, kBh = 96, kB3 = 160, kB4 = 192, kNBias = 193;
+constexpr int kZero = 252;  // f32 index of a 16-B zero chunk (the paired body's out-of-image gathers read it)
 
 // P0 + P1 of the forward (the part a paired workgroup runs in full before it
 // knows whether its partner arrived, conv28_pair.h). n = sample; after_p0()
@@ -400,6 +401,8 @@ __device__ __forceinline__ void fwd_p01(const FwdArgs& a, uint8_t* lds, int n, A
       float* bs = reinterpret_cast<float*>(lds + L::Bias);
       bs[tid] = tid < kB2 ? W.b1[tid] : tid < kBh ? W.b2[tid - kB2] : tid < kB3 ? W.bh[tid - kBh]
               : tid < kB4 ? W.b3[tid - kB3] : W.b4[0];
+    } else if (tid >= kZero && tid < kZero + 4) {
+      reinterpret_cast<float*>(lds + L::Bias)[tid] = 0.f;
     }
   }
   stage_conv_image(W.W2, W3s);  // enc2 weights first; dec1's tap images replace them after P2
@@ -987,8 +990,9 @@ struct StepLayout {
   static constexpr int CSB = Bd + kFlat * 4;     // f32 [32][197]
   static constexpr int D1 = CSB + 32 * 197 * 4;  // bf16 [196][32] dec1 out (P7 input, Q1 mask)
   static constexpr int GA2F = D1;                //   bwd f32 [3136] (D1 dead after Q1)
-  static constexpr int Bias = D1 + kFlat * 4;   // f32 [256] small biases
-  static constexpr int LDS = Bias + 1024;
+  static constexpr int Bias = D1 + kFlat * 4;   // f32 [256] small biases (+ a zero chunk at kZero)
+  static constexpr int PTab = Bias + 1024;      // u64 [32] pointer table of the paired body (conv28_pair.h)
+  static constexpr int LDS = PTab + 256;
   static_assert(W1 % 16 == 0 && X % 16 == 0 && G % 16 == 0 && A1 % 16 == 0 && A2 % 16 == 0 && D0 % 16 == 0 &&
                     Dummy % 16 == 0 && Bd % 16 == 0 && CSB % 16 == 0 && D1 % 16 == 0 && LDS <= 163840,
                 "step LDS map");

@@ -41,6 +41,7 @@ __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, P
     while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * (unsigned)pc.delay_us) __builtin_amdgcn_s_sleep(8);
   }
   if (threadIdx.x == 0) ticket = __hip_atomic_fetch_add(word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  fill_ptab<StepLayout>(lds, fa, ba, pc, n);  // read by the paired body after P0's barrier
   fwd_p01<StepLayout>(fa, lds, n, [&] {
     if (threadIdx.x == 0 && ticket == 0)
       __hip_atomic_compare_exchange_strong(word, &seen, 3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
@@ -70,7 +71,7 @@ __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, P
     bwd_body<StepLayout, true>(ba, lds, n);
     return;
   }
-  pair_rest<StepLayout>(fa, ba, lds, n, mode == kModeRole1 ? 1 : 0, pc);
+  pair_rest<StepLayout>(lds, n, mode == kModeRole1 ? 1 : 0);
 }
 
 }  // namespace f28

@@ -56,14 +56,21 @@ struct PairCtl {
 // granule offsets inside one (sample, role) slab
 constexpr int kX1 = 0, kX2 = 72, kX3 = kX2 + 800, kX4 = kX3 + 784, kX5 = kX4 + 1568, kX6 = kX5 + 32;
 constexpr int kXW = kX6 + 800;
-#ifdef MDT_F28_NOSTORE  // timing experiment only: no global stores of the backward's inputs
-constexpr bool kGS = false;
-#else
-constexpr bool kGS = true;
-#endif
 constexpr unsigned long long kSpinTicks = 25000000ull;  // 0.25 s of s_memrealtime (100 MHz)
 
 enum : int { kModeSolo = 0, kModeRole0 = 1, kModeRole1 = 2, kModeExit = 3 };
+
+// Pointer table in LDS (StepLayout::PTab): the paired body takes every buffer
+// pointer from here, already offset to its sample, instead of from the kernel
+// arguments. Kept as arguments, the ~60 pointers of FwdArgs + BwdArgs did not
+// fit the 102 SGPRs: the compiler spilled them to VGPR lanes and reloaded a
+// 16-SGPR block (16 v_readlane) around every global store of an epilogue. A
+// table read costs one ds_read_b64 + two readfirstlane per pointer per phase.
+enum : int {
+  kTWh, kTWd, kTW3, kTW2, kTSt, kTHp, kTA2, kTMulv, kTEps, kTZ16, kTD0, kTD1, kTDlog, kTRecon, kTBce, kTKld,
+  kTDb4, kTStamp, kTGd1, kTDb3, kTGd0, kTDbd, kTDmulv, kTDmulv16, kTGa2, kTDb2, kTGa1, kTDb1, kTXg, kTErr,
+  kTInts, kTNum  // kTInts: M | stream << 16 ... packed below
+};
 
 using g64 = __attribute__((address_space(1))) unsigned long long;
 using g32i = __attribute__((address_space(1))) int;
@@ -125,32 +132,97 @@ __device__ __forceinline__ void xget(unsigned long long* base, const int (&gi)[N
     }
 }
 
+template <class L, class T>
+__device__ __forceinline__ T* tab(const uint8_t* lds, int i) {
+  const unsigned long long v = reinterpret_cast<const unsigned long long*>(lds + L::PTab)[i];
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  // through a global-address-space pointer, so the accesses stay global_* (a
+  // generic pointer would make them flat_*, which also count in lgkmcnt and
+  // so hold every later LDS wait until the global access completes)
+  auto* g = (__attribute__((address_space(1))) T*)(((unsigned long long)hi << 32) | lo);
+  return (T*)g;
+}
+
+// Thread 0 writes the table for sample n (visible after P0's barrier).
+template <class L>
+__device__ __forceinline__ void fill_ptab(uint8_t* lds, const FwdArgs& a, const BwdArgs& b, const PairCtl& pc, int n) {
+  if (threadIdx.x != 0) return;
+  unsigned long long* t = reinterpret_cast<unsigned long long*>(lds + L::PTab);
+  auto at = [](const void* p, size_t bytes) {
+    return p ? (unsigned long long)(reinterpret_cast<const char*>(p) + bytes) : 0ull;
+  };
+  const size_t N = (size_t)n;
+  t[kTWh] = at(a.w.Wh, 0);
+  t[kTWd] = at(a.w.Wd, 0);
+  t[kTW3] = at(a.w.W3, 0);
+  t[kTW2] = at(a.w.W2, 0);
+  t[kTSt] = at(a.st, 0);
+  t[kTHp] = at(a.hp, 0);
+  t[kTA2] = at(a.a2, N * kFlat * 2);
+  t[kTMulv] = at(a.mulv, N * 64 * 4);
+  t[kTEps] = at(a.eps, N * 32 * 4);
+  t[kTZ16] = at(a.z16, N * 32 * 2);
+  t[kTD0] = at(a.d0, N * kFlat * 2);
+  t[kTD1] = at(a.d1, N * 6272 * 2);
+  t[kTDlog] = at(a.dlog, N * 784 * 4);
+  t[kTRecon] = at(a.recon, N * 784 * 4);
+  t[kTBce] = at(a.bce_part, N * 4);
+  t[kTKld] = at(a.kld_part, N * 4);
+  t[kTDb4] = at(a.db4_part, N * 4);
+  t[kTStamp] = at(a.stamps, (size_t)blockIdx.x * 16 * 8);
+  t[kTGd1] = at(b.gd1, N * 6272 * 2);
+  t[kTDb3] = at(b.db3_part, N * 32 * 4);
+  t[kTGd0] = at(b.gd0, N * kFlat * 2);
+  t[kTDbd] = at(b.dbd_part, N * kFlat * 4);
+  t[kTDmulv] = at(b.dmulv, N * 64 * 4);
+  t[kTDmulv16] = at(b.dmulv16, N * 64 * 2);
+  t[kTGa2] = at(b.ga2, N * kFlat * 2);
+  t[kTDb2] = at(b.db2_part, N * 64 * 4);
+  t[kTGa1] = at(b.ga1, N * 6272 * 2);
+  t[kTDb1] = at(b.db1_part, N * 32 * 4);
+  t[kTXg] = at(pc.xg, N * 2 * kXW * 8);
+  t[kTErr] = at(pc.err, 0);
+  t[kTInts] = (unsigned long long)(pc.M & 0xffff) | ((unsigned long long)(a.train ? 1 : 0) << 16) |
+              ((unsigned long long)a.stream << 32);
+}
+
 __device__ __forceinline__ uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
 __device__ __forceinline__ float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
 __device__ __forceinline__ uint32_t bf16bits(__bf16 h) { return (uint32_t)__builtin_bit_cast(uint16_t, h); }
 
 // conv14to7 restricted to output pixels [p0, p1) (<= 32 of them): 2 m-tiles
 // x 4 n-tiles, one item per wave.
+// Out-of-image taps read the 16-B zero chunk `zero` (a select, not a branch
+// around the load), and all 16 A and B fragments are read before the first
+// MFMA: the gathers are issued back to back and only the MFMA chain waits.
 template <class BFrag, class Pre, class Epi>
-__device__ __forceinline__ void conv14to7_rows(const uint8_t* in_img, int p0, int p1, BFrag bfrag, Pre pre, Epi epi) {
+__device__ __forceinline__ void conv14to7_rows(const uint8_t* in_img, const uint8_t* zero, int p0, int p1,
+                                               BFrag bfrag, Pre pre, Epi epi) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = w & 3, mt = w >> 2;
   float pv[4];
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int p = p0 + mt * 16 + 4 * (lane >> 4) + rr;
-    pv[rr] = p < p1 ? pre(p, 16 * j + (lane & 15)) : 0.f;
+    pv[rr] = pre(p < p1 ? p : p1 - 1, 16 * j + (lane & 15));
   }
-  const int r = p0 + mt * 16 + (lane & 15);
-  const int oy = r / 7, ox = r - 7 * (r / 7);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int r0 = p0 + mt * 16 + (lane & 15);
+  const int r = r0 < 49 ? r0 : 48;  // padding rows (>= p1) compute garbage that is never stored
+  const int oy = r / 7, ox = r - 7 * (r / 7), ch = lane >> 4;
+  const uint32_t zoff = (uint32_t)(zero - in_img);
+  bf16x8 av[16], bv[16];
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
     const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
-    const bool ok = r < p1 && (unsigned)iy < 14u && (unsigned)ix < 14u;
-    const bf16x8 a = ok ? *reinterpret_cast<const bf16x8*>(in_img + img14(iy * 14 + ix, lane >> 4)) : zero8();
-    acc = mfma_bf16(a, bfrag(j, t), acc);
+    const bool ok = (unsigned)iy < 14u && (unsigned)ix < 14u;
+    const int pix = ok ? iy * 14 + ix : 0;
+    const uint32_t off = ok ? (uint32_t)img14(pix, ch) : zoff;
+    av[t] = *reinterpret_cast<const bf16x8*>(in_img + off);
+    bv[t] = bfrag(j, t);
   }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc = mfma_bf16(av[t], bv[t], acc);
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int p = p0 + mt * 16 + 4 * (lane >> 4) + rr;
@@ -163,7 +235,8 @@ __device__ __forceinline__ void conv14to7_rows(const uint8_t* in_img, int p0, in
 // w & 3). Returns this lane's column (16 nj + (lane & 15)) sum of epi's values
 // over the wave's items.
 template <class Pre, class Epi>
-__device__ __forceinline__ float tconv7to14_half(const uint8_t* in, const uint8_t* wimg, int nj, Pre pre, Epi epi) {
+__device__ __forceinline__ float tconv7to14_half(const uint8_t* in, const uint8_t* zero, const uint8_t* wimg, int nj,
+                                                 Pre pre, Epi epi) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int mt = w & 3;
   float pv[2][4];
@@ -173,28 +246,34 @@ __device__ __forceinline__ float tconv7to14_half(const uint8_t* in, const uint8_
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int r2 = mt * 16 + 4 * (lane >> 4) + rr;
-      const int jy2 = r2 / 7, jx2 = r2 - 7 * (r2 / 7);
-      pv[i][rr] = r2 < 49 ? pre((2 * jy2 + (q >> 1)) * 14 + 2 * jx2 + (q & 1), 16 * nj + (lane & 15)) : 0.f;
+      const int rc = r2 < 49 ? r2 : 48;
+      const int jy2 = rc / 7, jx2 = rc - 7 * (rc / 7);
+      pv[i][rr] = pre((2 * jy2 + (q >> 1)) * 14 + 2 * jx2 + (q & 1), 16 * nj + (lane & 15));
     }
   }
+  const uint32_t zoff = (uint32_t)(zero - in);
+  const int r0 = mt * 16 + (lane & 15);
+  const int r = r0 < 49 ? r0 : 48;  // rows >= 49: garbage, never stored
+  const int jy = r / 7, jx = r - 7 * (r / 7);
   float cs = 0.f;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = (w >> 2) + 2 * i;
     const int a = q >> 1, b = q & 1;
-    const int r = mt * 16 + (lane & 15);
-    const int jy = r / 7, jx = r - 7 * (r / 7);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    bf16x8 av[8], bv[8];
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
+    for (int ks = 0; ks < 8; ++ks) {  // every fragment of the item first, then the MFMA chain
       const int ty = ks >> 2, tx = (ks >> 1) & 1, hh = ks & 1;
       const int iy = jy + a - ty, ix = jx + b - tx;
-      const bool ok = r < 49 && (unsigned)iy < 7u && (unsigned)ix < 7u;
-      const bf16x8 av = ok ? *reinterpret_cast<const bf16x8*>(in + img49(iy * 7 + ix, 4 * hh + (lane >> 4))) : zero8();
+      const bool ok = (unsigned)iy < 7u && (unsigned)ix < 7u;
+      const uint32_t off = ok ? (uint32_t)img49(iy * 7 + ix, 4 * hh + (lane >> 4)) : zoff;
+      av[ks] = *reinterpret_cast<const bf16x8*>(in + off);
       const int tap = ((1 - a) + 2 * ty) * 4 + (1 - b) + 2 * tx;
-      const bf16x8 bv = tr_frag<32>(wimg + tap * 4096, 16 * nj, 32 * hh, lane);
-      acc = mfma_bf16(av, bv, acc);
+      bv[ks] = tr_frag<32>(wimg + tap * 4096, 16 * nj, 32 * hh, lane);
     }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) acc = mfma_bf16(av[ks], bv[ks], acc);
     float s = 0.f;
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
@@ -214,8 +293,7 @@ __device__ __forceinline__ float tconv7to14_half(const uint8_t* in, const uint8_
 // P2 .. Q6 of one sample, role r (0/1) of its pair. LDS map: StepLayout (the
 // solo merged step's), every region used for the same thing.
 template <class L>
-__device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, uint8_t* lds, int n, int r,
-                                          const PairCtl& pc) {
+__device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
   float* Xs = reinterpret_cast<float*>(lds + L::X);
   float* W4s = reinterpret_cast<float*>(lds + L::W4);
   uint8_t* A1s = lds + L::A1;
@@ -240,21 +318,32 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const Weights& W = a.w;
-  const int M = pc.M;
+  auto TB = [&](int i) { return tab<L, __bf16>(lds, i); };
+  auto TF = [&](int i) { return tab<L, float>(lds, i); };
+  const unsigned long long ints = reinterpret_cast<const unsigned long long*>(lds + L::PTab)[kTInts];
+  const int M = __builtin_amdgcn_readfirstlane((int)(ints & 0xffff));
+  const bool train = ((ints >> 16) & 1) != 0;
+  const uint32_t stream = __builtin_amdgcn_readfirstlane((uint32_t)(ints >> 32));
+  auto pstamp = [&](int k) {
+    if (tid == 0) {
+      unsigned long long* st = tab<L, unsigned long long>(lds, kTStamp);
+      if (st) st[k] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
   const int p0 = r ? 24 : 0, p1 = r ? 49 : 24;  // own pixels of the 7x7 maps
   const int q0 = r ? 0 : 24, q1 = r ? 24 : 49;  // the partner's
   const int k0 = 64 * p0, klen = 64 * (p1 - p0);
-  const uint32_t tg = (uint32_t)a.st->step * 8u;  // tags tg + 1 .. tg + 6 (never 0: +1)
-  unsigned long long* xo = pc.xg + ((size_t)n * 2 + r) * kXW;        // own slab (written)
-  unsigned long long* xi = pc.xg + ((size_t)n * 2 + (r ^ 1)) * kXW;  // partner's (read, cleared)
-  const bool train = a.train != 0;
+  const uint32_t tg = (uint32_t)tab<L, const TrainState>(lds, kTSt)->step * 8u;  // tags tg+1 .. tg+6 (never 0)
+  unsigned long long* xo = tab<L, unsigned long long>(lds, kTXg) + r * kXW;        // own slab (written)
+  unsigned long long* xi = tab<L, unsigned long long>(lds, kTXg) + (r ^ 1) * kXW;  // partner's (read, cleared)
+  unsigned* err = tab<L, unsigned>(lds, kTErr);
   const float* Bias = reinterpret_cast<const float*>(lds + L::Bias);
+  const uint8_t* Zero = lds + L::Bias + 4 * kZero;
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
   if (tid == 0) xput(xo + kX1 + 64, tg + 1, xcc, false);  // X1 also carries this XCD's id
 
-  stamp(a.stamps, 2);
+  pstamp(2);
   // P3's first two own-K weight rows per wave, in flight under P2
   auto ld_rows = [&](int c2, bf16x8 (&v)[8]) {
 #pragma unroll
@@ -262,23 +351,24 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int o = w + 16 * c2 + 8 * h, k = 512 * i + 8 * lane;
-        v[4 * h + i] = k < klen ? *reinterpret_cast<const bf16x8*>(W.Wh + (size_t)o * kFlat + k0 + k) : zero8();
+        v[4 * h + i] = k < klen ? *reinterpret_cast<const bf16x8*>(TB(kTWh) + (size_t)o * kFlat + k0 + k) : zero8();
       }
   };
   bf16x8 wh0[8];
   ld_rows(0, wh0);
   // ---- P2: enc2 on own pixels, ReLU
-  conv14to7_rows(A1s, p0, p1, [&](int j, int t) { return conv_bfrag(IMG, j, t, lane); },
+  __bf16* const a2p = TB(kTA2);  // table reads hoisted above the epilogue's LDS stores (which may alias them)
+  conv14to7_rows(A1s, Zero, p0, p1, [&](int j, int t) { return conv_bfrag(IMG, j, t, lane); },
                  [&](int, int col) { return Bias[kB2 + col]; }, [&](int p, int col, float v, float bias) {
     const __bf16 o = (__bf16)fmaxf(v + bias, 0.f);
     A2s[p * 64 + col] = o;
-    if (kGS && train) a.a2[(size_t)n * kFlat + p * 64 + col] = o;
+    if (train) a2p[p * 64 + col] = o;
   });
   lds_barrier();
 
   TapImageRegs w3r;
-  w3r.load(W.W3);  // dec1 tap images: in flight during P3-P5
-  stamp(a.stamps, 3);
+  w3r.load(TB(kTW3));  // dec1 tap images: in flight during P3-P5
+  pstamp(3);
   // ---- P3: head partial sums over own K (= own pixels). Wave w: rows
   // w + 16 c2 and w + 16 c2 + 8 per step c2 (two rows of loads per step, the
   // next step's in flight: the row loop is L2-latency bound, not bandwidth)
@@ -331,7 +421,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
   }
   // P5's first dec_fc weight loads (own n-tiles t = 4 p0 + w + 8 i), in flight across P4
   const int t0 = 4 * p0, t1 = 4 * p1;
-  const __bf16* wp5 = W.Wd + (size_t)(lane & 15) * 32 + 8 * (lane >> 4);
+  const __bf16* wp5 = TB(kTWd) + (size_t)(lane & 15) * 32 + 8 * (lane >> 4);
   auto wd5_ld = [&](int i) {
     const int t = t0 + w + 8 * i;
     return *reinterpret_cast<const bf16x8*>(wp5 + (size_t)(t < t1 ? t : t0) * 512);
@@ -341,7 +431,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
   for (int i = 0; i < 13; ++i) wd5[i] = wd5_ld(i);
   lds_barrier();
 
-  stamp(a.stamps, 4);
+  pstamp(4);
   // ---- X1 + P4: mu | logvar = (role-0 part + role-1 part) + bias; reparam + KLD (both halves)
   if (tid < 64) {
     float kl = 0.f;
@@ -349,33 +439,33 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
       const int c = tid;
       const int gi[2] = {kX1 + c, kX1 + 32 + c};
       uint32_t pv[2];
-      xget<2>(xi, gi, tg + 1, pv, pc.err, false);
+      xget<2>(xi, gi, tg + 1, pv, err, false);
       const float m0 = Hs[c], l0 = Hs[32 + c], mp = bitsf(pv[0]), lp = bitsf(pv[1]);
       const float mu = (r ? mp + m0 : m0 + mp) + Bias[kBh + c];
       const float lv = (r ? lp + l0 : l0 + lp) + Bias[kBh + 32 + c];
       Hs[c] = mu;
       Hs[32 + c] = lv;
-      const unsigned long long stp = (unsigned long long)a.st->step;
-      const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(n * 32 + c), a.stream, (uint32_t)(stp & 0xffffffffu),
+      const unsigned long long stp = (unsigned long long)tab<L, const TrainState>(lds, kTSt)->step;
+      const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(n * 32 + c), stream, (uint32_t)(stp & 0xffffffffu),
                                              (uint32_t)(stp >> 32)},
-                                       a.hp->seed_lo, a.hp->seed_hi);
+                                       tab<L, const HParams>(lds, kTHp)->seed_lo, tab<L, const HParams>(lds, kTHp)->seed_hi);
       const float ep = normal_from_bits(bits.x, bits.y);
       const float sd = expf(0.5f * lv);
       const float zz = mu + ep * sd;
       kl = 1.f + lv - mu * mu - sd * sd;
       Zs[c] = (__bf16)zz;
       Eps[c] = ep;
-      if (kGS && train && r == 0) {
-        if (kGS) a.mulv[(size_t)n * 64 + c] = mu;
-        if (kGS) a.mulv[(size_t)n * 64 + 32 + c] = lv;
-        if (kGS) a.eps[(size_t)n * 32 + c] = ep;
-        if (kGS) a.z16[(size_t)n * 32 + c] = (__bf16)zz;
+      if (train && r == 0) {
+        TF(kTMulv)[c] = mu;
+        TF(kTMulv)[32 + c] = lv;
+        TF(kTEps)[c] = ep;
+        TB(kTZ16)[c] = (__bf16)zz;
       }
     }
     if (tid == 32) {
       const int gi[1] = {kX1 + 64};
       uint32_t pv[1];
-      xget<1>(xi, gi, tg + 1, pv, pc.err, false);
+      xget<1>(xi, gi, tg + 1, pv, err, false);
       reinterpret_cast<int*>(Scr)[30] = pv[0] == xcc;
     }
     kl = wave_sum(kl);
@@ -383,11 +473,15 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
   }
   lds_barrier();
   const bool near = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(Scr)[30]) != 0;
-  if (a.stamps && tid == 0) a.stamps[blockIdx.x * 16 + 15] |= (unsigned long long)near << 4;  // mode | near << 4
+  if (tid == 0) {  // slot 15: mode | near << 4
+    unsigned long long* st = tab<L, unsigned long long>(lds, kTStamp);
+    if (st) st[15] |= (unsigned long long)near << 4;
+  }
 
-  stamp(a.stamps, 5);
+  pstamp(5);
   // ---- P5: dec_fc on own pixels (n-tiles [t0, t1)), ReLU; X2 publishes them
   {
+    __bf16* const d0p = TB(kTD0);
     const bf16x8 av = (lane & 15) == 0 ? *reinterpret_cast<const bf16x8*>(Zs + 8 * (lane >> 4)) : zero8();
     stream2_pre<13, 1>(wd5, wd5_ld, [&](int i, const bf16x8& bw) {
       const int t = t0 + w + 8 * i;
@@ -398,7 +492,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
         const uint32_t ob = bf16bits(o), nb = (uint32_t)__shfl_xor((int)ob, 1, 64);
         if (lane < 16) {
           *reinterpret_cast<__bf16*>(D0u + img49e(jj >> 6, jj & 63)) = o;
-          if (kGS && train) a.d0[(size_t)n * kFlat + jj] = o;
+          if (train) d0p[jj] = o;
           if ((lane & 1) == 0) xput(xo + kX2 + ((jj - k0) >> 1), tg + 2, ob | (nb << 16), near);
         }
       }
@@ -409,7 +503,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
     const int cnt = 32 * (q1 - q0);
     const int gi[2] = {tid < cnt ? kX2 + tid : -1, tid + 512 < cnt ? kX2 + tid + 512 : -1};
     uint32_t pv[2];
-    xget<2>(xi, gi, tg + 2, pv, pc.err, near);
+    xget<2>(xi, gi, tg + 2, pv, err, near);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       if (gi[k] >= 0) {
@@ -420,20 +514,23 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
   }
   lds_barrier();
 
-  stamp(a.stamps, 6);
+  pstamp(6);
   // ---- P6: dec1 (convT 64 -> 32) on own channels [16 r, 16 r + 16), ReLU
-  tconv7to14_half(D0u, IMG, r, [&](int, int co) { return Bias[kB3 + co]; }, [&](int pix, int co, float v, float bias) {
+  __bf16* const d1p = TB(kTD1);
+  tconv7to14_half(D0u, Zero, IMG, r, [&](int, int co) { return Bias[kB3 + co]; }, [&](int pix, int co, float v, float bias) {
     const __bf16 o = (__bf16)fmaxf(v + bias, 0.f);
     D1s[pix * 32 + co] = o;
-    if (kGS && train) a.d1[((size_t)n * 196 + pix) * 32 + co] = o;
+    if (train) d1p[pix * 32 + co] = o;
     return 0.f;
   });
   lds_barrier();
 
-  stamp(a.stamps, 7);
+  pstamp(7);
   // ---- P7: dec2 partial logits over own channels, X3, then BCE + dlogits (both)
   float loss = 0.f, gsum = 0.f;
   {
+    float* const dlp = TF(kTDlog);
+    float* const rcp = TF(kTRecon);
     float tp[2] = {0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -468,7 +565,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
     }
     const int gi[2] = {tid < 784 ? kX3 + tid : -1, tid + 512 < 784 ? kX3 + tid + 512 : -1};
     uint32_t pv[2];
-    xget<2>(xi, gi, tg + 3, pv, pc.err, near);
+    xget<2>(xi, gi, tg + 3, pv, err, near);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int pix = tid + 512 * k;
@@ -482,8 +579,8 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
         loss += x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
         gsum += g;
         Gs[pix] = g;
-        if (kGS && train && (pix >= 392) == (r == 1)) a.dlog[(size_t)n * 784 + pix] = g;
-        if (kGS && a.recon && (pix >= 392) == (r == 1)) a.recon[(size_t)n * 784 + pix] = p;
+        if (train && (pix >= 392) == (r == 1)) dlp[pix] = g;
+        if (rcp && (pix >= 392) == (r == 1)) rcp[pix] = p;
       }
     }
   }
@@ -501,13 +598,14 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
       sl += Scr[8 + i];
       sg += Scr[16 + i];
     }
-    if (kGS) a.bce_part[n] = sl;
-    if (kGS) a.kld_part[n] = Scr[0];
-    if (kGS && a.db4_part) a.db4_part[n] = sg;
+    TF(kTBce)[0] = sl;
+    TF(kTKld)[0] = Scr[0];
+    if (float* d4 = TF(kTDb4)) d4[0] = sg;
   }
 
-  stamp(a.stamps, 8);
+  pstamp(8);
   // ---- Q1: dec2 backward-data on own channels (8 per thread) x dec1 ReLU mask; X4 publishes gd1
+  __bf16* const gd1p = TB(kTGd1);
   if (tid < 392) {
     const int pix = tid >> 1, h = tid & 1, cg = 2 * r + h;  // 8-channel chunk cg of 4
     const int oy = pix / 14, ox = pix - 14 * (pix / 14);
@@ -535,7 +633,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
       CSB[(8 * h + e) * 197 + pix] = v;  // dec1 bias partials (own channel 8 h + e)
     }
     *reinterpret_cast<bf16x8*>(GD1s + img14(pix, cg)) = o;
-    if (kGS) *reinterpret_cast<bf16x8*>(b.gd1 + ((size_t)n * 196 + pix) * 32 + 8 * cg) = o;
+    *reinterpret_cast<bf16x8*>(gd1p + pix * 32 + 8 * cg) = o;
 #pragma unroll
     for (int e = 0; e < 8; e += 2)  // granule layout [4][392]: one wave store = 512 contiguous bytes
       xput(xo + kX4 + (e >> 1) * 392 + tid, tg + 4, bf16bits(o[e]) | (bf16bits(o[e + 1]) << 16), near);
@@ -544,7 +642,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
   const int jr = lane >> 2;
   auto wd_ld = [&](int it) {
     const int jj = k0 + it * 128 + w * 16 + jr;
-    return *reinterpret_cast<const bf16x8*>(W.Wd + (size_t)(jj < k0 + klen ? jj : k0) * 32 + 8 * (lane & 3));
+    return *reinterpret_cast<const bf16x8*>(TB(kTWd) + (size_t)(jj < k0 + klen ? jj : k0) * 32 + 8 * (lane & 3));
   };
   bf16x8 wd0[13];
 #pragma unroll
@@ -557,14 +655,14 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
-    if (part == 0) b.db3_part[(size_t)n * 32 + 16 * r + c] = s;
+    if (part == 0) TF(kTDb3)[16 * r + c] = s;
   }
   {  // X4: the partner's gd1 channels into the img14 image
     int gi[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) gi[k] = tid + 512 * k < 1568 ? kX4 + tid + 512 * k : -1;
     uint32_t pv[4];
-    xget<4>(xi, gi, tg + 4, pv, pc.err, near);
+    xget<4>(xi, gi, tg + 4, pv, err, near);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (gi[k] >= 0) {
@@ -576,26 +674,28 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
   }
   lds_barrier();
 
-  stamp(a.stamps, 9);
+  pstamp(9);
   // ---- Q2: dec1 backward-data (conv 32 -> 64, B from dec1's tap images) on own pixels x dec_fc mask
-  conv14to7_rows(GD1s, p0, p1,
+  __bf16* const gd0p = TB(kTGd0);
+  float* const dbdp = TF(kTDbd);
+  conv14to7_rows(GD1s, Zero, p0, p1,
                  [&](int j, int t) {
                    return *reinterpret_cast<const bf16x8*>(IMG + t * 4096 + timg<32>(16 * j + (lane & 15), lane >> 4));
                  },
                  [&](int p, int col) { return (float)*reinterpret_cast<const __bf16*>(D0u + img49e(p, col)); },
                  [&](int p, int col, float v, float mask) {
-    const size_t e = (size_t)n * kFlat + p * 64 + col;
+    const int e = p * 64 + col;
     const float g = mask > 0.f ? v : 0.f;
     const __bf16 o = (__bf16)g;
     GD0s[p * 64 + col] = o;
-    if (kGS) b.gd0[e] = o;
-    if (kGS) b.dbd_part[e] = g;
+    gd0p[e] = o;
+    dbdp[e] = g;
   });
   lds_barrier();
 
   TapImageRegs w2r;
-  w2r.load(W.W2);  // enc2 tap images: in flight during Q3-Q5
-  stamp(a.stamps, 10);
+  w2r.load(TB(kTW2));  // enc2 tap images: in flight during Q3-Q5
+  pstamp(10);
   // ---- Q3: dz partial over own dec_fc rows
   {
     float acc[8];
@@ -626,13 +726,13 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
   // Q5's first 16 head-weight loads: row group grp = tid >> 8 (rows 32 grp ..), own 8-chunk ck
   const int nck = klen >> 3, grp = tid >> 8, ck = tid & 255;
   const int kk = k0 + 8 * (ck < nck ? ck : 0);
-  auto wh_ld = [&](int i) { return *reinterpret_cast<const bf16x8*>(W.Wh + (size_t)(32 * grp + i) * kFlat + kk); };
+  auto wh_ld = [&](int i) { return *reinterpret_cast<const bf16x8*>(TB(kTWh) + (size_t)(32 * grp + i) * kFlat + kk); };
   bf16x8 wh5[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) wh5[i] = wh_ld(i);
   lds_barrier();
 
-  stamp(a.stamps, 11);
+  pstamp(11);
   // ---- X5 + Q4: dz = role-0 part + role-1 part; reparam backward (both halves)
   if (tid < 32) {
     const int c = tid;
@@ -642,9 +742,9 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
     xput(xo + kX5 + c, tg + 5, fbits(mine), near);
     const int gi[1] = {kX5 + c};
     uint32_t pv[1];
-    xget<1>(xi, gi, tg + 5, pv, pc.err, near);
+    xget<1>(xi, gi, tg + 5, pv, err, near);
     const float dz = r ? bitsf(pv[0]) + mine : mine + bitsf(pv[0]);
-    const float beta = a.hp->kl_beta;
+    const float beta = tab<L, const HParams>(lds, kTHp)->kl_beta;
     const float mu = Hs[c], lv = Hs[32 + c], ep = Eps[c];
     const float sd = expf(0.5f * lv);
     const float dm = dz + beta * mu;
@@ -652,15 +752,15 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
     DMs[c] = dm;
     DMs[32 + c] = dl;
     if (r == 0) {
-      if (kGS) b.dmulv[(size_t)n * 64 + c] = dm;
-      if (kGS) b.dmulv[(size_t)n * 64 + 32 + c] = dl;
-      if (kGS) b.dmulv16[(size_t)n * 64 + c] = (__bf16)dm;
-      if (kGS) b.dmulv16[(size_t)n * 64 + 32 + c] = (__bf16)dl;
+      TF(kTDmulv)[c] = dm;
+      TF(kTDmulv)[32 + c] = dl;
+      TB(kTDmulv16)[c] = (__bf16)dm;
+      TB(kTDmulv16)[32 + c] = (__bf16)dl;
     }
   }
   lds_barrier();
 
-  stamp(a.stamps, 12);
+  pstamp(12);
   // ---- Q5: head backward-data on own K: two row groups of 32 per 8-chunk, combined in a fixed order
   {
     float acc[8];
@@ -676,6 +776,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
       for (int e = 0; e < 8; ++e) CSB[ck * 8 + e] = acc[e];
     }
     lds_barrier();
+    __bf16* const ga2p = TB(kTGa2);
     if (grp == 0 && ck < nck) {
       const bf16x8 mk = *reinterpret_cast<const bf16x8*>(A2s + kk);
       bf16x8 o;
@@ -687,7 +788,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
         GA2F[kk + e] = v;
       }
       *reinterpret_cast<bf16x8*>(GA2u + img49(kk >> 6, (kk >> 3) & 7)) = o;
-      if (kGS) *reinterpret_cast<bf16x8*>(b.ga2 + (size_t)n * kFlat + kk) = o;
+      *reinterpret_cast<bf16x8*>(ga2p + kk) = o;
 #pragma unroll
       for (int e = 0; e < 8; e += 2)  // granule layout [4][200] (8-chunk ck of the own range)
         xput(xo + kX6 + (e >> 1) * 200 + ck, tg + 6, bf16bits(o[e]) | (bf16bits(o[e + 1]) << 16), near);
@@ -703,7 +804,7 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
       gi[k] = g < 800 && c < nckp ? kX6 + g : -1;
     }
     uint32_t pv[2];
-    xget<2>(xi, gi, tg + 6, pv, pc.err, near);
+    xget<2>(xi, gi, tg + 6, pv, err, near);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       if (gi[k] >= 0) {
@@ -717,20 +818,21 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
   if (tid < 64) {  // enc2 bias partials over own pixels, in order: row r of [2][M][64]
     float s = 0.f;
     for (int p = p0; p < p1; ++p) s += GA2F[p * 64 + tid];
-    if (kGS) b.db2_part[((size_t)r * M + n) * 64 + tid] = s;
+    TF(kTDb2)[(size_t)r * M * 64 + tid] = s;
   }
 
-  stamp(a.stamps, 13);
+  pstamp(13);
   // ---- Q6: enc2 backward-data (convT 64 -> 32 with the conv weights) on own channels x enc1 mask
   {
-    const float cs = tconv7to14_half(GA2u, IMG, r,
+    __bf16* const ga1p = TB(kTGa1);
+    const float cs = tconv7to14_half(GA2u, Zero, IMG, r,
                                      [&](int pix, int co) {
                                        return (float)*reinterpret_cast<const __bf16*>(A1s + img14(pix, co >> 3) +
                                                                                       ((co & 7) << 1));
                                      },
                                      [&](int pix, int co, float v, float mask) {
       const float g = mask > 0.f ? v : 0.f;
-      if (kGS) b.ga1[((size_t)n * 196 + pix) * 32 + co] = (__bf16)g;
+      ga1p[pix * 32 + co] = (__bf16)g;
       return g;
     });
     if (lane < 16) CS[w * 16 + lane] = cs;
@@ -740,9 +842,9 @@ __device__ __forceinline__ void pair_rest(const FwdArgs& a, const BwdArgs& b, ui
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) s += CS[i * 16 + tid];
-    if (kGS) b.db1_part[(size_t)n * 32 + 16 * r + tid] = s;
+    TF(kTDb1)[16 * r + tid] = s;
   }
-  stamp(a.stamps, 14);
+  pstamp(14);
 }
 
 }  // namespace f28
