@@ -198,6 +198,23 @@ __device__ __forceinline__ void stage_conv_image(const __bf16* W, uint8_t* img) 
   }
 }
 
+// stage_conv_image split in two: the loads now, the LDS stores later.
+struct ConvImageRegs {
+  bf16x8 v[8];
+  __device__ __forceinline__ void load(const __bf16* W) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const bf16x8*>(W + (threadIdx.x + i * kThreads) * 8);
+  }
+  __device__ __forceinline__ void store(uint8_t* img) const {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = threadIdx.x + i * kThreads;
+      const int co = q >> 6, tap = (q >> 2) & 15, ch = q & 3;
+      *reinterpret_cast<bf16x8*>(img + cimg(co, tap, ch)) = v[i];
+    }
+  }
+};
+
 // B fragment of n-tile j, k-step (tap) t: lane holds W[16j + (l & 15)][t][8(l >> 4) ..]
 __device__ __forceinline__ bf16x8 conv_bfrag(const uint8_t* img, int j, int t, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + cimg(16 * j + (lane & 15), t, lane >> 4));
@@ -363,50 +380,70 @@ __device__ __forceinline__ void fwd_p01(const FwdArgs& a, uint8_t* lds, int n, A
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Weights& W = a.w;
   stamp(a.stamps, 0);
+  ConvImageRegs w2regs;  // enc2's conv-layout image: loaded in P0, written to LDS after P1
 
-  // ---- P0: L2 prefetch of the Linear weights, batch row gather, small
-  // weights, dec1 tap images, enc2 B fragments.
-  // The head (400 KB) and dec_fc (200 KB) weights were just rewritten by the
-  // optimizer on other XCDs, so P3 / P5 would stream them from the Infinity
-  // Cache at ~2 us per round trip. The workgroups that share an XCD (block
-  // ids b, b+8, ...: round-robin dispatch; a wrong guess costs speed only;
-  // 16 of them for one workgroup per sample, 32 for two) each pull one slice
-  // into that XCD's L2 now, through LDS-DMA loads into a scratch LDS zone
-  // (nothing reads it), during P0-P2.
-  {
-    constexpr int kWh = kFlat * 64 * 2, kWd = kFlat * 32 * 2;
-    const int nsl = a.pf_slices, kSlice = (kWh + kWd) / nsl;
-    const int r = (int)(blockIdx.x >> 3) % nsl;
-    for (int k = w; k * 1024 < kSlice; k += 8) {
-      const int off = r * kSlice + k * 1024 + lane * 16;
-      const uint8_t* src = off < kWh ? reinterpret_cast<const uint8_t*>(W.Wh) + off
-                                     : reinterpret_cast<const uint8_t*>(W.Wd) + (off - kWh < kWd ? off - kWh : 0);
-      glds16(src, lds + L::Dummy + w * 1024);
-    }
-  }
+  // ---- P0: batch row gather, small weights, enc2's B image (into registers,
+  // written to LDS after P1), L2 prefetch of the Linear weights.
+  // Issue order matters: vmcnt retires in order, so the loads P1 needs (the
+  // row, W1, biases) go first; the enc2 image loads and the prefetch DMAs go
+  // after them and stay in flight through P1 (P0 ends on an LDS-only barrier).
   {
     const int row = a.idx[(size_t)a.st->cursor * a.B + n];
     const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)row * 784);
+    float4 xv = {0.f, 0.f, 0.f, 0.f};
+    if (tid < 196) xv = src[tid];
+    const float w1 = W.W1f[tid], w4 = W.W4f[tid];
+    float bv = 0.f;
+    if (tid < kNBias)
+      bv = tid < kB2 ? W.b1[tid] : tid < kBh ? W.b2[tid - kB2] : tid < kB3 ? W.bh[tid - kBh]
+         : tid < kB4 ? W.b3[tid - kB3] : W.b4[0];
+    float4 bdv[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * kThreads;
+      bdv[i] = e < kFlat / 4 ? reinterpret_cast<const float4*>(W.bd)[e] : float4{0.f, 0.f, 0.f, 0.f};
+    }
+    w2regs.load(W.W2);
+    // The head (400 KB) and dec_fc (200 KB) weights were just rewritten by
+    // the optimizer on other XCDs, so P3 / P5 would stream them from the
+    // Infinity Cache. The workgroups that share an XCD (block ids b, b+8, ...:
+    // round-robin dispatch; a wrong guess costs speed only; 16 of them for
+    // one workgroup per sample, 32 for two) each pull one slice into that
+    // XCD's L2 now, through LDS-DMA loads into a scratch LDS zone (nothing
+    // reads it). The builtin (not asm) keeps them in the compiler's vmcnt
+    // accounting, so no wait above includes them.
+    {
+      constexpr int kWh = kFlat * 64 * 2, kWd = kFlat * 32 * 2;
+      const int nsl = a.pf_slices, kSlice = (kWh + kWd) / nsl;
+      const int r = (int)(blockIdx.x >> 3) % nsl;
+      for (int k = w; k * 1024 < kSlice; k += 8) {
+        const int off = r * kSlice + k * 1024 + lane * 16;
+        const uint8_t* psrc = off < kWh ? reinterpret_cast<const uint8_t*>(W.Wh) + off
+                                        : reinterpret_cast<const uint8_t*>(W.Wd) + (off - kWh < kWd ? off - kWh : 0);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)psrc,
+                                         (__attribute__((address_space(3))) void*)(lds + L::Dummy + w * 1024), 16, 0,
+                                         0);
+      }
+    }
     if (tid < 196) {
-      const float4 v = src[tid];
-      reinterpret_cast<float4*>(Xs)[tid] = v;
-      if (a.train) reinterpret_cast<float4*>(a.xb + (size_t)n * 784)[tid] = v;
+      reinterpret_cast<float4*>(Xs)[tid] = xv;
+      if (a.train) reinterpret_cast<float4*>(a.xb + (size_t)n * 784)[tid] = xv;
     }
     const int c = tid >> 4, t = tid & 15;  // 512 threads = 32 channels x 16 taps
-    W1s[t * 32 + c] = W.W1f[tid];
-    W4s[t * 32 + c] = W.W4f[tid];
-    for (int e = tid; e < kFlat / 4; e += kThreads)
-      reinterpret_cast<float4*>(lds + L::Bd)[e] = reinterpret_cast<const float4*>(W.bd)[e];
+    W1s[t * 32 + c] = w1;
+    W4s[t * 32 + c] = w4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * kThreads;
+      if (e < kFlat / 4) reinterpret_cast<float4*>(lds + L::Bd)[e] = bdv[i];
+    }
     if (tid < kNBias) {
-      float* bs = reinterpret_cast<float*>(lds + L::Bias);
-      bs[tid] = tid < kB2 ? W.b1[tid] : tid < kBh ? W.b2[tid - kB2] : tid < kB3 ? W.bh[tid - kBh]
-              : tid < kB4 ? W.b3[tid - kB3] : W.b4[0];
+      reinterpret_cast<float*>(lds + L::Bias)[tid] = bv;
     } else if (tid >= kZero && tid < kZero + 4) {
       reinterpret_cast<float*>(lds + L::Bias)[tid] = 0.f;
     }
   }
-  stage_conv_image(W.W2, W3s);  // enc2 weights first; dec1's tap images replace them after P2
-  __syncthreads();
+  lds_barrier();
   after_p0();
 
   stamp(a.stamps, 1);
@@ -443,6 +480,7 @@ __device__ __forceinline__ void fwd_p01(const FwdArgs& a, uint8_t* lds, int n, A
       if (a.train) *reinterpret_cast<bf16x8*>(a.a1 + ((size_t)n * 196 + pix) * 32 + 8 * ch) = o;
     }
   }
+  w2regs.store(W3s);  // enc2 weights (dec1's tap images replace them after P2); the caller's barrier publishes
 }
 
 // P2 .. P7 of the forward, one workgroup per sample.
