@@ -366,12 +366,11 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
   });
   lds_barrier();
 
-  TapImageRegs w3r;
-  w3r.load(TB(kTW3));  // dec1 tap images: in flight during P3-P5
   pstamp(3);
   // ---- P3: head partial sums over own K (= own pixels). Wave w: rows
-  // w + 16 c2 and w + 16 c2 + 8 per step c2 (two rows of loads per step, the
-  // next step's in flight: the row loop is L2-latency bound, not bandwidth)
+  // w + 16 c2 + 8 h (c2 < 4, h < 2). All eight rows' loads are in flight at
+  // once (the first two since P2): the phase is L2-latency bound, so one
+  // round trip instead of four.
   {
     bf16x8 av[4];
 #pragma unroll
@@ -379,19 +378,21 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
       const int k = 512 * i + 8 * lane;
       av[i] = k < klen ? *reinterpret_cast<const bf16x8*>(A2s + k0 + k) : zero8();
     }
-    bf16x8 vc[8], vn[8];
+    bf16x8 wr[4][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) vc[i] = wh0[i];
-#pragma unroll 1
-    for (int c2 = 0; c2 < 4; ++c2) {
-      if (c2 + 1 < 4) ld_rows(c2 + 1, vn);
-      float d[2];
+    for (int i = 0; i < 8; ++i) wr[0][i] = wh0[i];
+    ld_rows(1, wr[1]);
+    ld_rows(2, wr[2]);
+    ld_rows(3, wr[3]);
+    float d[8];
+#pragma unroll
+    for (int c2 = 0; c2 < 4; ++c2)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         float dq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const bf16x8& wv = vc[4 * h + i];
+          const bf16x8& wv = wr[c2][4 * h + i];
           if (512 * i + 8 * lane < klen) {
             dq[0] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 0, 1),
                                                     __builtin_shufflevector(wv, wv, 0, 1), dq[0], false);
@@ -403,22 +404,21 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
                                                     __builtin_shufflevector(wv, wv, 6, 7), dq[3], false);
           }
         }
-        d[h] = (dq[0] + dq[1]) + (dq[2] + dq[3]);
-      }
-      d[0] = wave_sum(d[0]);
-      d[1] = wave_sum(d[1]);
-      if (lane == 0) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int o = w + 16 * c2 + 8 * h;
-          Hs[o] = d[h];
-          xput(xo + kX1 + o, tg + 1, fbits(d[h]), false);
-        }
+        d[2 * c2 + h] = (dq[0] + dq[1]) + (dq[2] + dq[3]);
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) vc[i] = vn[i];
+    for (int i = 0; i < 8; ++i) d[i] = wave_sum(d[i]);
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int o = w + 16 * (i >> 1) + 8 * (i & 1);
+        Hs[o] = d[i];
+        xput(xo + kX1 + o, tg + 1, fbits(d[i]), false);
+      }
     }
   }
+  TapImageRegs w3r;
+  w3r.load(TB(kTW3));  // dec1 tap images: in flight during P4-P5
   // P5's first dec_fc weight loads (own n-tiles t = 4 p0 + w + 8 i), in flight across P4
   const int t0 = 4 * p0, t1 = 4 * p1;
   const __bf16* wp5 = TB(kTWd) + (size_t)(lane & 15) * 32 + 8 * (lane >> 4);
@@ -437,6 +437,13 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
     float kl = 0.f;
     if (tid < 32) {
       const int c = tid;
+      // eps first: it needs nothing from the partner, so it overlaps the X1 wait
+      const unsigned long long stp = (unsigned long long)tab<L, const TrainState>(lds, kTSt)->step;
+      const HParams* hp = tab<L, const HParams>(lds, kTHp);
+      const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(n * 32 + c), stream, (uint32_t)(stp & 0xffffffffu),
+                                             (uint32_t)(stp >> 32)},
+                                       hp->seed_lo, hp->seed_hi);
+      const float ep = normal_from_bits(bits.x, bits.y);
       const int gi[2] = {kX1 + c, kX1 + 32 + c};
       uint32_t pv[2];
       xget<2>(xi, gi, tg + 1, pv, err, false);
@@ -445,11 +452,6 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
       const float lv = (r ? lp + l0 : l0 + lp) + Bias[kBh + 32 + c];
       Hs[c] = mu;
       Hs[32 + c] = lv;
-      const unsigned long long stp = (unsigned long long)tab<L, const TrainState>(lds, kTSt)->step;
-      const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(n * 32 + c), stream, (uint32_t)(stp & 0xffffffffu),
-                                             (uint32_t)(stp >> 32)},
-                                       tab<L, const HParams>(lds, kTHp)->seed_lo, tab<L, const HParams>(lds, kTHp)->seed_hi);
-      const float ep = normal_from_bits(bits.x, bits.y);
       const float sd = expf(0.5f * lv);
       const float zz = mu + ep * sd;
       kl = 1.f + lv - mu * mu - sd * sd;
@@ -693,8 +695,7 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
   });
   lds_barrier();
 
-  TapImageRegs w2r;
-  w2r.load(TB(kTW2));  // enc2 tap images: in flight during Q3-Q5
+  TapImageRegs w2r;  // enc2 tap images (loaded in Q5, written before Q6)
   pstamp(10);
   // ---- Q3: dz partial over own dec_fc rows
   {
@@ -766,11 +767,17 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-    stream2_pre<16, 2>(wh5, wh_ld, [&](int i, const bf16x8& wv) {
+    bf16x8 wh6[16];  // rows 16..31 of the group: with wh5, all 32 in flight at once
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wh6[i] = wh_ld(16 + i);
+    w2r.load(TB(kTW2));  // enc2 tap images: in flight during Q5
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const bf16x8& wv = i < 16 ? wh5[i] : wh6[i - 16];
       const float dm = DMs[32 * grp + i];
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] = fmaf(dm, (float)wv[e], acc[e]);
-    });
+    }
     if (grp == 1 && ck < nck) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) CSB[ck * 8 + e] = acc[e];
