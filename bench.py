@@ -130,9 +130,12 @@ def main(argv=None):
         from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
 
         im = 28 if a.model == "conv28" else 128
-        return ConvVaeTrainer(batch_size=a.batch_size, image=im, z=32 if im == 28 else 64, device=dev,
-                              backend=a.backend, seed=spec.seed, lr=spec.lr, kl_beta=spec.beta,
-                              rng_stream=grank, use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
+        tr = ConvVaeTrainer(batch_size=a.batch_size, image=im, z=32 if im == 28 else 64, device=dev,
+                            backend=a.backend, seed=spec.seed, lr=spec.lr, kl_beta=spec.beta,
+                            rng_stream=grank, use_graphs=not a.no_graphs, graph_steps=a.graph_steps)
+        if T > 1:  # packed trials already fill the chip: one workgroup per sample (deterministic form)
+            tr.f28_pair = False
+        return tr
 
     trainers, streams = [], []
     img = 28 if a.model in ("mlp", "conv28") else 128

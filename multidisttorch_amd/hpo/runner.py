@@ -464,6 +464,10 @@ def run_packed_trials(specs, group, opts: RunOptions, data=None, num_trials: Opt
     tr = []
     for spec in specs:
         trainer = _make_trainer(spec, opts, device, 0, D)
+        if len(specs) > 1 and hasattr(trainer, "f28_pair"):
+            # packed trials fill the chip already; the one-workgroup-per-sample
+            # step keeps their numerics independent of how the trials interleave
+            trainer.f28_pair = False
         start = 1
         if opts.ckpt_dir and opts.resume:
             prog = ckpt.load_latest(opts.ckpt_dir, spec.group_id, trainer)

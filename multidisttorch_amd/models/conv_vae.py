@@ -1053,9 +1053,18 @@ class ConvVaeTrainer:
         segs = self._seg_rows(slabs)
         units, layer_units = self._finalize_units(segs)
         pack, grid = C.pack_jobs_multi(jobs)
+        # intra-group DDP: the decoder's weight gradients (ready first in the
+        # reference's backward order) get a launch of their own, so their
+        # bucket's all-reduce runs while the encoder's are still computed
+        names = list(srcs)
+        dec_pack, dec_grid = C.pack_jobs_multi([jobs[i] for i, n in enumerate(names) if n.startswith("dec")] +
+                                               [jobs[len(names)]])
+        enc_pack, enc_grid = C.pack_jobs_multi([jobs[i] for i, n in enumerate(names) if not n.startswith("dec")])
+        first_dec = next(i for i, l in enumerate(self.spec) if l.name.startswith("dec"))
         p = dict(fwd=fwd, bwd=bwd, jobs=jobs, jobs_pack=pack.to(dev), jobs_grid=grid, slabs=slabs,
                  segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
-                 nunits=len(units))
+                 nunits=len(units), layer_units=layer_units, first_dec=first_dec,
+                 dec_pack=dec_pack.to(dev), dec_grid=dec_grid, enc_pack=enc_pack.to(dev), enc_grid=enc_grid)
         if self.f28_fin:
             # weight-gradient jobs 0..5 (srcs order), loss/step job 6, finalize
             # job 7: a weight unit waits for its layer's job, every unit for the
@@ -1090,14 +1099,43 @@ class ConvVaeTrainer:
         if self.f28_fin and red is None and not self.f28_skip_adam:
             C.launch_jobs_multi(p["fin_pack"], p["fin_grid"])
             return
-        C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
-        C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
-                        p["nunits"], st.train_state, st.hparams, red is None and not self.f28_skip_adam)
-        if red is not None:
-            red.launch_all()
-            red.wait_all()
+        if red is None:
+            C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
+            C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
+                            p["nunits"], st.train_state, st.hparams, not self.f28_skip_adam)
+            return
+        # DDP (reference: the Reducer's bucket all-reduces launched from the
+        # autograd hooks while backward continues, /root/reference/vae-hpo.py:72,
+        # :130): decoder weight gradients -> their finalize -> every bucket
+        # that holds only decoder parameters goes out on the comm stream ->
+        # encoder weight gradients (overlapping those all-reduces) -> their
+        # finalize -> the remaining buckets -> wait -> Adam + bf16 cast.
+        lu, fd, L = p["layer_units"], p["first_dec"], len(self.spec)
+        dec0 = self.layer_ranges()[fd][1]
+        bounds = list(red.bounds())
+        nbk = len(bounds) - 1
+        C.launch_jobs_multi(p["dec_pack"], p["dec_grid"])
+        self._finalize_unit_range(p, lu[fd], lu[L])
+        for k in reversed(range(nbk)):
+            if bounds[k] >= dec0:
+                red.launch(k)
+        C.launch_jobs_multi(p["enc_pack"], p["enc_grid"])
+        self._finalize_unit_range(p, lu[0], lu[fd])
+        for k in reversed(range(nbk)):
+            if bounds[k] < dec0:
+                red.launch(k)
+        red.wait_all()
+        if not self.f28_skip_adam:
             C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
                         st.train_state, st.hparams, True)
+
+    def _finalize_unit_range(self, p, u0, u1):
+        """Slab reduction into the gradient arena (no Adam) of finalize units [u0, u1)."""
+        if u1 > u0:
+            st = self.state
+            self.C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"],
+                                 p["units"].narrow(0, u0 * 12, (u1 - u0) * 12), u1 - u0, st.train_state,
+                                 st.hparams, False)
 
     # layer groups whose gradients are finalized together (optimizer + bf16
     # re-cast + transposed copies) on the side stream once the backward-data

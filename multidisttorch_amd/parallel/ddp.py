@@ -196,13 +196,16 @@ def reducer_kind(pg, flat: torch.Tensor) -> str:
 
 
 def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: bool = True,
-                       prefer_native: bool = True, kind: Optional[str] = None):
+                       prefer_native: bool = True, kind: Optional[str] = None, scale: float = 0.0):
     """Bucket reducer over a flat gradient arena ([begin, end) buckets).
 
     On MI355X trial groups (RCCL) this is the direct-RCCL reducer of
     csrc/runtime/xgmi_comm.cpp: PreMulSum(1/s) averaging fused into the
     collective, a dedicated high-priority comm stream, event fences only.
     gloo groups (CPU tests, control plane) use the c10d-based native reducer.
+    ``scale`` (RCCL only) replaces the 1/s pre-multiplier; any scale other
+    than 1 issues the collective even on a one-rank group (tests use it to
+    put real ``ncclAllReduce`` kernels into a one-GPU step graph).
     """
     if pg is None:
         pg = dist.distributed_c10d._get_default_group()
@@ -210,7 +213,7 @@ def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: b
     b = [int(x) for x in bounds]
     if kind == "rccl":
         size = dist.get_world_size(pg)
-        return native.require().RcclBucketReducer(rccl_comm_ptr(pg, flat.device), size, flat, b, average)
+        return native.require().RcclBucketReducer(rccl_comm_ptr(pg, flat.device), size, flat, b, average, scale)
     if kind == "p2p":
         return make_p2p_reducer(pg, flat, b, average)
     if kind == "c10d" and native.available():

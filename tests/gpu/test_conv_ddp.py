@@ -136,18 +136,22 @@ def test_conv_trainer_rccl_reducer_matches_single(nccl_world, native_ext, image)
         torch.testing.assert_close(p, p0, rtol=1e-5, atol=1e-6, msg=str(key))
 
 
-@pytest.mark.parametrize("image", [28, 128])
-def test_conv_bucket_launches_interleave_with_backward(nccl_world, native_ext, image):
+@pytest.mark.parametrize("image,f28", [(28, True), (28, False), (128, False)])
+def test_conv_bucket_launches_interleave_with_backward(nccl_world, native_ext, image, f28):
     """Eager step with three or more buckets: the first (decoder-end) bucket's
     all-reduce is issued before the backward GEMMs of the earlier layers, and
-    the wait comes after the last backward launch."""
+    the wait comes after the last backward launch. The fused 28x28 step
+    (f28) issues the decoder bucket between its decoder and encoder
+    weight-gradient launches."""
     from multidisttorch_amd.parallel.ddp import make_arena_reducer
 
     dev = torch.device("cuda", 0)
     B = 128 if image == 28 else 32
     X, idx = _data(image, 2, B, dev)
     tr = _trainer(image, B, dev, graphs=False)
-    tr.f28 = False  # the layer-by-layer step launches buckets during its backward
+    if image == 28:
+        assert tr.f28
+        tr.f28 = f28
     bounds = tr.bucket_bounds(0.25 if image == 28 else 2.0)
     assert len(bounds) - 1 >= 3, bounds
     log = []
@@ -160,10 +164,47 @@ def test_conv_bucket_launches_interleave_with_backward(nccl_world, native_ext, i
     nbk = len(bounds) - 1
     first = log.index(f"bucket{nbk - 1}")  # the last arena bucket holds the decoder: ready first
     wait = log.index("wait_all")
-    bwd = [i for i, n in enumerate(log) if n in ("wgrad", "igemm", "thin_conv", "launch_jobs")]
+    bwd = [i for i, n in enumerate(log) if n in ("wgrad", "igemm", "thin_conv", "launch_jobs", "launch_jobs_multi")]
     assert any(first < i < wait for i in bwd), log
     assert all(f"bucket{k}" in log[:wait] for k in range(nbk)), log
     assert log.index("adam_cast") > wait, log
+    if image == 28 and f28:
+        jm = [i for i, n in enumerate(log) if n == "launch_jobs_multi"]
+        assert len(jm) == 2 and jm[0] < first < jm[1], log  # decoder wgrads | decoder bucket | encoder wgrads
+
+
+@pytest.mark.parametrize("image,f28", [(28, True), (28, False), (128, False)])
+def test_conv_step_graph_issues_real_collectives(nccl_world, native_ext, image, f28):
+    """A one-rank group's all-reduce is an identity, so the reducer skips it
+    unless told otherwise. Here it runs with PreMulSum scale 2 (a real
+    ncclAllReduce on every bucket, captured into the replayed step graphs)
+    while Adam's grad_scale is 0.5: the result equals the reducer-free run
+    only if every collective actually executed inside the graph (a skipped
+    one would leave the gradients at half)."""
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+
+    dev = torch.device("cuda", 0)
+    B = 128 if image == 28 else 32
+    nb, steps = 4, 8
+    X, idx = _data(image, nb, B, dev)
+    runs = {}
+    for mode in ("single", "scaled"):
+        tr = _trainer(image, B, dev, True)
+        if image == 28:
+            tr.f28 = f28
+        if mode == "scaled":
+            red = make_arena_reducer(nccl_world, tr.grads, tr.bucket_bounds(0.25 if image == 28 else 2.0), scale=2.0)
+            tr.attach_reducer(red)
+            tr.set_hparams(grad_scale=0.5)
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, nb)
+        tr.train_steps(steps)
+        torch.cuda.synchronize()
+        runs[mode] = (tr.params.clone(), tr.loss_history()[:steps].copy())
+        if mode == "scaled":
+            assert red.launched_count() == 5 * red.num_buckets() and red.num_buckets() >= 2
+    np.testing.assert_allclose(runs["scaled"][1], runs["single"][1], rtol=1e-5)
+    torch.testing.assert_close(runs["scaled"][0], runs["single"][0], rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("model", ["conv28", "mlp"])
@@ -198,7 +239,10 @@ def test_prepare_locks_graphs_for_timed_steps(native_ext, model):
 def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb):
     from multidisttorch_amd.launch import launch
 
-    env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2"}
+    # several processes share the GPU: the fused 28x28 step keeps one workgroup
+    # per sample (a paired sample whose partner is not resident falls back to
+    # the solo form, whose f32 summation order differs at rounding level)
+    env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2", "MDT_F28_PAIR": "0"}
     rc, outs = launch([sys.executable, os.path.join(HERE, "conv_ddp_worker.py"), str(image), str(graphs), mb], s,
                       emulate="torchrun", timeout=150, extra_env=env, capture=True)
     text = "\n".join(o or "" for o in outs)
