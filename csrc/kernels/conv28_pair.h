@@ -100,9 +100,6 @@ __device__ __forceinline__ void xget(unsigned long long* base, const int (&gi)[N
     v[k] = 0;
     if (gi[k] >= 0) pend |= 1u << k;
   }
-#ifdef MDT_F28_XNOWAIT  // timing experiment only: no hand-off wait (wrong numerics)
-  pend = 0;
-#endif
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned spin = 0;; ++spin) {
 #pragma unroll

@@ -379,24 +379,17 @@ __global__ void __launch_bounds__(256) dconv_k(DcArgs a) {
 
 // The configurations (swizzles searched for conflict-free fragment reads of
 // every tap: scripts/dconv_banks.py).
+// R = 4 rows per workgroup (two workgroups per CU, <= 80 KB LDS): measured
+// 15-18 % faster than R = 8 (one per CU) and 3-4 % faster than R = 2 (three
+// per CU, shallower weight rings) at B = 64 and 128 (profiles/r2_dconv).
 //                mode CA  WA NCOLS NB  R  WM S  AL BE MK
-using DcS1 = DcCfg<0, 32, 64, 64, 64, 8, 4, 8, 0, 2, 3>;     // conv 64x64x32 -> 32x32x64
-using DcS2 = DcCfg<0, 64, 32, 128, 64, 8, 2, 8, 0, 1, 7>;    // conv 32x32x64 -> 16x16x128
-using DcT2 = DcCfg<1, 128, 16, 64, 32, 8, 1, 6, 0, 0, 15>;   // tconv 16x16x128 -> 32x32x64
-using DcT3 = DcCfg<1, 64, 32, 32, 32, 8, 1, 3, 0, 1, 7>;     // tconv 32x32x64 -> 64x64x32
+using DcS1 = DcCfg<0, 32, 64, 64, 64, 4, 2, 4, 0, 2, 3>;     // conv 64x64x32 -> 32x32x64
+using DcS2 = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7>;    // conv 32x32x64 -> 16x16x128
+using DcT2 = DcCfg<1, 128, 16, 64, 32, 4, 1, 3, 0, 0, 15>;   // tconv 16x16x128 -> 32x32x64
+using DcT3 = DcCfg<1, 64, 32, 32, 32, 4, 1, 3, 0, 1, 7>;     // tconv 32x32x64 -> 64x64x32
 // 16x16 <-> 8x8 layers: one image (conv, M = 64) / the whole 8x8 class grid
 // (tconv, 4 x 64 rows) per workgroup, 64 / 32 output channels
 using DcS3 = DcCfg<0, 128, 16, 256, 64, 8, 2, 4, 4, 0, 15>;  // conv 16x16x128 -> 8x8x256
 using DcT1 = DcCfg<1, 256, 8, 128, 32, 8, 1, 3, 8, 0, 15>;   // tconv 8x8x256 -> 16x16x128
-// two-workgroups-per-CU variants (R = 4, <= 80 KB LDS; the default, MDT_DCONV_ALT=0 for the above)
-using DcS1b = DcCfg<0, 32, 64, 64, 64, 4, 2, 4, 0, 2, 3>;
-using DcS2b = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7>;
-using DcT2b = DcCfg<1, 128, 16, 64, 32, 4, 1, 3, 0, 0, 15>;
-using DcT3b = DcCfg<1, 64, 32, 32, 32, 4, 1, 3, 0, 1, 7>;
-// three-workgroups-per-CU variants (R = 2, shallower weight rings; MDT_DCONV_ALT=8,
-// the 32x32x64 -> 16x16x128 conv keeps its R = 4 tile)
-using DcS1c = DcCfg<0, 32, 64, 64, 64, 2, 2, 3, 0, 2, 3>;
-using DcT2c = DcCfg<1, 128, 16, 64, 32, 2, 1, 2, 0, 0, 15>;
-using DcT3c = DcCfg<1, 64, 32, 32, 32, 2, 1, 2, 0, 1, 7>;
 
 }  // namespace mdt

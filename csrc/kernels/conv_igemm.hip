@@ -56,11 +56,8 @@ struct DcInfo {
 };
 template <class CF>
 constexpr DcInfo dc_info() { return DcInfo{CF::RB, CF::NBB, CF::MT, CF::NB}; }
-static const DcInfo kDcInfo[] = {dc_info<DcS1>(),  dc_info<DcS2>(),  dc_info<DcT2>(),  dc_info<DcT3>(),
-                                  dc_info<DcS1b>(), dc_info<DcS2b>(), dc_info<DcT2b>(), dc_info<DcT3b>(),
-                                  dc_info<DcS3>(),  dc_info<DcT1>(),
-                                  dc_info<DcS1c>(), dc_info<DcS2b>() /* 11: unused */, dc_info<DcT2c>(),
-                                  dc_info<DcT3c>()};
+static const DcInfo kDcInfo[] = {dc_info<DcS1>(), dc_info<DcS2>(), dc_info<DcT2>(),
+                                  dc_info<DcT3>(), dc_info<DcS3>(), dc_info<DcT1>()};
 
 // the 16x16 <-> 8x8 geometries (MDT_DCONV_SMALL=0 keeps them on im2col)
 static bool direct_small() {
@@ -76,13 +73,9 @@ int direct_cfg(int mode, const ConvDesc& d, bool fwd) {
     const char* e = getenv("MDT_CONV_DIRECT");
     return !(e && e[0] == '0');
   }();
-  // default: the two-workgroups-per-CU tiles (R = 4), measured 15-18 % faster
-  // than the one-per-CU R = 8 tiles at B = 64 and 128 (profiles/r2_dconv);
-  // MDT_DCONV_ALT=0 selects the latter
-  static const int alt = [] {
-    const char* e = getenv("MDT_DCONV_ALT");
-    return e && e[0] == '0' ? 0 : (e && e[0] == '8' ? 8 : 4);
-  }();
+  // the two-workgroups-per-CU tiles (R = 4): measured 15-18 % faster than
+  // one-per-CU R = 8 tiles and 3-4 % faster than three-per-CU R = 2 tiles at
+  // B = 64 and 128 (profiles/r2_dconv)
   // MDT_DCONV_BWD=0: forward calls only (backward-data keeps the fusable im2col kernel)
   static const bool bwd = [] {
     const char* e = getenv("MDT_DCONV_BWD");
@@ -92,15 +85,15 @@ int direct_cfg(int mode, const ConvDesc& d, bool fwd) {
   if (!fwd && !bwd) return -1;
   if (d.H != d.W || d.OH != d.OW || d.H != 2 * d.OH) return -1;
   if (mode == kModeConv) {  // A = input (H, C), columns = CO
-    if (d.C == 32 && d.H == 64 && d.CO == 64) return alt == 8 ? 10 : 0 + alt;
-    if (d.C == 64 && d.H == 32 && d.CO == 128) return alt == 8 ? 5 : 1 + alt;
+    if (d.C == 32 && d.H == 64 && d.CO == 64) return 0;
+    if (d.C == 64 && d.H == 32 && d.CO == 128) return 1;
     // 16x16 -> 8x8: forward only; as a backward-data GEMM the im2col kernel
     // fuses with the weight gradient in one launch, which measured faster
-    if (d.C == 128 && d.H == 16 && d.CO == 256 && fwd && direct_small()) return 8;
+    if (d.C == 128 && d.H == 16 && d.CO == 256 && fwd && direct_small()) return 4;
   } else {  // A = conv output (OH, CO), columns = C
-    if (d.CO == 128 && d.OH == 16 && d.C == 64) return alt == 8 ? 12 : 2 + alt;
-    if (d.CO == 64 && d.OH == 32 && d.C == 32) return alt == 8 ? 13 : 3 + alt;
-    if (d.CO == 256 && d.OH == 8 && d.C == 128 && fwd && direct_small()) return 9;
+    if (d.CO == 128 && d.OH == 16 && d.C == 64) return 2;
+    if (d.CO == 64 && d.OH == 32 && d.C == 32) return 3;
+    if (d.CO == 256 && d.OH == 8 && d.C == 128 && fwd && direct_small()) return 5;
   }
   return -1;
 }
@@ -299,19 +292,6 @@ bool plan_wgrad(const ConvDesc& d, WgradPlan* p) {
   return true;
 }
 
-// Staging path for bf16 vector-gather GEMMs: the register-staged double
-// buffer (default) or the S-stage LDS-DMA ring (MDT_CONV_GLDS=1). Measured on
-// MI355X (bench/gemm_calib.py, profiles/r1_conv_igemm/README.md): the DMA
-// ring needs 80-128 KB LDS, i.e. one block per CU, and loses 10-60 % at every
-// conv shape and at 4096^3, so it is kept only as an A/B option.
-bool use_glds() {
-  static const bool v = [] {
-    const char* e = getenv("MDT_CONV_GLDS");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 int build_igemm(int mode, const void* A, const void* B16, ConvDesc d, const float* bias, int relu, void* y16,
                 float* y32, const void* omask, float* colsum, float* ws, IgArgs* pa, FwdPlan* pq, CombineArgs* pc,
                 int* nc) {
@@ -398,15 +378,8 @@ int launch_direct(int cfg, const void* A, const void* B16, const ConvDesc& d, co
     case 1: launch_dc<DcS2>(a, s); break;
     case 2: launch_dc<DcT2>(a, s); break;
     case 3: launch_dc<DcT3>(a, s); break;
-    case 4: launch_dc<DcS1b>(a, s); break;
-    case 5: launch_dc<DcS2b>(a, s); break;
-    case 6: launch_dc<DcT2b>(a, s); break;
-    case 7: launch_dc<DcT3b>(a, s); break;
-    case 8: launch_dc<DcS3>(a, s); break;
-    case 9: launch_dc<DcT1>(a, s); break;
-    case 10: launch_dc<DcS1c>(a, s); break;
-    case 12: launch_dc<DcT2c>(a, s); break;
-    case 13: launch_dc<DcT3c>(a, s); break;
+    case 4: launch_dc<DcS3>(a, s); break;
+    case 5: launch_dc<DcT1>(a, s); break;
     default: return 2;
   }
   return (int)hipGetLastError();
@@ -443,39 +416,11 @@ int dispatch_fwd_cfg(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
   return 2;
 }
 
-template <int MODE, class TC, int S>
-void launch_glds(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
-  dim3 grid(q.mtiles * q.ntiles, q.ksplit, q.classes);
-  hipLaunchKernelGGL((igemm_glds_k<MODE, TC, S>), grid, dim3(256), 0, s, a);
-}
-
-// bf16 vector-gather problems: S-stage LDS-DMA pipeline (S*STAGE <= 128 KB)
-template <int MODE>
-int dispatch_glds(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
-  switch (q.cfg) {
-    case 0: launch_glds<MODE, F0, 4>(a, q, s); return 0;
-    case 1: launch_glds<MODE, F1, 4>(a, q, s); return 0;
-    case 2: launch_glds<MODE, F2, 4>(a, q, s); return 0;
-    case 3: launch_glds<MODE, F3, 4>(a, q, s); return 0;
-    case 4: launch_glds<MODE, F4, 4>(a, q, s); return 0;
-    case 5: launch_glds<MODE, F5, 6>(a, q, s); return 0;
-    case 6: launch_glds<MODE, F6, 6>(a, q, s); return 0;
-    case 7: launch_glds<MODE, F7, 6>(a, q, s); return 0;
-  }
-  return 2;
-}
-
 template <typename AT>
 int dispatch_thin(const IgArgs& a, const FwdPlan& q, hipStream_t s) {
   if (q.cfg == 2) { launch_fwd<kModeConv, AT, false, F2>(a, q, s); return 0; }
   if (q.cfg == 6) { launch_fwd<kModeConv, AT, false, F6>(a, q, s); return 0; }
   return 2;
-}
-
-template <class TC, int S>
-void launch_wgg(const WgArgs& a, const WgradPlan& q, hipStream_t s) {
-  dim3 grid(q.cotiles * q.ktiles * q.nsplit);
-  hipLaunchKernelGGL((wgrad_glds_k<TC, S>), grid, dim3(256), 0, s, a);
 }
 
 template <typename XT, bool VEC, class TC>
@@ -532,12 +477,11 @@ int mdt_igemm(int mode, const void* A, int a_is_f32, const void* B16, ConvDesc d
   } else if (mode == kModeConv) {
     if (q.thin) rc = a_is_f32 ? dispatch_thin<float>(a, q, s) : dispatch_thin<__bf16>(a, q, s);
     else if (a_is_f32) rc = 3;
-    else if (use_glds()) rc = dispatch_glds<kModeConv>(a, q, s);
     else rc = dispatch_fwd_cfg<kModeConv, __bf16, true>(a, q, s);
   } else if (a_is_f32) {
     rc = 3;
   } else {
-    rc = use_glds() ? dispatch_glds<kModeTconv>(a, q, s) : dispatch_fwd_cfg<kModeTconv, __bf16, true>(a, q, s);
+    rc = dispatch_fwd_cfg<kModeTconv, __bf16, true>(a, q, s);
   }
   if (rc) return rc;
   if (nc > 0 && !skip_combine) hipLaunchKernelGGL(splitk_combine_k, dim3(nc), dim3(256), 0, s, c);
@@ -561,7 +505,7 @@ int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* o
     else return 2;
     return (int)hipGetLastError();
   }
-  if (!q.thin && !use_glds()) {
+  if (!q.thin) {
     if (x_is_f32) return 3;
     switch (q.cfg) {
       case 0: launch_wg<__bf16, true, W0>(a, q, s); break;
@@ -570,17 +514,6 @@ int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* o
       case 3: launch_wg<__bf16, true, W3>(a, q, s); break;
       case 4: launch_wg<__bf16, true, W4>(a, q, s); break;
       case 5: launch_wg<__bf16, true, W5>(a, q, s); break;
-      default: return 2;
-    }
-  } else if (!q.thin) {
-    if (x_is_f32) return 3;
-    switch (q.cfg) {
-      case 0: launch_wgg<W0, 6>(a, q, s); break;
-      case 1: launch_wgg<W1, 6>(a, q, s); break;
-      case 2: launch_wgg<W2, 6>(a, q, s); break;
-      case 3: launch_wgg<W3, 6>(a, q, s); break;
-      case 4: launch_wgg<W4, 6>(a, q, s); break;
-      case 5: launch_wgg<W5, 6>(a, q, s); break;
       default: return 2;
     }
   } else {

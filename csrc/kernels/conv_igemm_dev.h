@@ -255,33 +255,13 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, f32x4 (&acc)[TC:
 }
 
 // Register-prefetch depth of the k-loops: k-tiles whose global loads are in
-// flight while the MFMAs of the current LDS tile run. Measured on MI355X
-// (profiles/r1_conv_jobs/README.md): a 3-deep ring for small tiles / 2-deep
-// for large ones made every conv GEMM 0.4-1.4 us SLOWER (conv28 step 0.138 ->
-// 0.145 ms, conv128 0.549 -> 0.625 ms; 113-134 VGPRs instead of 64-78), so
-// the default is the single tile in flight; -DMDT_CONV_PF=N keeps the ring
-// for experiments.
-#ifndef MDT_CONV_PF
-#define MDT_CONV_PF 1
-#endif
-// k-loop barrier of the register-staged GEMMs: 0 = __syncthreads (its fence
-// waits vmcnt(0), draining the register prefetches still in flight), 1 =
-// lgkmcnt(0) + s_barrier (LDS writes visible, global prefetches stay in flight)
-#ifndef MDT_CONV_KBAR
-#define MDT_CONV_KBAR 0
-#endif
-__device__ __forceinline__ void kloop_barrier() {
-  if constexpr (MDT_CONV_KBAR == 1) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  } else {
-    __syncthreads();
-  }
-}
+// flight while the MFMAs of the current LDS tile run. One: a 3-deep ring for
+// small tiles / 2-deep for large ones measured 0.4-1.4 us SLOWER per conv GEMM
+// on MI355X (113-134 VGPRs instead of 64-78; profiles/r1_conv_jobs/README.md).
+__device__ __forceinline__ void kloop_barrier() { __syncthreads(); }
 template <int STAGE_REGS>
 constexpr int prefetch_depth() {
-  return MDT_CONV_PF > 0 ? MDT_CONV_PF : (STAGE_REGS <= 4 ? 3 : 2);
+  return 1;
 }
 template <class TC>
 constexpr int ig_prefetch() { return prefetch_depth<TC::BM / 32 + (TC::BN * 8 + 255) / 256>(); }
@@ -517,26 +497,12 @@ static __device__ __attribute__((aligned(64))) uint8_t g_zero16[64];
 // in flight every later LDS read is followed by s_waitcnt lgkmcnt(0) (a k loop
 // then waits out the reads issued for the NEXT k-step before each MFMA;
 // profiles/r2_dconv/waitcnt). The hardware counts the DMA on vmcnt only, and
-// every user waits for it explicitly (wait_tiles / dc_wait_stages) before a
+// every user waits for it explicitly (dc_wait_stages) before a
 // barrier. `lds_base` must be wave-uniform.
 __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_base) {
   const uint32_t l = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_base;
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
                ::"s"(__builtin_amdgcn_readfirstlane(l)), "v"(src) : "memory");
-}
-
-// Counted wait on this wave's outstanding LDS-DMA loads: `n` newer tiles of
-// `NI` instructions each may stay in flight.
-template <int NI, int S>
-__device__ __forceinline__ void wait_tiles(int n) {
-  static_assert(NI * (S - 2) <= 63, "vmcnt range");
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory"); break;
-    case 2: if constexpr (S >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory"); break;
-    case 3: if constexpr (S >= 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NI) : "memory"); break;
-    default: if constexpr (S >= 6) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NI) : "memory"); break;
-  }
 }
 
 // Workgroup barrier that neither drains the LDS-DMA queue (unlike
@@ -546,140 +512,6 @@ __device__ __forceinline__ void stage_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-}
-
-// Forward-type GEMM with an S-stage LDS ring filled by global_load_lds
-// (bf16 vector gathers only): S-1 k-tiles are in flight while one is
-// multiplied, with no staging registers. The per-lane global address does
-// the im2col gather AND the XOR swizzle (the LDS side of a DMA is lane-linear).
-template <int MODE, class TC, int S>
-__global__ void __launch_bounds__(256) igemm_glds_k(IgArgs a) {
-  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
-  constexpr int BR = BN < 32 ? 32 : BN;         // staged B rows (>= one DMA row group per wave)
-  constexpr int A_CH = BM / 32, B_CH = BR / 32;  // DMA instructions per wave per tile
-  constexpr int NI = A_CH + B_CH;
-  constexpr int A_BYTES = BM * 128, STAGE = (BM + BR) * 128;
-  static_assert(TC::RED_BYTES + WM * BN * 4 <= S * STAGE, "epilogue scratch exceeds LDS");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[S * STAGE];
-
-  const ConvDesc& d = a.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = tile / a.ntiles, nt = tile - mt * a.ntiles;
-  const int kz = blockIdx.y, cls = blockIdx.z;
-  const int kt0 = kz * a.kt_per_split;
-  const int nk = min(a.ktiles, kt0 + a.kt_per_split) - kt0;
-
-  int ea = 0, eb = 0, oa = 0, ob = 0;
-  if constexpr (MODE == kModeTconv) {
-    const int ca = cls / d.S, cb = cls - ca * d.S;
-    oa = ((ca - d.P) % d.S + d.S) % d.S;
-    ob = ((cb - d.P) % d.S + d.S) % d.S;
-    ea = (oa + d.P - ca) / d.S;
-    eb = (ob + d.P - cb) / d.S;
-  }
-  // lane-linear DMA: lane l of wave w fills row 32i + 8w + (l>>3), slot l&7,
-  // which must hold logical chunk slot ^ (row & 7)
-  const int ach = (tid & 7) ^ ((tid >> 3) & 7);
-  int abase[A_CH], ay[A_CH], ax[A_CH];
-  bool aok[A_CH];
-#pragma unroll
-  for (int i = 0; i < A_CH; ++i) {
-    const int m = mt * BM + (tid >> 3) + 32 * i;
-    aok[i] = m < a.M;
-    const uint32_t mm = aok[i] ? (uint32_t)m : 0u;
-    const uint32_t n = fdiv(mm, a.f_pix);
-    const uint32_t rem = mm - n * a.f_pix.d;
-    const uint32_t yy = fdiv(rem, a.f_w);
-    const uint32_t xx = rem - yy * a.f_w.d;
-    if constexpr (MODE == kModeConv) {
-      abase[i] = (int)n * d.H * d.W * d.C;
-      ay[i] = (int)yy * d.S - d.P;
-      ax[i] = (int)xx * d.S - d.P;
-    } else {
-      abase[i] = (int)n * d.OH * d.OW * d.CO;
-      ay[i] = (int)yy + ea;
-      ax[i] = (int)xx + eb;
-    }
-  }
-  const __bf16* Ap = reinterpret_cast<const __bf16*>(a.A);
-  const __bf16* Bc = a.B + (size_t)cls * a.Ncols * a.K;
-
-  auto issue = [&](int kt, int buf) {
-    uint8_t* As = lds + buf * STAGE;
-    uint8_t* Bs = As + A_BYTES;
-    const int kk = kt * 64 + 8 * ach;
-    const uint32_t tap = fdiv((uint32_t)kk, a.f_ch);
-    const int ch = kk - (int)(tap * a.f_ch.d);
-    const uint32_t t0 = fdiv(tap, a.f_tw);
-    const int t1 = (int)(tap - t0 * a.f_tw.d);
-    const bool kok = kk < a.K;
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      int off;
-      bool ok;
-      if constexpr (MODE == kModeConv) {
-        const int iy = ay[i] + (int)t0, ix = ax[i] + t1;
-        ok = aok[i] && kok && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-        off = abase[i] + (iy * d.W + ix) * d.C + ch;
-      } else {
-        const int oy = ay[i] - (int)t0, ox = ax[i] - t1;
-        ok = aok[i] && kok && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
-        off = abase[i] + (oy * d.OW + ox) * d.CO + ch;
-      }
-      glds16(ok ? (const void*)(Ap + off) : (const void*)g_zero16, As + (32 * i + 8 * w) * 128);
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      const int col = nt * BN + r;
-      const bool ok = r < BN && col < a.Ncols && kk < a.K;
-      glds16(ok ? (const void*)(Bc + (size_t)col * a.K + kk) : (const void*)g_zero16, Bs + (32 * i + 8 * w) * 128);
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const uint8_t* As = lds + buf * STAGE;
-    const uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2 / KWS; ++s) {
-      const int ks = KWS == 2 ? wk : s;
-      const int ch = ks * 4 + (lane >> 4);
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-        af[fm] = *reinterpret_cast<const bf16x8*>(As + rimg(wm * (BM / WM) + fm * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn)
-        bfr[fn] = *reinterpret_cast<const bf16x8*>(Bs + rimg(wn * (BN / WN) + fn * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
-    }
-  };
-
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(kt0 + s, s);
-  for (int it = 0; it < nk; ++it) {
-    const int newer = min(nk - 1 - it, S - 2);
-    wait_tiles<NI, S>(newer);
-    stage_barrier();
-    if (it + S - 1 < nk) issue(kt0 + it + S - 1, (it + S - 1) % S);
-    compute(it % S);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  stage_barrier();
-  igemm_epilogue<MODE, TC>(a, acc, lds, mt, nt, kz, cls, oa, ob);
 }
 
 // ================================================================= wgrad ====
@@ -897,116 +729,6 @@ __global__ void __launch_bounds__(256) wgrad_k(WgArgs a) {
   wgrad_body<XT, VEC, TC>(a, lds, blockIdx.x, gridDim.x);
 }
 
-// Weight-gradient GEMM with an S-stage LDS-DMA ring (bf16 inputs, C % 8 == 0).
-// Both m-major images are filled lane-linearly; the tr_b16 XOR swizzle is
-// applied on the source side (lane slot p holds logical chunk p ^ trsw(row)).
-template <class TC, int S>
-__global__ void __launch_bounds__(256) wgrad_glds_k(WgArgs a) {
-  constexpr int BM = TC::BM, BN = TC::BN, WM = TC::WM, WN = TC::WN, KWS = TC::KWS, FM = TC::FM, FN = TC::FN;
-  constexpr int CPR_A = BM / 8, A_RPP = 256 / CPR_A, A_CH = 64 / A_RPP;
-  constexpr int CPR_B = BN / 8, B_RPP = 256 / CPR_B, B_CH = (64 + B_RPP - 1) / B_RPP;
-  constexpr int NI = A_CH + B_CH;
-  constexpr int A_BYTES = 64 * BM * 2;
-  constexpr int B_BYTES = (B_RPP * B_CH) * BN * 2;  // rows past 64 only absorb zero DMAs
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  static_assert(TC::RED_BYTES <= S * STAGE, "reduction scratch exceeds LDS");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[S * STAGE];
-
-  const ConvDesc& d = a.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = w / (WM * WN), wm = (w % (WM * WN)) / WN, wn = w % WN;
-  // 1-D grid, split-major after the XCD remap: an XCD owns a contiguous
-  // m-range for ALL (co, k') tiles, so its slice of G and X is fetched into
-  // its L2 once instead of once per tile.
-  const int wid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntile = a.cotiles * a.ktiles;
-  const int split = wid / ntile;
-  const int tile = wid - split * ntile;
-  const int ct = tile / a.ktiles, nt = tile - ct * a.ktiles;
-  const int mt0 = split * a.mt_per_split;
-  const int nk = min(a.mtiles, mt0 + a.mt_per_split) - mt0;
-
-  const int rA0 = tid / CPR_A, rB0 = tid / CPR_B;
-  const int cA = (tid % CPR_A) ^ trsw<BM>(rA0);
-  const int cB = (tid % CPR_B) ^ trsw<BN>(rB0);
-  const int co = ct * BM + 8 * cA;
-  const bool coka = co < d.CO;
-  const int kp = nt * BN + 8 * cB;
-  const bool kokb = kp < a.K2;
-  const uint32_t tap = fdiv((uint32_t)(kokb ? kp : 0), a.f_c);
-  const int ci = (kokb ? kp : 0) - (int)(tap * a.f_c.d);
-  const uint32_t kyu = fdiv(tap, a.f_kw);
-  const int ky = (int)kyu, kx = (int)(tap - kyu * a.f_kw.d);
-  const __bf16* Xp = reinterpret_cast<const __bf16*>(a.X);
-  const int HWC = d.H * d.W * d.C;
-
-  auto issue = [&](int mtile, int buf) {
-    uint8_t* As = lds + buf * STAGE;
-    uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const int m = mtile * 64 + rA0 + A_RPP * i;
-      const bool ok = coka && m < a.M;
-      glds16(ok ? (const void*)(a.G + (size_t)m * d.CO + co) : (const void*)g_zero16,
-             As + (A_RPP * i + w * (64 / CPR_A)) * (BM * 2));
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int r = rB0 + B_RPP * i;
-      const int m = mtile * 64 + r;
-      const bool mok = r < 64 && m < a.M;
-      const uint32_t mm = mok ? (uint32_t)m : 0u;
-      const uint32_t n = fdiv(mm, a.f_pix);
-      const uint32_t rem = mm - n * a.f_pix.d;
-      const uint32_t oy = fdiv(rem, a.f_w);
-      const uint32_t ox = rem - oy * a.f_w.d;
-      const int iy = (int)oy * d.S - d.P + ky, ix = (int)ox * d.S - d.P + kx;
-      const bool ok = mok && kokb && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-      glds16(ok ? (const void*)(Xp + (int)n * HWC + (iy * d.W + ix) * d.C + ci) : (const void*)g_zero16,
-             Bs + (B_RPP * i + w * (64 / CPR_B)) * (BN * 2));
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const uint8_t* As = lds + buf * STAGE;
-    const uint8_t* Bs = As + A_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2 / KWS; ++s) {
-      const int kb = 32 * (KWS == 2 ? wk : s);
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm) af[fm] = tr_frag<BM>(As, wm * (BM / WM) + 16 * fm, kb, lane);
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) bfr[fn] = tr_frag<BN>(Bs, wn * (BN / WN) + 16 * fn, kb, lane);
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma_bf16(af[fm], bfr[fn], acc[fm][fn]);
-    }
-  };
-
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(mt0 + s, s);
-  for (int it = 0; it < nk; ++it) {
-    const int newer = min(nk - 1 - it, S - 2);
-    wait_tiles<NI, S>(newer);
-    stage_barrier();
-    if (it + S - 1 < nk) issue(mt0 + it + S - 1, (it + S - 1) % S);
-    compute(it % S);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  stage_barrier();
-  wgrad_epilogue<TC>(a, acc, lds, ct, nt, split);
-}
-
 // ======================================================= small reductions ====
 // Split-K combine: y = sum_z slab[z] + bias (+relu) -> f32 and/or bf16.
 // `cnt` outputs per block, 256/cnt threads per output summing interleaved
@@ -1095,7 +817,6 @@ bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p, bool al
 int direct_cfg(int mode, const ConvDesc& d, bool fwd);
 int dwgrad_cfg(const ConvDesc& d);
 bool plan_wgrad(const ConvDesc& d, WgradPlan* p);
-bool use_glds();
 // Kernel arguments of one forward-type GEMM; with split-K (q->ksplit > 1) `c`
 // receives the combine pass (nc = its block count), else nc = 0.
 int build_igemm(int mode, const void* A, const void* B16, ConvDesc d, const float* bias, int relu, void* y16,

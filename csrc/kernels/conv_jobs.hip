@@ -134,22 +134,6 @@ struct JobPackN {
   JobBlob j[kMaxMultiJobs];
   int start[kMaxMultiJobs + 1];
   int n;
-  // Optional in-launch hand-off from the weight-gradient jobs to a finalize
-  // job (the fused 28x28 step's launch 2): job `fin` (the LAST job, so its
-  // workgroups have the highest ids and are dispatched after every block
-  // they wait for) owns one finalize unit per block; a unit whose segment is
-  // a weight waits until every block of its layer's weight-gradient job has
-  // arrived on tickets[job], then runs the same finalize + Adam body as the
-  // stand-alone grad_finalize_k (bitwise identical result). The finalize of a
-  // layer thus overlaps the other layers' weight gradients instead of waiting
-  // for a kernel boundary behind the slowest one.
-  int fin;                     // finalize job index, -1: no hand-off
-  int first;                   // job every finalize unit waits for first (the loss / step-advance job
-                               // that writes the Adam bias-correction products), -1 none
-  int arrive[kMaxMultiJobs];   // 1: job i's blocks arrive on tickets[i]
-  int waiters[kMaxMultiJobs];  // finalize units that wait for job i
-  int* tickets;                // device int[2 * kMaxMultiJobs + 1]: arrivals, passed waiters, timeout flag
-  const int* unit_wait;        // per finalize unit: job index to wait for, -1 none
 };
 
 constexpr int kMultiLds = cmax(cmax(cmax(wgrad_lds_bytes<W0>(), wgrad_lds_bytes<W1>()),
@@ -192,55 +176,13 @@ __device__ __forceinline__ void run_multi_job(const JobBlob& j, uint8_t* lds, in
 // makes the compiler copy the whole 2.4 KB pack into per-lane scratch
 // (measured 2368 B/lane, the launch ~10x slower), and selecting it with
 // constant indices inlines every body eight times (1100+ SGPR spills).
-// Ticket wait of a finalize unit (thread 0 spins with acquire loads and
-// s_sleep back-off, bounded: tickets[2 * kMaxMultiJobs] = 1 flags a timeout
-// instead of hanging); the last waiter of job t resets its two counters for
-// the next launch (graph replays included).
-__device__ __forceinline__ void multi_wait1(const JobPackN* __restrict__ p, int t) {
-  int* tk = p->tickets;
-  const int need = p->j[t].nblk;
-  int it = 0;
-  // relaxed polls (an acquire load per poll invalidates this CU's caches every
-  // time -- measured 0.34 ms/step instead of 0.072 with ~100 polling units);
-  // the acquire is the single fence in multi_wait after the loop
-  while (__hip_atomic_load(tk + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-    if (++it > (1 << 20)) {
-      __hip_atomic_store(tk + 2 * kMaxMultiJobs, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  if (__hip_atomic_fetch_add(tk + kMaxMultiJobs + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-      p->waiters[t] - 1) {
-    __hip_atomic_store(tk + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(tk + kMaxMultiJobs + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__device__ __forceinline__ void multi_wait(const JobPackN* __restrict__ p, int t0, int t1) {
-  if (threadIdx.x == 0) {
-    if (t0 >= 0) multi_wait1(p, t0);
-    if (t1 >= 0) multi_wait1(p, t1);
-  }
-  __syncthreads();
-  __threadfence();  // acquire for every wave: the awaited jobs' stores are visible
-}
-
 __global__ void __launch_bounds__(256) jobs_multi_k(const JobPackN* __restrict__ p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kMultiLds];
   const int b = blockIdx.x;
   const int n = p->n;
   int i = 0;
   while (i + 1 < n && b >= p->start[i + 1]) ++i;
-  const int lb = b - p->start[i];
-  const int fin = p->fin;
-  if (i == fin) multi_wait(p, p->first, p->unit_wait[lb]);
-  run_multi_job(p->j[i], lds, lb);
-  if (fin >= 0 && i != fin && p->arrive[i]) {
-    __threadfence();  // every wave releases its slab stores (agent scope: other XCDs' L2s)
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(p->tickets + i, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  run_multi_job(p->j[i], lds, b - p->start[i]);
 }
 
 __host__ inline bool multi_kind_ok(int k) {
@@ -257,57 +199,6 @@ __global__ void __launch_bounds__(256) jobs_k(JobPack p) {
   if (b < p.start1) A::run(p.j[0], lds, b);
   else if (b < p.start2) B::run(p.j[1], lds, b - p.start1);
   else C::run(p.j[2], lds, b - p.start2);
-}
-
-// The optimizer tail as ONE launch. Blocks [0, start1) compute the first
-// layer's weight-gradient partial slabs (job 0) and then arrive on a device
-// ticket (release). Blocks [start1, start2) finalize + Adam the other layers
-// that are still pending (job 2). Blocks [start2, grid) -- the highest block
-// ids, so the dispatcher places every weight-gradient block before them --
-// each own one of the first layer's finalize units (job 1): one thread waits
-// (acquire, s_sleep back-off, bounded: ticket[2] = 1 flags a timeout instead of
-// hanging) until all weight-gradient blocks have arrived, then the block runs
-// the same finalize body as the stand-alone launch (bitwise identical). The
-// grid (a few hundred blocks) is far below the chip's resident capacity, so
-// the waiting blocks never keep an arriving block from running. The last
-// waiter resets the ticket for the next launch (graph replays included).
-// This replaces "wgrad0 || finalize(1..L)" followed by a separate
-// "finalize(0) || transposes" launch; the transposed weight copies move to
-// the next step's first launch (models/conv_vae.py, `_tail1_active`).
-// ticket: int32 [3] = {arrived, waiters passed, timeout flag}.
-template <class W>
-__global__ void __launch_bounds__(256) tail_k(JobPack p, int* ticket) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[cmax(W::LDS, JFinalize::LDS)];
-  const int b = blockIdx.x;
-  if (b < p.start1) {
-    W::run(p.j[0], lds, b);
-    __threadfence();  // every wave releases its slab stores (agent scope: other XCDs' L2s)
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if (b < p.start2) {
-    JFinalize::run(p.j[2], lds, b - p.start1);
-    return;
-  }
-  if (threadIdx.x == 0) {
-    int it = 0;
-    while (__hip_atomic_load(ticket, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < p.start1) {
-      if (++it > (1 << 20)) {  // ~50 ms: never reached unless the ticket protocol is broken
-        __hip_atomic_store(ticket + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    const int waiters = (int)gridDim.x - p.start2;
-    if (__hip_atomic_fetch_add(ticket + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == waiters - 1) {
-      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ticket + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  __threadfence();  // acquire for every wave: all weight-gradient slabs are visible
-  JFinalize::run(p.j[1], lds, b - p.start2);
 }
 
 }  // namespace mdt
@@ -376,7 +267,7 @@ const Combo kCombos[] = {
     COMBO2(IgT2, Wg0),
     COMBO2(IgT5, Wg0),
     // backward-data || weight gradient || finalize+Adam of the layers whose
-    // gradients the previous launches completed (spread optimizer, tail1 mode)
+    // gradients the previous launches completed (spread optimizer)
     COMBO3(IgC1, Wg0, JFinalize),
     COMBO3(IgC4, Wg0, JFinalize),
     COMBO3(IgC5, Wg0, JFinalize),
@@ -390,7 +281,7 @@ const Combo kCombos[] = {
     COMBO2(WgT5f, JFinalize),
     COMBO2(JFinalize, JWtrans),
     // step's first launch (batch gather + step begin + first layer) || the
-    // transposed weight copies the previous step's one-launch tail left out
+    // transposed weight copies of the previous step's update (MDT_CONV_DEFER_WT=1)
     COMBO2(ThinC32f, JWtrans),
     // ... or the first decoder GEMM (MDT_CONV_DEFER_WT=2)
     COMBO2(IgC1, JWtrans),
@@ -430,7 +321,7 @@ int mdt_job_igemm(JobBlob* g, JobBlob* c, int mode, const void* A, int a_is_f32,
   memset(c, 0, sizeof(*c));
   // direct-kernel geometries have no job form yet: kind 0 sends the caller
   // to mdt_igemm (their column-sum rows follow the direct plan)
-  const bool ok = !a_is_f32 && !q.thin && !use_glds() && direct_cfg(mode, d, false) < 0;
+  const bool ok = !a_is_f32 && !q.thin && direct_cfg(mode, d, false) < 0;
   g->kind = ok ? kJobIgemm + mode * 100 + q.cfg : 0;
   g->nblk = q.mtiles * q.ntiles * q.ksplit * q.classes;
   g->aux[0] = q.mtiles * q.ntiles;
@@ -451,7 +342,7 @@ int mdt_job_wgrad(JobBlob* j, const void* G16, const void* X, int x_is_f32, Conv
   memset(j, 0, sizeof(*j));
   if (q.cfg == 110) j->kind = kJobThinWgM + (x_is_f32 ? 1 : 0);  // MFMA thin weight gradient
   else if (q.cfg >= 100) j->kind = 0;  // direct weight gradient (conv_dwgrad.h): its own launch
-  else if (!q.thin) j->kind = (x_is_f32 || use_glds()) ? 0 : kJobWgrad + q.cfg;
+  else if (!q.thin) j->kind = x_is_f32 ? 0 : kJobWgrad + q.cfg;
   else j->kind = kJobWgradThin + (x_is_f32 ? 20 : 0) + q.cfg;
   j->nblk = q.cotiles * q.ktiles * q.nsplit;
   put_args(j, a);
@@ -544,72 +435,15 @@ int mdt_launch_jobs(const JobBlob* jobs, int n, hipStream_t s) {
   return 1;
 }
 
-// One-launch optimizer tail (tail_k): `wg` = the first layer's weight
-// gradient, `fin0` = its finalize units (run by the last wgrad block),
-// `finr` = finalize of the other layers not finalized yet (may be empty:
-// nblk 0, when the backward sweep finalized them in its own launches). Returns 1 (nothing launched) when
-// the kinds have no instantiation.
-int mdt_launch_tail(const JobBlob* wg, const JobBlob* fin0, const JobBlob* finr, int* ticket, hipStream_t s) {
-  if (!ticket || wg->nblk <= 0 || fin0->nblk <= 0 || finr->nblk < 0) return 2;
-  if (fin0->kind != kJobFinalize || (finr->nblk > 0 && finr->kind != kJobFinalize)) return 1;
-  JobPack p;
-  memset(&p, 0, sizeof(p));
-  p.j[0] = *wg;
-  p.j[1] = *fin0;
-  p.j[2] = *finr;
-  p.start1 = wg->nblk;
-  p.start2 = wg->nblk + finr->nblk;
-  const int grid = p.start2 + fin0->nblk;
-  if (wg->kind == WgT5f::ID) hipLaunchKernelGGL((tail_k<WgT5f>), dim3(grid), dim3(256), 0, s, p, ticket);
-  else if (wg->kind == WgT5::ID) hipLaunchKernelGGL((tail_k<WgT5>), dim3(grid), dim3(256), 0, s, p, ticket);
-  else return 1;
-  return (int)hipGetLastError() ? -1 : 0;
-}
-
 // Pack 1..kMaxMultiJobs jobs of any supported kinds into a JobPackN image at
 // `dst` (host memory, mdt_jobs_multi_bytes() bytes; the caller uploads it once).
 // Returns the grid size, 0 for an unsupported kind, -1 for bad input.
 int mdt_jobs_multi_bytes() { return (int)sizeof(JobPackN); }
 
-int mdt_pack_jobs_multi_fin(const JobBlob* jobs, int n, void* dst, int fin, int first, const int* unit_wait_host,
-                            const int* unit_wait_dev, int* tickets);
-
 int mdt_pack_jobs_multi(const JobBlob* jobs, int n, void* dst) {
-  return mdt_pack_jobs_multi_fin(jobs, n, dst, -1, -1, nullptr, nullptr, nullptr);
-}
-
-// fin >= 0: job `fin` must be the last job and a finalize job with one unit
-// per block; unit_wait_host / unit_wait_dev (same contents, host copy for
-// validation) name per unit the weight-gradient job it waits for (-1 none);
-// first (>= 0): a job every unit waits for before its own (the loss / step
-// advance job whose state the Adam constants read); tickets: zeroed device
-// int[2 * kMaxMultiJobs + 1].
-int mdt_pack_jobs_multi_fin(const JobBlob* jobs, int n, void* dst, int fin, int first, const int* unit_wait_host,
-                            const int* unit_wait_dev, int* tickets) {
   if (n < 1 || n > kMaxMultiJobs) return -1;
   JobPackN p;
   memset(&p, 0, sizeof(p));
-  p.fin = -1;
-  p.first = -1;
-  if (fin >= 0) {
-    if (fin != n - 1 || jobs[fin].kind != kJobFinalize || !unit_wait_host || !unit_wait_dev || !tickets) return -1;
-    if (first >= fin || (first >= 0 && jobs[first].kind != kJobLossStep && jobs[first].kind != kJobLoss)) return -1;
-    if (first >= 0) p.waiters[first] = jobs[fin].nblk;
-    p.first = first;
-    for (int u = 0; u < jobs[fin].nblk; ++u) {
-      const int t = unit_wait_host[u];
-      if (t < -1 || t >= fin || (t >= 0 && t == first)) return -1;
-      if (t >= 0) {
-        const int k = jobs[t].kind;
-        if (!((k >= kJobWgrad && k <= kJobWgrad + 5) || (k >= kJobWgradThin && k <= kJobWgradThin + 25))) return -1;
-        p.waiters[t] += 1;
-      }
-    }
-    for (int i = 0; i < fin; ++i) p.arrive[i] = p.waiters[i] > 0;
-    p.fin = fin;
-    p.tickets = tickets;
-    p.unit_wait = unit_wait_dev;
-  }
   int grid = 0;
   for (int i = 0; i < n; ++i) {
     if (jobs[i].nblk <= 0) return -1;

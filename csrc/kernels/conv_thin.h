@@ -49,7 +49,7 @@ struct ThinConvArgs {
   int B;
   float* xb;
   int nblk;
-  int mfma;            // 1: thin_conv_mfma_body (host: thin_conv_mfma_ok), 2: VALU with SGPR weights
+  int mfma;            // 1: thin_conv_mfma_body (host: thin_conv_mfma_ok)
 };
 
 // Geometry of the MFMA form of thin_conv (the 128x128 model's enc1 and its
@@ -57,10 +57,8 @@ struct ThinConvArgs {
 // output rows per 256-pixel workgroup (bit 1 of MDT_THIN_MFMA below).
 // MDT_THIN_MFMA: bit mask of the MFMA edge-layer forms in use: 1 thin conv
 // with f32 input (enc1 forward), 8 thin conv with bf16 input (last layer's
-// backward-data), 2 transposed conv + BCE, 4 weight gradients, 16 VALU thin
-// conv with SGPR weights (any geometry, bitwise equal to the LDS form, but
-// measured slower: enc1 16.7 vs 15.2 us, conv28 layer path 0.1167 vs 0.1137
-// ms -- opt-in); 0 keeps every VALU / im2col body with LDS weights. Default
+// backward-data), 2 transposed conv + BCE, 4 weight gradients; 0 keeps every
+// VALU / im2col body with LDS weights. Default
 // 14; bits 2, 4, 8: they leave the model-level
 // gradients exactly as close to the bf16-emulating f64 reference as the VALU
 // kernels (profiles/r2_thin/ab_mask); bit 1 is ~6 us faster per 128x128 step
@@ -81,12 +79,11 @@ __host__ inline bool thin_mfma_geom(const ConvDesc& d) {
 }
 
 // bit 1: f32 input (enc1 forward), bit 8: bf16 input (last layer's backward-data).
-// Returns the body selector of ThinConvArgs::mfma: 1 = MFMA form, 2 = VALU
-// body with the weights as SGPR operands (bit 16, default on), 0 = VALU body
-// with LDS-broadcast weights.
+// Returns the body selector of ThinConvArgs::mfma: 1 = MFMA form, 0 = VALU
+// body with LDS-broadcast weights (a VALU form with the weights as SGPR
+// operands measured slower: enc1 16.7 vs 15.2 us).
 __host__ inline int thin_conv_mfma_ok(const ConvDesc& d, int x_is_f32) {
-  if ((thin_mfma_mask() & (x_is_f32 ? 1 : 8)) && thin_mfma_geom(d)) return 1;
-  return (thin_mfma_mask() & 16) ? 2 : 0;
+  return (thin_mfma_mask() & (x_is_f32 ? 1 : 8)) && thin_mfma_geom(d) ? 1 : 0;
 }
 
 
@@ -148,19 +145,7 @@ __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* 
   float acc[CO];
 #pragma unroll
   for (int c = 0; c < CO; ++c) acc[c] = bias ? bias[c] : 0.f;
-  if (ta.mfma == 2) {
-    // weights as SGPR operands: the [co][16 taps] f32 rows are wave-uniform
-    // and read-only here, so they are read through the constant address
-    // space (s_load_dwordx16, one co row per load) instead of the LDS
-    // broadcasts below (an LDS instruction costs the same for one address as
-    // for 64). Same per-channel FMA chain over t = 0..15: bitwise identical.
-    typedef const __attribute__((address_space(4))) float cfloat;
-    const cfloat* Wk = (const cfloat*)Wf;
-#pragma unroll
-    for (int c = 0; c < CO; ++c)
-#pragma unroll
-      for (int t = 0; t < TAPS; ++t) acc[c] = fmaf(xin[t], Wk[c * TAPS + t], acc[c]);
-  } else {
+  {
     // weights staged once per block in LDS as [tap][co]; the FMA loop reads
     // them with wave-uniform (broadcast) ds_read_b128, 4 channels per read
     for (int e = threadIdx.x; e < TAPS * CO; e += blockDim.x) {
@@ -328,126 +313,17 @@ __device__ __forceinline__ void thin_tconv_body(const ThinTconvArgs& ta, uint8_t
 }
 
 
-// k4/s2/p1 transposed conv with C_out = 1 (the VAE's last layer), one thread
-// per INPUT position (n, j, i): it produces the 2x2 output block rows 2j..2j+1,
-// cols 2i..2i+1 -- one pixel of each stride-parity class -- from the 3x3 input
-// neighbourhood, so every input chunk is read 9/4 times per output instead of
-// 4 times (per-class kernel above), and the output / target rows move as
-// 8-byte pairs. All 16 taps x CO weights are staged in LDS ([class][tap][co],
-// wave-uniform broadcast reads). Same fused BCE / dlogits / partials.
-template <int CO>
-constexpr int thin_tconv4_lds_bytes() { return (16 + 16 * CO) * 4; }
-
-template <int CO>
-__device__ __forceinline__ void thin_tconv4_body(const ThinTconvArgs& ta, uint8_t* lds, int bid) {
-  const ConvDesc& d = ta.d;
-  float* scratch = reinterpret_cast<float*>(lds);
-  float* wl = scratch + 16;
-  const int HS = d.H / 2, WS = d.W / 2;
-  const int Mc = d.N * HS * WS;
-  const int m = bid * blockDim.x + threadIdx.x;
-  const bool live = m < Mc;
-  const int mm = live ? m : 0;
-  const int n = mm / (HS * WS);
-  const int rem = mm - n * HS * WS;
-  const int j = rem / WS, i = rem - j * WS;
-  // weights [((ca*2 + cb)*2 + ty)*2 + tx][co]: tap (ky, kx) = (ca + 2ty, cb + 2tx)
-  for (int e = threadIdx.x; e < 16 * CO; e += blockDim.x) {
-    const int tap = e / CO, c = e - tap * CO;
-    const int ca = tap >> 3, cb = (tap >> 2) & 1, ty = (tap >> 1) & 1, tx = tap & 1;
-    wl[e] = ta.Wf[(c * 4 + ca + 2 * ty) * 4 + cb + 2 * tx];
-  }
-  __syncthreads();
-  const float b0 = ta.bias ? ta.bias[0] : 0.f;
-  float acc[2][2] = {{b0, b0}, {b0, b0}};
-  const __bf16* Gn = ta.G + (size_t)n * d.OH * d.OW * CO;
-#pragma unroll
-  for (int c8 = 0; c8 < CO / 8; ++c8) {
-    float g[3][3][8];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int oy = j - 1 + r, ox = i - 1 + c;
-        const bool ok = live && (unsigned)oy < (unsigned)d.OH && (unsigned)ox < (unsigned)d.OW;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(Gn + ((size_t)(ok ? oy : 0) * d.OW + (ok ? ox : 0)) * CO +
-                                                          8 * c8);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) g[r][c][q] = ok ? (float)v[q] : 0.f;
-      }
-#pragma unroll
-    for (int ca = 0; ca < 2; ++ca)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int ty = 0; ty < 2; ++ty)
-#pragma unroll
-          for (int tx = 0; tx < 2; ++tx) {
-            // p = 1: class ca reads input rows j + (1 - ca) - ty
-            const int r = (1 - ca) - ty + 1, c = (1 - cb) - tx + 1;
-            const float* w = wl + (((ca * 2 + cb) * 2 + ty) * 2 + tx) * CO + 8 * c8;
-            const float4 w0 = *reinterpret_cast<const float4*>(w), w1 = *reinterpret_cast<const float4*>(w + 4);
-            float a = acc[ca][cb];
-            a = fmaf(g[r][c][0], w0.x, a); a = fmaf(g[r][c][1], w0.y, a);
-            a = fmaf(g[r][c][2], w0.z, a); a = fmaf(g[r][c][3], w0.w, a);
-            a = fmaf(g[r][c][4], w1.x, a); a = fmaf(g[r][c][5], w1.y, a);
-            a = fmaf(g[r][c][6], w1.z, a); a = fmaf(g[r][c][7], w1.w, a);
-            acc[ca][cb] = a;
-          }
-  }
-  // class ca -> output row 2j + (1 - ca); class cb -> column 2i + (1 - cb)
-  float loss = 0.f, gsum = 0.f;
-#pragma unroll
-  for (int ca = 0; ca < 2; ++ca) {
-    const int iy = 2 * j + (1 - ca);
-    const size_t e = ((size_t)n * d.H + iy) * d.W + 2 * i;
-    const float t0 = acc[ca][1], t1 = acc[ca][0];  // columns 2i, 2i+1
-    if (live && ta.y32) *reinterpret_cast<float2*>(ta.y32 + e) = make_float2(t0, t1);
-    if (ta.X && live) {
-      const float2 x2 = *reinterpret_cast<const float2*>(ta.X + e);
-      const float tv[2] = {t0, t1}, xv[2] = {x2.x, x2.y};
-      float pv[2], gv[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const float t = tv[u], x = xv[u];
-        const float p = 1.f / (1.f + expf(-t));
-        pv[u] = p;
-        gv[u] = p - x;
-        const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));
-        loss += x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
-        gsum += gv[u];
-      }
-      if (ta.dlog) {
-        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-        bf16x2 g2;
-        g2[0] = (__bf16)gv[0];
-        g2[1] = (__bf16)gv[1];
-        *reinterpret_cast<bf16x2*>(ta.dlog + e) = g2;
-      }
-      if (ta.recon) *reinterpret_cast<float2*>(ta.recon + e) = make_float2(pv[0], pv[1]);
-    }
-  }
-  if (ta.X) {
-    const float sl = block_sum(loss, scratch);
-    if (threadIdx.x == 0) ta.part[bid] = sl;
-    if (ta.gpart) {
-      __syncthreads();
-      const float gs = block_sum(gsum, scratch);
-      if (threadIdx.x == 0) ta.gpart[bid] = gs;
-    }
-  }
-}
-
-// Halo-patch variant of thin_tconv4 (the default where it applies: CO = 32,
-// class grid WS columns with WS | 256). One workgroup = one image's R = 256 / WS
-// class-grid rows x all WS columns, one thread per class pixel (all four
-// parity outputs). The (R+2) x (WS+2) x CO bf16 neighbourhood is staged in LDS
+// k4/s2/p1 transposed conv with C_out = 1 (the VAE's last layer) where CO = 32
+// and the class grid has WS columns with WS | 256: one workgroup = one image's
+// R = 256 / WS class-grid rows x all WS columns, one thread per class pixel
+// producing its 2x2 output block (one pixel of each stride-parity class) from
+// the 3x3 input neighbourhood. The (R+2) x (WS+2) x CO bf16 neighbourhood is staged in LDS
 // once with contiguous 16-B row loads (zero padding materialised), instead of
 // every thread gathering its own 3x3 neighbourhood through the TA (each input
 // chunk 9/4 times: 151 MB of 16-B gathers per 128x128 B=64 step, TA-bound at
 // ~25 us). Chunk q of slot x sits at q ^ ((x >> 2) & 3): the 16 consecutive
-// slots a lane group reads land on 16 different bank groups. Same arithmetic
-// order as thin_tconv4_body, same fused BCE / dlogits / partials.
+// slots a lane group reads land on 16 different bank groups. Same fused
+// BCE / dlogits / partials as the per-class kernel.
 template <int CO, int WS>
 constexpr int thin_tconv_patch_lds_bytes() { return (256 / WS + 2) * (WS + 2) * CO * 2 + (16 * CO + 16) * 4; }
 

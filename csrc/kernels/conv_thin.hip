@@ -26,12 +26,6 @@ __global__ void __launch_bounds__(256) thin_conv_k(ThinConvArgs ta) {
   thin_conv_body<CO, K, TIN>(ta, lds, blockIdx.x);
 }
 
-template <int CO>
-__global__ void __launch_bounds__(256) thin_tconv4_k(ThinTconvArgs ta) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[thin_tconv4_lds_bytes<CO>()];
-  thin_tconv4_body<CO>(ta, lds, blockIdx.x);
-}
-
 template <int CO, int WS>
 __global__ void __launch_bounds__(256) thin_tconv_patch_k(ThinTconvArgs ta) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[thin_tconv_patch_lds_bytes<CO, WS>()];
@@ -86,20 +80,6 @@ int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, cons
   return (int)hipGetLastError();
 }
 
-// blocks of the per-block partial outputs (colsum rows for thin_conv,
-// loss partials for thin_tconv)
-// Opt-in (MDT_THIN_TCONV4=1): measured SLOWER on MI355X than the per-class
-// kernel (conv28 step +1.7 us, conv128 +10 us): a quarter of the threads, each
-// with a 4x longer dependent FMA chain, hides less load latency than the 4x
-// re-read costs (profiles/r1_knobs/ab7_thin_tconv4.txt).
-static bool tconv4_ok(const ConvDesc& d) {
-  static const bool on = [] {
-    const char* e = getenv("MDT_THIN_TCONV4");
-    return e && e[0] == '1';
-  }();
-  return on && d.KH == 4 && d.KW == 4 && d.S == 2 && d.P == 1;
-}
-
 // Halo-patch kernel (thin_tconv_patch_body): CO = 32, square 4x4/s2/p1, class
 // grid width 64 (the 128x128 model's last layer). MDT_THIN_PATCH=0 disables.
 static bool tconv_patch_ok(const ConvDesc& d) {
@@ -115,10 +95,11 @@ static bool tconv_patch_ok(const ConvDesc& d) {
 // partials): bit 2 of MDT_THIN_MFMA (conv_thin.h thin_mfma_mask).
 static bool thin_mfma_on() { return (thin_mfma_mask() & 2) != 0; }
 
+// blocks of the per-block partial outputs (colsum rows for thin_conv,
+// loss partials for thin_tconv)
 int mdt_thin_blocks(int tconv, ConvDesc d) {
   if (!tconv) return cdiv_t((long long)d.N * d.OH * d.OW, 256);
   if (tconv_patch_ok(d)) return d.N * (d.OH / 4);
-  if (tconv4_ok(d)) return cdiv_t((long long)d.N * (d.H / 2) * (d.W / 2), 256);
   return cdiv_t((long long)d.N * (d.H / d.S) * (d.W / d.S), 256) * d.S * d.S;
 }
 
@@ -135,17 +116,6 @@ int mdt_thin_tconv(const void* G16, const float* Wf, ConvDesc d, const float* bi
       hipLaunchKernelGGL(thin_tconv_mfma_k, dim3(d.N * (d.OH / 4)), dim3(256), 0, s, tp);
     else
       hipLaunchKernelGGL((thin_tconv_patch_k<32, 64>), dim3(d.N * (d.OH / 4)), dim3(256), 0, s, tp);
-    return (int)hipGetLastError();
-  }
-  if (tconv4_ok(d)) {  // one thread per input position: all four parity classes
-    const ThinTconvArgs t4{reinterpret_cast<const __bf16*>(G16), Wf, d, bias, y32, X,
-                           reinterpret_cast<__bf16*>(dlog16), recon, part, gpart, gx};
-    switch (d.CO) {
-      case 16: hipLaunchKernelGGL((thin_tconv4_k<16>), dim3(gx), dim3(256), 0, s, t4); break;
-      case 32: hipLaunchKernelGGL((thin_tconv4_k<32>), dim3(gx), dim3(256), 0, s, t4); break;
-      case 64: hipLaunchKernelGGL((thin_tconv4_k<64>), dim3(gx), dim3(256), 0, s, t4); break;
-      default: return 2;
-    }
     return (int)hipGetLastError();
   }
   dim3 grid(gx * d.S * d.S), blk(256);

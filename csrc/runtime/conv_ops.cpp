@@ -65,8 +65,6 @@ int mdt_job_loss(mdt::JobBlob* j, const float* bce_part, int nb, const float* kl
 int mdt_launch_jobs(const mdt::JobBlob* jobs, int n, hipStream_t s);
 int mdt_jobs_multi_bytes();
 int mdt_pack_jobs_multi(const mdt::JobBlob* jobs, int n, void* dst);
-int mdt_pack_jobs_multi_fin(const mdt::JobBlob* jobs, int n, void* dst, int fin, int first,
-                            const int* unit_wait_host, const int* unit_wait_dev, int* tickets);
 int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s);
 int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train, hipStream_t s);
 int mdt_f28_backward(const long long* p, int M, hipStream_t s);
@@ -74,8 +72,6 @@ int mdt_f28_step(const long long* pf, const long long* pb, const long long* pp, 
                  int pair, int delay_us, hipStream_t s);
 int mdt_f28_pair_words();
 int mdt_launch_job1(const mdt::JobBlob* j, hipStream_t s);
-int mdt_launch_tail(const mdt::JobBlob* wg, const mdt::JobBlob* fin0, const mdt::JobBlob* finr, int* ticket,
-                    hipStream_t s);
 }
 
 namespace mdt {
@@ -328,18 +324,6 @@ void loss_finalize2(const at::Tensor& bce_part, int64_t nb, const at::Tensor& kl
 // Launch recorded jobs as ONE fused kernel when an instantiation exists for
 // their kinds (returns true), else launch nothing and return false (the caller
 // then issues the ops' own kernels). Follow-up combines run right after.
-// One-launch optimizer tail (conv_jobs.hip::tail_k). `ticket`: int32 [3],
-// zero before the first launch (each launch leaves [0] and [1] at zero; [2]
-// is a sticky timeout flag).
-bool launch_tail(Job* wg, Job* fin0, Job* finr, at::Tensor ticket) {
-  TORCH_CHECK(ticket.is_cuda() && ticket.scalar_type() == torch::kInt32 && ticket.numel() >= 3, "ticket");
-  TORCH_CHECK(!wg->has_post() && !fin0->has_post() && !finr->has_post(), "launch_tail: jobs with a post pass");
-  TORCH_CHECK(finr->main.kind != 0 || finr->main.nblk == 0, "launch_tail: finr");
-  const int r = mdt_launch_tail(&wg->main, &fin0->main, &finr->main, ticket.data_ptr<int>(), cur());
-  TORCH_CHECK(r >= 0 && r != 2, "mdt: launch_tail failed (", r, ")");
-  return r == 0;
-}
-
 bool launch_jobs(const std::vector<Job*>& jobs) {
   TORCH_CHECK(jobs.size() >= 2 && jobs.size() <= 3, "launch_jobs takes 2 or 3 jobs");
   JobBlob v[3];
@@ -358,13 +342,7 @@ bool launch_jobs(const std::vector<Job*>& jobs) {
 // Pack recorded jobs (any supported kinds, up to 8) into a job table for ONE
 // jobs_multi_k launch: returns (uint8 CPU tensor image, grid). The caller keeps
 // the table in device memory for the lifetime of the plan (graph replays).
-// fin >= 0 (the last job, a finalize job): in-launch weight-gradient ->
-// finalize hand-off (conv_jobs.hip JobPackN); unit_wait = device int32 [units]
-// (job index each finalize unit waits for, -1 none), tickets = zeroed device
-// int32 [17] owned by the caller for the lifetime of the pack.
-std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs, int64_t fin, int64_t first,
-                                                const c10::optional<at::Tensor>& unit_wait,
-                                                const c10::optional<at::Tensor>& tickets) {
+std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs) {
   TORCH_CHECK(!jobs.empty() && jobs.size() <= 8, "pack_jobs_multi takes 1..8 jobs");
   std::vector<JobBlob> v;
   for (auto* j : jobs) {
@@ -373,22 +351,7 @@ std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs, i
     v.push_back(j->main);
   }
   auto img = torch::zeros({(int64_t)mdt_jobs_multi_bytes()}, torch::kUInt8);
-  int grid;
-  if (fin >= 0) {
-    TORCH_CHECK(unit_wait.has_value() && tickets.has_value(), "pack_jobs_multi: fin needs unit_wait and tickets");
-    const at::Tensor& uw = *unit_wait;
-    const at::Tensor& tk = *tickets;
-    TORCH_CHECK(uw.is_cuda() && uw.scalar_type() == torch::kInt32 && uw.is_contiguous() && uw.dim() == 1 &&
-                    uw.numel() == v[fin].nblk, "pack_jobs_multi: unit_wait must be device int32 [finalize units]");
-    TORCH_CHECK(tk.is_cuda() && tk.scalar_type() == torch::kInt32 && tk.is_contiguous() && tk.numel() >= 17,
-                "pack_jobs_multi: tickets must be device int32 [>= 17]");
-    auto uw_host = uw.cpu();
-    grid = mdt_pack_jobs_multi_fin(v.data(), (int)v.size(), img.data_ptr(), (int)fin, (int)first,
-                                   uw_host.data_ptr<int>(),
-                                   uw.data_ptr<int>(), tk.data_ptr<int>());
-  } else {
-    grid = mdt_pack_jobs_multi(v.data(), (int)v.size(), img.data_ptr());
-  }
+  const int grid = mdt_pack_jobs_multi(v.data(), (int)v.size(), img.data_ptr());
   TORCH_CHECK(grid > 0, "pack_jobs_multi: unsupported job kind or bad job (", grid, ")");
   return {img, (int64_t)grid};
 }
@@ -721,9 +684,7 @@ void bind_conv(pybind11::module& m) {
       .def_property_readonly("kind", &Job::kind)
       .def_property_readonly("has_post", &Job::has_post);
   m.def("launch_jobs", &launch_jobs);
-  m.def("pack_jobs_multi", &pack_jobs_multi, py::arg("jobs"), py::arg("fin") = -1, py::arg("first") = -1,
-        py::arg("unit_wait") = py::none(),
-        py::arg("tickets") = py::none());
+  m.def("pack_jobs_multi", &pack_jobs_multi, py::arg("jobs"));
   m.def("launch_jobs_multi", &launch_jobs_multi);
   m.def("f28_forward", &f28_forward, py::arg("tensors"), py::arg("B"), py::arg("M"), py::arg("stream"),
         py::arg("train"));
@@ -732,7 +693,6 @@ void bind_conv(pybind11::module& m) {
   m.def("f28_step", &f28_step, py::arg("fwd_tensors"), py::arg("bwd_tensors"), py::arg("B"), py::arg("M"),
         py::arg("stream"), py::arg("pair") = std::vector<c10::optional<at::Tensor>>{},
         py::arg("pair_delay_us") = 0);
-  m.def("launch_tail", &launch_tail);
   m.def("igemm", &igemm, py::arg("mode"), py::arg("A"), py::arg("B16"), py::arg("desc"), py::arg("bias"),
         py::arg("relu"), py::arg("y16"), py::arg("y32"), py::arg("omask") = py::none(),
         py::arg("colsum") = py::none(), py::arg("ws") = py::none(), py::arg("job") = py::none(),

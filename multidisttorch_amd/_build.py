@@ -90,7 +90,7 @@ def _compile(cmd, src, obj, stamp):
 
 
 def hip_flags():
-    # MDT_HIP_EXTRA_FLAGS: compile-time A/B switches (e.g. -DMDT_CONV_PF=2)
+    # MDT_HIP_EXTRA_FLAGS: compile-time A/B switches (e.g. -DNAME=1)
     extra = os.getenv("MDT_HIP_EXTRA_FLAGS", "").split()
     return ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
             "-Wno-unused-result", "-I" + os.path.join(CSRC, "kernels")] + extra

@@ -225,10 +225,6 @@ class ConvVaeTrainer:
         self.graph_steps = max(1, graph_steps)
         self._graphs = {}
         self.reducer = None
-        # two-stream backward (see _backward_overlap), opt-in with MDT_CONV_OVERLAP=1: measured
-        # slower on MI355X (conv28 0.180 -> 0.277 ms/step) -- cross-stream graph edges cost more
-        # than the overlap recovers
-        self.overlap = self.device.type == "cuda" and os.getenv("MDT_CONV_OVERLAP", "0") == "1"
         # horizontal fusion of independent backward launches (conv_jobs.hip);
         # MDT_CONV_JOBS=0 issues every op as its own kernel (A/B, bitwise equal)
         self.fuse_jobs = os.getenv("MDT_CONV_JOBS", "1") != "0"
@@ -240,13 +236,6 @@ class ConvVaeTrainer:
         # (profiles/r1_tail); with the transposes deferred (below) 1 % faster
         # at 28x28 (0.1208 -> 0.1196 ms, profiles/r1_defer): on up to 64x64
         self.spread_fin = os.getenv("MDT_CONV_SPREAD_FIN", "1" if image <= 64 else "0") == "1"
-        # one-launch optimizer tail (conv_jobs.hip::tail_k, device ticket) with
-        # the transposed weight copies moved into the next step's first launch.
-        # Opt-in (MDT_CONV_TAIL1=1): measured slower on MI355X -- the per-wave
-        # agent-scope release fences (L2 write-back, buffer_wbl2) of ~200
-        # weight-gradient blocks cost more than the launch they save
-        # (profiles/r1_tail/README.md)
-        self.tail1 = os.getenv("MDT_CONV_TAIL1", "0") == "1"
         # two-launch tail without the transposes (MDT_CONV_DEFER_WT=1|2, no
         # ticket, no fences): the tail's second launch is the first layer's
         # finalize alone, and the transposed weight copies ride in the next
@@ -271,15 +260,6 @@ class ConvVaeTrainer:
         # B = 128 trial fills all 256 CUs instead of 128. MDT_F28_PAIR=0 (A/B): one per sample
         self.f28_pair = os.getenv("MDT_F28_PAIR", "1") != "0"
         self.f28_pair_delay_us = 0  # tests: delay every partner workgroup (forces the solo fallback)
-        # finalize + Adam as the last job of the weight-gradient launch, each
-        # unit released by its layer's ticket (conv_jobs.hip JobPackN): 2
-        # launches per step instead of 3. Bitwise-tested but measured 4x
-        # SLOWER (0.31 vs 0.072 ms/step, profiles/r2_fin): every cross-XCD
-        # hand-off needs an agent-scope release (L2 write-back) per
-        # weight-gradient block and an acquire (L2 invalidate) per finalize
-        # unit, which evicts the L2 working set of the blocks still running.
-        # Opt-in: MDT_F28_FIN=1.
-        self.f28_fin = os.getenv("MDT_F28_FIN", "0") == "1"
         # profiling: int64 [B*16] tensors (fwd, bwd) receiving per-workgroup
         # phase-end s_memrealtime stamps (obs/f28_phases.py); None = off
         self.f28_stamps = (None, None)
@@ -303,7 +283,6 @@ class ConvVaeTrainer:
         else:
             self.C = native.require()
             self.state = self.C.TrialState(self.device.index or 0)
-            self._ticket = torch.zeros(3, dtype=torch.int32, device=self.device)  # tail_k: arrived, passed, timeout
             self._alloc_hip()
         self._push_hparams()
 
@@ -716,7 +695,7 @@ class ConvVaeTrainer:
                 first_conv = (lambda job, l=l: C.thin_conv(X, self._wf32(l), self._desc(l, M), self._b(l), l.relu,
                                                            self.acts[l.name], job=job, idx=idx, state=state,
                                                            hparams=hp, B=self.B, xb=self.xb))
-                if wt and not (self.wt_in_dec and not self.tail1):
+                if wt and not self.wt_in_dec:
                     # the transposed copies share the step's first launch (nothing in it reads them)
                     self._run_group([first_conv, lambda job: self._wtrans_layers(1, len(self.spec), job)])
                     wt = False
@@ -726,7 +705,7 @@ class ConvVaeTrainer:
             else:
                 C.step_begin(state, hp)
                 C.gather_rows(X, idx, state, self.B, M, self.xb)
-        if wt and not (self.wt_in_dec and not self.tail1 and self.fuse_jobs):
+        if wt and not (self.wt_in_dec and self.fuse_jobs):
             self._wtrans_layers(1, len(self.spec))
             wt = False
         pro = {}
@@ -819,7 +798,7 @@ class ConvVaeTrainer:
         # spread mode: layers [fin_hi, L) already finalized (+Adam) as the third
         # job of a backward launch -- layer j's gradients are complete once the
         # launch of layer j ran, and nothing later in the step reads its weights
-        spread = (optimizer and self.spread_fin and self.fuse_jobs and self.reducer is None and not self.overlap)
+        spread = (optimizer and self.spread_fin and self.fuse_jobs and self.reducer is None)
         fin_hi = len(spec)
         if with_loss:
             carry.append(lambda job: C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part,
@@ -881,15 +860,6 @@ class ConvVaeTrainer:
                                      C.colsum(gin, M, n, p["rows_per"], cso, job=job))
             if prev is None and optimizer:
                 L = len(spec)
-                if self._tail1_active() and len(fns) == 1:
-                    jobs = [C.Job() for _ in range(3)]
-                    fns[0](jobs[0])
-                    self._finalize_layers(M, 0, 1, jobs[1])
-                    if fin_hi > 1:
-                        self._finalize_layers(M, 1, fin_hi, jobs[2])
-                    if jobs[0].kind > 0 and C.launch_tail(jobs[0], jobs[1], jobs[2], self._ticket):
-                        self._fused_launches += 1
-                        break
                 if fin_hi > 1:
                     fns.append(lambda job, hi=fin_hi: self._finalize_layers(M, 1, hi, job))
                 self._run_group(fns)
@@ -929,18 +899,10 @@ class ConvVaeTrainer:
             print(f"[jobs] no finalize fusion: kinds={sorted(j.kind for j in jobs)}", file=sys.stderr, flush=True)
         return False
 
-    def _tail1_active(self):
-        """One-launch optimizer tail in use: the backward ends with tail_k and
-        leaves the transposed weight copies (w16t) to the next forward, which
-        writes them before any launch reads them (``_forward_hip``)."""
-        return (self.tail1 and self.fuse_jobs and self._thin_first and self.reducer is None
-                and not self.overlap and len(self.spec) > 1)
-
     def _wt_deferred(self):
         """The transposed weight copies (w16t) of a step's update are written by
-        the next step's first launch (one-launch tail, or MDT_CONV_DEFER_WT)."""
-        return ((self.tail1 or self.defer_wt) and self.fuse_jobs and self._thin_first and self.reducer is None
-                and not self.overlap and len(self.spec) > 1)
+        the next step's first launch or the first decoder launch (MDT_CONV_DEFER_WT)."""
+        return self.defer_wt and self.fuse_jobs and self._thin_first and self.reducer is None and len(self.spec) > 1
 
     def _finalize_layers(self, M, lo, hi, job=None):
         """Finalize + Adam + bf16 cast of layers [lo, hi) (their units of the plan)."""
@@ -981,12 +943,6 @@ class ConvVaeTrainer:
         C = self.C
         X, idx = self._data[0], self._data[1]
         st = self.state
-        if self.reducer is None and self.overlap:
-            C.step_begin(st.train_state, st.hparams)
-            C.gather_rows(X, idx, st.train_state, self.B, M, self.xb)
-            self._forward_hip(M, st.train_state, self.rng_stream)
-            self._backward_overlap(M)
-            return
         self._forward_hip(M, st.train_state, self.rng_stream, src=(X, idx))
         if self.reducer is None:
             # backward + optimizer tail (finalize/Adam/bf16 cast/transposes) in fused launches
@@ -1065,20 +1021,6 @@ class ConvVaeTrainer:
                  segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
                  nunits=len(units), layer_units=layer_units, first_dec=first_dec,
                  dec_pack=dec_pack.to(dev), dec_grid=dec_grid, enc_pack=enc_pack.to(dev), enc_grid=enc_grid)
-        if self.f28_fin:
-            # weight-gradient jobs 0..5 (srcs order), loss/step job 6, finalize
-            # job 7: a weight unit waits for its layer's job, every unit for the
-            # step-advance job (the Adam bias corrections it writes)
-            jf = C.Job()
-            C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
-                            len(units), st.train_state, st.hparams, True, job=jf)
-            names = list(srcs)
-            uw = [names.index(self.spec[si // 2].name) if si % 2 == 0 else -1 for si, _s, _c in units]
-            p["unit_wait"] = torch.tensor(uw, dtype=torch.int32, device=dev)
-            p["tickets"] = torch.zeros(17, dtype=torch.int32, device=dev)
-            packf, gridf = C.pack_jobs_multi(jobs + [jf], fin=len(jobs), first=len(jobs) - 1,
-                                             unit_wait=p["unit_wait"], tickets=p["tickets"])
-            p.update(jf=jf, fin_pack=packf.to(dev), fin_grid=gridf)
         self._plans28[M] = p
         return p
 
@@ -1096,9 +1038,6 @@ class ConvVaeTrainer:
             C.f28_forward(p["fwd"], self.B, M, self.rng_stream, True)
             C.f28_backward(p["bwd"], M)
         red = self.reducer
-        if self.f28_fin and red is None and not self.f28_skip_adam:
-            C.launch_jobs_multi(p["fin_pack"], p["fin_grid"])
-            return
         if red is None:
             C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
             C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
@@ -1136,89 +1075,6 @@ class ConvVaeTrainer:
             self.C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"],
                                  p["units"].narrow(0, u0 * 12, (u1 - u0) * 12), u1 - u0, st.train_state,
                                  st.hparams, False)
-
-    # layer groups whose gradients are finalized together (optimizer + bf16
-    # re-cast + transposed copies) on the side stream once the backward-data
-    # sweep has passed them; the last group's launches end the step.
-    FINALIZE_GROUPS = {28: ("dec_fc", "enc2", "enc1"), 128: ("dec2", "dec_fc", "enc3", "enc2", "enc1")}
-
-    def _side_stream(self):
-        s = getattr(self, "_side", None)
-        if s is None:
-            s = self._side = torch.cuda.Stream(self.device)
-        return s
-
-    def _backward_overlap(self, M):
-        """Backward with two streams (both captured into the step graph as
-        parallel branches). The main stream runs only the backward-data chain
-        (the critical path); the side stream runs every weight-gradient GEMM,
-        the bias column sums, the loss reduction and -- per layer group, as soon
-        as the chain no longer reads those weights -- the gradient finalize +
-        fused Adam + bf16 cast and the transposed weight copies. Same kernels,
-        same arithmetic and the same deterministic reduction order as the
-        sequential path; only the launch order across streams changes."""
-        C = self.C
-        p = self._plan(M)
-        spec = self.spec
-        st = self.state
-        main = torch.cuda.current_stream(self.device)
-        side = self._side_stream()
-        names = [l.name for l in spec]
-        cut = {names.index(n) for n in self.FINALIZE_GROUPS.get(self.image, ("enc1",)) if n in names}
-        cut.add(0)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, self._n_kld(M),
-                             st.train_state, st.hparams, True)
-        g = self.dlog16
-        hi = len(spec)  # layers [i, hi) wait for their finalize
-        for i in range(len(spec) - 1, -1, -1):
-            l = spec[i]
-            prev = spec[i - 1] if i > 0 else None
-            d = self._desc(l, M)
-            a_in = self.xb if i == 0 else (self.z16 if l.name == "dec_fc" else self.acts[prev.name])
-            wslab = p["slabs"].get(l.name + ".weight")
-            wout = wslab[0] if wslab is not None else self._gw(l)
-            with torch.cuda.stream(side):
-                if l.kind == "convT":
-                    C.wgrad(a_in, g, d, wout)
-                else:
-                    C.wgrad(g, a_in, d, wout)
-            side_cs = []
-            if prev is not None:
-                omask = a_in if prev.relu else None
-                if l.name == "dec_fc":  # as in _backward_hip: the same reduction order
-                    ks = C.igemm_plan(1, d, True)[10]
-                    C.igemm(1, g, self._wt(l), d, None, False, None, self.dz, ws=p["ws"], combine=ks == 1)
-                    if ks > 1:
-                        C.combine_reparam_bwd(p["ws"], ks, self.mulv, self.eps, self.dmulv, self.dmulv16, self.dz,
-                                              M, self.Z, st.hparams)
-                    else:
-                        C.reparam_bwd(self.dz, self.mulv, self.eps, self.dmulv, self.dmulv16, M, self.Z,
-                                      st.hparams)
-                    gin = self.dmulv16
-                    side_cs.append((gin, 2 * self.Z, p["colsum"][prev.name]))
-                elif i == len(spec) - 1 and self._thin_last:
-                    gin = self.gacts[prev.name]
-                    C.thin_conv(g, self._wf32(l), d, None, False, gin, omask, p["colsum"][prev.name])
-                else:
-                    gin = self.gacts[prev.name]
-                    cs = None if prev.name == "dec_fc" else p["colsum"].get(prev.name)
-                    C.igemm(0 if l.kind == "convT" else 1, g, self._w(l) if l.kind == "convT" else self._wt(l), d,
-                            None, False, gin, None, omask, cs)
-                    if prev.name == "dec_fc":
-                        side_cs.append((gin, prev.cout, p["colsum"][prev.name]))
-                g = gin
-            side.wait_stream(main)  # layer i's backward-data is done: its weights are free to update
-            with torch.cuda.stream(side):
-                for t, n, out in side_cs:
-                    C.colsum(t, M, n, p["rows_per"], out)
-                if i in cut:
-                    self._finalize_layers(M, i, hi)
-                    if hi > max(i, 1):
-                        self._wtrans_layers(max(i, 1), hi)
-                    hi = i
-        main.wait_stream(side)
 
     def _finalize_grads(self, M, do_adam):
         """Reduce the partial slabs into the gradient arena (deterministic order);

@@ -204,39 +204,6 @@ def test_f28_merged_step_is_bitwise_two_launches(M, native_ext):
         assert all(torch.equal(ga[k], res[0][4][k]) for k in ga) and torch.equal(dm, res[0][5])
 
 
-@pytest.mark.parametrize("M", [128, 77])
-def test_f28_fin_in_wgrad_launch_is_bitwise(M, native_ext):
-    """Finalize + Adam as the ticket-released last job of the weight-gradient
-    launch (f28_fin, 2 launches per step) == the separate grad_finalize launch
-    (3 launches): same losses, weights, moments, state, eager and graph-replayed
-    (graph replays reuse the tickets: the last waiter must reset them); no
-    ticket wait timed out."""
-    from multidisttorch_amd.data.datasets import synthetic_images
-
-    dev = torch.device("cuda")
-    X = synthetic_images(1024, device=dev)
-    idx = torch.arange(1024, device=dev, dtype=torch.int32)
-    res = []
-    for fin, graphs in ((False, False), (True, False), (True, True)):
-        tr = _trainer(seed=8, use_graphs=graphs, graph_steps=3)
-        tr.f28_fin = fin
-        tr.bind_train_data(X, idx)
-        tr.set_cursor(0, 8)
-        tr.train_steps(7, M=M)
-        torch.cuda.synchronize()
-        if fin:
-            tk = tr._plan28(M)["tickets"].cpu()
-            assert int(tk[16]) == 0, "ticket wait timed out"
-            assert int(tk[:16].abs().sum()) == 0, tk  # every counter reset by its last waiter
-        st = tr.read_state()
-        res.append((tr.loss_history()[:7].copy(), tr.params.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone(),
-                    tr.w16.clone(), st["step"], st["cursor"]))
-    for h, p, m, v, w16, step, cur in res[1:]:
-        np.testing.assert_array_equal(h, res[0][0])
-        assert torch.equal(p, res[0][1]) and torch.equal(m, res[0][2]) and torch.equal(v, res[0][3])
-        assert torch.equal(w16, res[0][4]) and step == res[0][5] == 7 and cur == res[0][6]
-
-
 def test_f28_adam_matches_torch_optim(native_ext):
     """The finalize + fused Adam of the fused step against torch.optim.Adam
     fed with the kernel's own gradients, over 3 steps (lr, betas, eps, bias

@@ -268,35 +268,6 @@ def test_conv_vae_transposed_weights_are_parity_ordered(native_ext):
         torch.testing.assert_close(tr._wt(l), parity_transpose(w, l.s), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("image,batch", [(28, 128), (128, 16)])
-def test_two_stream_backward_is_bitwise_sequential(image, batch, native_ext):
-    """The two-stream backward (weight gradients, finalize+Adam and transposes
-    on a side stream, captured as parallel graph branches) runs the same
-    kernels with the same reduction order: losses and weights match the
-    single-stream path bit for bit, eager and graph-replayed."""
-    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
-
-    dev = torch.device("cuda")
-    D = image * image
-    X = torch.rand(8 * batch, D, device=dev)
-    idx = torch.arange(8 * batch, device=dev, dtype=torch.int32)
-    out = []
-    for overlap, graphs in ((False, False), (True, False), (True, True)):
-        tr = ConvVaeTrainer(batch_size=batch, image=image, device=dev, backend="hip", seed=5,
-                            use_graphs=graphs, graph_steps=3)
-        tr.overlap = overlap
-        tr.bind_train_data(X, idx)
-        tr.set_cursor(0, 8)
-        tr.train_steps(7)
-        torch.cuda.synchronize()
-        out.append((tr.loss_history()[:7].copy(), tr.params.clone(), _wt_layers(tr)))
-    for h, p, wt in out[1:]:
-        np.testing.assert_array_equal(h, out[0][0])
-        assert torch.equal(p, out[0][1])
-        bad = [n for n in wt if not torch.equal(wt[n], out[0][2][n])]
-        assert not bad, bad
-
-
 @pytest.mark.parametrize("image,batch", [(28, 128), (28, 64), (128, 32)])
 def test_fused_job_launches_are_bitwise_unfused(image, batch, native_ext):
     """Horizontally fused backward launches (conv_jobs.hip: weight gradient ||
@@ -361,41 +332,6 @@ def test_encoder_head_prologue_matches_combine_launch(native_ext, monkeypatch):
 
 
 @pytest.mark.parametrize("image,batch", [(28, 128), (128, 32)])
-def test_one_launch_optimizer_tail_is_bitwise_two_launch(image, batch, native_ext):
-    """conv_jobs.hip::tail_k: the last first-layer weight-gradient block (device
-    ticket) finalizes the first layer while the other blocks finalize the rest,
-    and the transposed copies move into the next step's first launch. Same
-    losses, master weights, Adam moments and transposed weights as the
-    two-launch tail (MDT_CONV_TAIL1=0 path), eager and graph-replayed; the
-    ticket is back at zero after every launch."""
-    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
-
-    dev = torch.device("cuda")
-    D = image * image
-    X = torch.rand(6 * batch, D, device=dev)
-    idx = torch.arange(6 * batch, device=dev, dtype=torch.int32)
-    out = []
-    for tail1, graphs in ((False, False), (True, False), (True, True)):
-        tr = ConvVaeTrainer(batch_size=batch, image=image, device=dev, backend="hip", seed=11,
-                            use_graphs=graphs, graph_steps=2)
-        tr.tail1 = tail1
-        tr.spread_fin = False
-        assert tr._tail1_active() == tail1
-        tr.bind_train_data(X, idx)
-        tr.set_cursor(0, 6)
-        tr.train_steps(5)
-        torch.cuda.synchronize()
-        assert tr._ticket.tolist() == [0, 0, 0]
-        out.append((tr.loss_history()[:5].copy(), tr.params.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone(),
-                    _wt_layers(tr)))
-    for h, p, m, v, wt in out[1:]:
-        np.testing.assert_array_equal(h, out[0][0])
-        assert torch.equal(p, out[0][1]) and torch.equal(m, out[0][2]) and torch.equal(v, out[0][3])
-        bad = [n for n in wt if not torch.equal(wt[n], out[0][4][n])]
-        assert not bad, bad
-
-
-@pytest.mark.parametrize("image,batch", [(28, 128), (128, 32)])
 def test_deferred_transposes_are_bitwise_two_launch(image, batch, native_ext):
     """MDT_CONV_DEFER_WT: the tail's second launch finalizes only the first
     layer and the transposed copies are written by the next step's first launch
@@ -413,7 +349,6 @@ def test_deferred_transposes_are_bitwise_two_launch(image, batch, native_ext):
                                   (True, True, False), (True, True, True)):
         tr = ConvVaeTrainer(batch_size=batch, image=image, device=dev, backend="hip", seed=11,
                             use_graphs=graphs, graph_steps=2)
-        tr.tail1 = False
         tr.defer_wt = defer
         tr.wt_in_dec = in_dec
         tr.spread_fin = False
@@ -436,8 +371,7 @@ def test_spread_finalize_is_bitwise_tail_finalize(image, batch, native_ext):
     """Finalize+Adam of layer j as the third job of the backward launch after
     layer j's gradients completed (MDT_CONV_SPREAD_FIN, default) gives the same
     losses, weights, moments and transposed weights as finalizing every layer
-    in the optimizer tail, eager and graph-replayed, with and without the
-    one-launch tail."""
+    in the optimizer tail, eager and graph-replayed."""
     from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
 
     dev = torch.device("cuda")
@@ -445,11 +379,10 @@ def test_spread_finalize_is_bitwise_tail_finalize(image, batch, native_ext):
     X = torch.rand(6 * batch, D, device=dev)
     idx = torch.arange(6 * batch, device=dev, dtype=torch.int32)
     out = []
-    for spread, tail1, graphs in ((False, False, False), (True, False, False), (True, False, True),
-                                  (True, True, True)):
+    for spread, graphs in ((False, False), (True, False), (True, True)):
         tr = ConvVaeTrainer(batch_size=batch, image=image, device=dev, backend="hip", seed=13,
                             use_graphs=graphs, graph_steps=2)
-        tr.spread_fin, tr.tail1 = spread, tail1
+        tr.spread_fin = spread
         tr.bind_train_data(X, idx)
         tr.set_cursor(0, 6)
         tr.train_steps(5)
