@@ -1,4 +1,4 @@
-// One-shot peer-to-peer all-reduce over xGMI (host/device shared declarations).
+// Peer-to-peer all-reduce over xGMI, one-shot and two-shot (host/device shared declarations).
 //
 // Included by the HIP kernel (p2p_allreduce.hip) and by the host reducer
 // (csrc/runtime/p2p_comm.cpp); plain data only.
@@ -20,8 +20,10 @@ struct P2PArgs {
   unsigned* ep;                         // per-block epoch counters of this bucket (local only)
   int* status;                          // 0 = ok, 1 + bucket = a wait timed out
   long long recv_off;                   // this bucket's receive slab: [2 parity][s src][n]
-  long long flag_off;                   // this bucket's flags: [s src][grid]
+                                        // (two-shot: RS [2 parity][s src][chunk] then AG, same shape)
+  long long flag_off;                   // this bucket's flags: [2 phase][s src][grid]
   int me, s, bucket;
+  int two_shot;                         // 1: reduce-scatter by chunk owner + all-gather
   float scale;                          // 1/s for averaging
   long long timeout_ticks;              // s_memrealtime ticks (100 MHz)
 };

@@ -1,4 +1,4 @@
-// XgmiP2PReducer: one-shot peer-to-peer bucket all-reduce over xGMI (hipIpc).
+// XgmiP2PReducer: one-shot / two-shot peer-to-peer bucket all-reduce over xGMI (hipIpc).
 //
 // on a fully connected 8x MI355X node a group of s GPUs
 // has s-1 direct xGMI links per GPU. RCCL's ring crosses one link per step and
@@ -7,7 +7,13 @@
 // ring all-reduce for them). This reducer pushes each bucket to every peer at
 // once (kernel: csrc/kernels/p2p_allreduce.hip) and needs no communicator:
 //   * each rank allocates ONE uncached device region (receive slabs
-//     [bucket][parity][src][n] + per-(src, block) flags + epoch counters),
+//     [bucket][parity][src][n], or for a two-shot bucket reduce-scatter and
+//     all-gather slabs [2][parity][src][n/s] + per-(phase, src, block) flags +
+//     epoch counters),
+//   * buckets of at least `two_shot_min_bytes` (-1: never) run two-shot:
+//     reduce-scatter to the chunk owners, then all-gather, so each of the s-1
+//     links carries 2/s of the bucket (one-shot: all of it) -- the
+//     bandwidth-bound regime of the 128x128 model's ~18 MB of gradients,
 //     exports it with hipIpcGetMemHandle, and maps every peer's region with
 //     hipIpcOpenMemHandle (handles are exchanged by the caller over the gloo
 //     control plane, parallel/ddp.py::make_p2p_reducer);
@@ -30,7 +36,7 @@ namespace mdt {
 class XgmiP2PReducer : public StreamBuckets {
  public:
   XgmiP2PReducer(int64_t rank, int64_t size, at::Tensor flat, std::vector<int64_t> bounds, bool average,
-                 double scale, int64_t max_blocks, double timeout_s)
+                 double scale, int64_t max_blocks, double timeout_s, int64_t two_shot_min_bytes)
       : StreamBuckets(std::move(flat), std::move(bounds)), me_((int)rank), s_((int)size) {
     TORCH_CHECK(s_ >= 1 && s_ <= kP2PMaxRanks, "XgmiP2PReducer: group size must be 1..", kP2PMaxRanks);
     TORCH_CHECK(me_ >= 0 && me_ < s_, "XgmiP2PReducer: rank out of range");
@@ -41,14 +47,19 @@ class XgmiP2PReducer : public StreamBuckets {
     long long roff = 0, foff = 0, eoff = 0;
     for (int64_t b = 0; b < nb; ++b) {
       const long long n = bounds_[b + 1] - bounds_[b];
-      long long g = (n + 2047) / 2048;  // >= 2K elements (8 KB) per block
+      // two-shot (reduce-scatter + all-gather) for big buckets of groups >= 2: every link carries 2/s of
+      // the bucket instead of all of it, for one extra hop of latency
+      const bool two = s_ >= 2 && two_shot_min_bytes >= 0 && n * 4 >= two_shot_min_bytes;
+      const long long cs = ((n + s_ - 1) / s_ + 3) / 4 * 4;  // chunk per owner (kernel: same formula)
+      long long g = ((two ? cs : n) + 2047) / 2048;            // >= 2K elements (8 KB) per block
       g = std::max(1LL, std::min(g, (long long)max_blocks));
       grid_.push_back((int)g);
+      two_.push_back(two ? 1 : 0);
       recv_off_.push_back(roff);
       flag_off_.push_back(foff);
       ep_off_.push_back(eoff);
-      roff += 2LL * s_ * ((n + 63) / 64 * 64);
-      foff += (long long)s_ * g;
+      roff += two ? 4LL * s_ * ((cs + 63) / 64 * 64) : 2LL * s_ * ((n + 63) / 64 * 64);
+      foff += 2LL * s_ * g;
       eoff += g;
     }
     recv_elems_ = roff;
@@ -117,6 +128,7 @@ class XgmiP2PReducer : public StreamBuckets {
   }
   double scale() const { return scale_; }
   std::vector<int64_t> grids() const { return std::vector<int64_t>(grid_.begin(), grid_.end()); }
+  std::vector<int64_t> two_shot() const { return std::vector<int64_t>(two_.begin(), two_.end()); }
 
  protected:
   void issue(int64_t b, hipStream_t s) override {
@@ -137,6 +149,7 @@ class XgmiP2PReducer : public StreamBuckets {
     a.me = me_;
     a.s = s_;
     a.bucket = (int)b;
+    a.two_shot = two_[b];
     a.scale = scale_;
     a.timeout_ticks = timeout_ticks_;
     if (s_ == 1 && scale_ == 1.0f) return;
@@ -153,16 +166,17 @@ class XgmiP2PReducer : public StreamBuckets {
   bool opened_[kP2PMaxRanks] = {};
   bool connected_ = false;
   long long recv_elems_ = 0, flags_byte_ = 0, ep_byte_ = 0, status_byte_ = 0, bytes_ = 0;
-  std::vector<int> grid_;
+  std::vector<int> grid_, two_;
   std::vector<long long> recv_off_, flag_off_, ep_off_;
 };
 
 void bind_p2p(pybind11::module& m) {
   namespace py = pybind11;
   auto c = py::class_<XgmiP2PReducer>(m, "XgmiP2PReducer")
-               .def(py::init<int64_t, int64_t, at::Tensor, std::vector<int64_t>, bool, double, int64_t, double>(),
+               .def(py::init<int64_t, int64_t, at::Tensor, std::vector<int64_t>, bool, double, int64_t, double, int64_t>(),
                     py::arg("rank"), py::arg("size"), py::arg("flat"), py::arg("bounds"), py::arg("average") = true,
-                    py::arg("scale") = 0.0, py::arg("max_blocks") = 64, py::arg("timeout_s") = 60.0)
+                    py::arg("scale") = 0.0, py::arg("max_blocks") = 64, py::arg("timeout_s") = 60.0,
+                    py::arg("two_shot_min_bytes") = -1)
                .def("ipc_handle", &XgmiP2PReducer::ipc_handle)
                .def("local_base", &XgmiP2PReducer::local_base)
                .def("region_bytes", &XgmiP2PReducer::region_bytes)
@@ -170,7 +184,8 @@ void bind_p2p(pybind11::module& m) {
                .def("connect_local", &XgmiP2PReducer::connect_local)
                .def("status", &XgmiP2PReducer::status)
                .def("scale", &XgmiP2PReducer::scale)
-               .def("grids", &XgmiP2PReducer::grids);
+               .def("grids", &XgmiP2PReducer::grids)
+               .def("two_shot", &XgmiP2PReducer::two_shot);
   def_bucket_api(c);
 }
 

@@ -10,8 +10,9 @@ trainer of the same configuration (so the real trial's state is untouched),
 the per-rank times are max-reduced over the group so every member picks the
 same layout, and the winner is cached per (model, group size, batch, arena).
 ``autotune_comm`` searches the reducer too: RCCL's ring (``rccl``) against the
-one-shot hipIpc push over all s-1 xGMI links (``p2p``, csrc/runtime/p2p_comm.cpp)
-for every layout, when the group is on GPUs of one node.
+one-shot hipIpc push over all s-1 xGMI links (``p2p1``) and, for groups of 3+,
+the two-shot reduce-scatter + all-gather form (``p2p2``, both in
+csrc/runtime/p2p_comm.cpp) for every layout, when the group is on GPUs of one node.
 """
 
 from __future__ import annotations
@@ -67,12 +68,16 @@ def _store_cache(path: str, key: str, entry: dict) -> None:
 
 def comm_kinds(pg, device: torch.device) -> List[Optional[str]]:
     """Reducer kinds worth timing for this group: RCCL and the hipIpc p2p push
-    when every member drives a GPU of the same node; otherwise the default."""
+    (one-shot; two-shot too for groups of 3+, where it halves the bytes per
+    link or better) when every member drives a GPU of the same node;
+    otherwise the default."""
     if device.type != "cuda" or not dist.is_initialized() or dist.get_backend(pg) != "nccl":
         return [None]
     hosts = [None] * dist.get_world_size(pg)
     dist.all_gather_object(hosts, socket.gethostname(), group=pg)
-    return ["rccl", "p2p"] if len(set(hosts)) == 1 else ["rccl"]
+    if len(set(hosts)) != 1:
+        return ["rccl"]
+    return ["rccl", "p2p1"] + (["p2p2"] if len(hosts) >= 3 else [])
 
 
 def autotune_buckets(make_trainer: Callable[[], object], pg, X: torch.Tensor, idx: torch.Tensor,

@@ -33,7 +33,8 @@ from torch import nn
 from ..ops import native
 
 __all__ = ["XgmiModel", "plan_buckets", "make_arena_reducer", "PyBucketReducer", "ArenaDDP",
-           "broadcast_params", "rccl_comm_ptr", "reducer_kind", "make_p2p_reducer"]
+           "broadcast_params", "rccl_comm_ptr", "reducer_kind", "make_p2p_reducer", "P2P_KINDS",
+           "two_shot_min_bytes"]
 
 
 class XgmiModel:
@@ -182,9 +183,10 @@ def rccl_comm_ptr(pg, device: torch.device) -> int:
 
 
 def reducer_kind(pg, flat: torch.Tensor) -> str:
-    """'rccl' (direct RCCL on torch's communicator), 'p2p' (one-shot hipIpc push
-    over xGMI, opt-in), 'c10d' (native reducer over the ProcessGroup) or
-    'python'. MDT_REDUCER overrides the choice."""
+    """'rccl' (direct RCCL on torch's communicator), 'p2p' (hipIpc push over
+    xGMI: one-shot, two-shot for big buckets of groups >= 3), 'p2p1' (one-shot
+    only), 'p2p2' (two-shot only), 'c10d' (native reducer over the
+    ProcessGroup) or 'python'. MDT_REDUCER overrides the choice."""
     forced = os.getenv("MDT_REDUCER", "")
     if forced:
         return forced
@@ -214,8 +216,8 @@ def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: b
     if kind == "rccl":
         size = dist.get_world_size(pg)
         return native.require().RcclBucketReducer(rccl_comm_ptr(pg, flat.device), size, flat, b, average, scale)
-    if kind == "p2p":
-        return make_p2p_reducer(pg, flat, b, average)
+    if kind in P2P_KINDS:
+        return make_p2p_reducer(pg, flat, b, average, two_shot=P2P_KINDS[kind])
     if kind == "c10d" and native.available():
         return native.require().BucketReducer(pg, flat, b, average)
     if flat.is_cuda:
@@ -223,17 +225,37 @@ def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: b
     return PyBucketReducer(pg, flat, bounds, average)
 
 
+# reducer kind -> two-shot rule: "auto" (buckets >= MDT_P2P_TWO_SHOT_MB, default 4, in groups >= 3),
+# "never" (one-shot), "always"
+P2P_KINDS = {"p2p": "auto", "p2p1": "never", "p2p2": "always"}
+
+
+def two_shot_min_bytes(rule: str, group_size: int) -> int:
+    """Smallest bucket (bytes) the p2p reducer runs two-shot; -1 = never.
+
+    Per link, one-shot moves the whole bucket and two-shot 2/s of it for one
+    extra hop: at s = 2 the bytes are equal, so "auto" keeps one-shot there."""
+    if rule == "always":
+        return 0
+    if rule == "never" or group_size < 3:
+        return -1
+    return int(float(os.getenv("MDT_P2P_TWO_SHOT_MB", "4")) * (1 << 20))
+
+
 def make_p2p_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: bool = True,
-                     max_blocks: Optional[int] = None, timeout_s: Optional[float] = None):
-    """One-shot peer-to-peer bucket all-reduce over xGMI (csrc/runtime/p2p_comm.cpp).
+                     max_blocks: Optional[int] = None, timeout_s: Optional[float] = None, two_shot: str = "auto"):
+    """Peer-to-peer bucket all-reduce over xGMI (csrc/runtime/p2p_comm.cpp).
 
     Every group member allocates an uncached receive region, exports it with
     hipIpcGetMemHandle, and the 64-byte handles are all-gathered over the group
     itself; each rank then maps its peers' regions. A bucket is pushed to all
     s-1 peers at once (one xGMI hop, every link of the group busy) instead of
     RCCL's ring (2(s-1) hops over one link per step) -- the regime of the
-    VAE models' 1-4 MB buckets. All ranks of the group must share one node.
-    Selected with ``MDT_REDUCER=p2p`` (or ``kind="p2p"``); RCCL stays the default.
+    VAE models' 1-4 MB buckets. Big buckets run two-shot instead
+    (reduce-scatter to chunk owners + all-gather, 2/s of the bucket per link;
+    ``two_shot``: "auto" | "never" | "always", see ``two_shot_min_bytes``).
+    All ranks of the group must share one node. Selected with
+    ``MDT_REDUCER=p2p`` (or ``kind="p2p"/"p2p1"/"p2p2"``); RCCL stays the default.
     """
     if not flat.is_cuda:
         raise RuntimeError("the p2p reducer needs a GPU gradient arena")
@@ -241,7 +263,8 @@ def make_p2p_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: boo
     s, r = dist.get_world_size(pg), dist.get_rank(pg)
     max_blocks = max_blocks or int(os.getenv("MDT_P2P_BLOCKS", "64"))
     timeout_s = timeout_s or float(os.getenv("MDT_P2P_TIMEOUT_S", "60"))
-    red = C.XgmiP2PReducer(r, s, flat, [int(x) for x in bounds], average, 0.0, max_blocks, timeout_s)
+    red = C.XgmiP2PReducer(r, s, flat, [int(x) for x in bounds], average, 0.0, max_blocks, timeout_s,
+                           two_shot_min_bytes(two_shot, s))
     if s > 1:
         h = red.ipc_handle()
         if dist.get_backend(pg) == "nccl":

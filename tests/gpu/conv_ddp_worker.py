@@ -10,7 +10,7 @@ bitwise identical. Phase 2 (independent eps per replica, rng_stream = group
 rank, as the reference's unseeded replicas): replicas still bitwise identical
 after every step, while their per-replica losses differ.
 
-argv: image graphs(0|1) bucket_mb  -> prints RESULT json
+argv: image graphs(0|1) bucket_mb [reducer kind]  -> prints RESULT json
 """
 import json
 import os
@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 def main():
     image, graphs = int(sys.argv[1]), sys.argv[2] == "1"
     bucket_mb = None if sys.argv[3] == "none" else float(sys.argv[3])
+    kind = sys.argv[4] if len(sys.argv) > 4 else "p2p"
     dist.init_process_group("gloo")
     r, s = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
@@ -56,7 +57,7 @@ def main():
         tr = make(stream)
         broadcast_params([tr.params], dist.group.WORLD)  # DDP ctor broadcast (gloo: via host copy)
         tr.refresh_weights()
-        red = make_arena_reducer(dist.group.WORLD, tr.grads, tr.bucket_bounds(bucket_mb), kind="p2p")
+        red = make_arena_reducer(dist.group.WORLD, tr.grads, tr.bucket_bounds(bucket_mb), kind=kind)
         tr.attach_reducer(red)
         tr.bind_train_data(X, idx)
         tr.set_cursor(0, nb)

@@ -1,6 +1,7 @@
 """Worker for tests/gpu/test_p2p_reducer.py: s processes share the box's single
 MI355X, exchange hipIpc handles of their receive regions over gloo, and run the
-one-shot p2p all-reduce kernel (eager and graph-replayed). Prints RESULT json."""
+p2p all-reduce kernel (eager and graph-replayed). argv: reducer kind (p2p |
+p2p1 | p2p2). Prints RESULT json."""
 import json
 import os
 import sys
@@ -22,7 +23,8 @@ def main():
     bounds = [0, 1000, 65_536, n]
     flat = torch.zeros(n, device=dev)
     os.environ["MDT_P2P_TIMEOUT_S"] = "10"
-    red = make_arena_reducer(dist.group.WORLD, flat, bounds, kind="p2p")
+    kind = sys.argv[1] if len(sys.argv) > 1 else "p2p"
+    red = make_arena_reducer(dist.group.WORLD, flat, bounds, kind=kind)
     gen = lambda rank, it: torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + rank))
     errs, iters = [], 5
     for it in range(iters):
@@ -57,12 +59,13 @@ def main():
         ref = sum(gen(p, it).double() for p in range(s)) / s
         gerrs.append(float((flat.cpu().double() - ref).abs().max()))
     st2 = red.status()
+    red_two = red.two_shot()
     dist.barrier()  # peers stop touching our region before it is freed
     del g, red
     torch.cuda.synchronize()
     dist.barrier()
-    print("RESULT " + json.dumps({"rank": r, "errs": errs, "gerrs": gerrs, "status": [st, st2], "same": same}),
-          flush=True)
+    print("RESULT " + json.dumps({"rank": r, "errs": errs, "gerrs": gerrs, "status": [st, st2], "same": same,
+                                  "two_shot": list(red_two)}), flush=True)
     dist.destroy_process_group()
 
 

@@ -234,16 +234,17 @@ def test_prepare_locks_graphs_for_timed_steps(native_ext, model):
         tr.train_steps(1, M=64)
 
 
-@pytest.mark.parametrize("s,image,graphs,mb", [(2, 28, 1, "none"), (4, 28, 1, "0.25"), (2, 128, 1, "2"),
-                                               (4, 128, 0, "none")])
-def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb):
+@pytest.mark.parametrize("s,image,graphs,mb,kind", [(2, 28, 1, "none", "p2p"), (4, 28, 1, "0.25", "p2p"),
+                                                    (2, 128, 1, "2", "p2p"), (4, 128, 0, "none", "p2p"),
+                                                    (2, 28, 1, "none", "p2p2"), (4, 128, 1, "2", "p2p2")])
+def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb, kind):
     from multidisttorch_amd.launch import launch
 
     # several processes share the GPU: the fused 28x28 step keeps one workgroup
     # per sample (a paired sample whose partner is not resident falls back to
     # the solo form, whose f32 summation order differs at rounding level)
     env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2", "MDT_F28_PAIR": "0"}
-    rc, outs = launch([sys.executable, os.path.join(HERE, "conv_ddp_worker.py"), str(image), str(graphs), mb], s,
+    rc, outs = launch([sys.executable, os.path.join(HERE, "conv_ddp_worker.py"), str(image), str(graphs), mb, kind], s,
                       emulate="torchrun", timeout=150, extra_env=env, capture=True)
     text = "\n".join(o or "" for o in outs)
     assert rc == 0, text[-4000:]

@@ -22,10 +22,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 
 
-def _pair(C, s, n, bounds, timeout=5.0):
+def _pair(C, s, n, bounds, timeout=5.0, two_shot_min_bytes=-1):
     dev = torch.device("cuda", 0)
     flats = [torch.zeros(n, device=dev) for _ in range(s)]
-    reds = [C.XgmiP2PReducer(r, s, flats[r], bounds, True, 0.0, 64, timeout) for r in range(s)]
+    reds = [C.XgmiP2PReducer(r, s, flats[r], bounds, True, 0.0, 64, timeout, two_shot_min_bytes) for r in range(s)]
     bases = [r.local_base() for r in reds]
     for r in reds:
         r.connect_local(bases)
@@ -40,12 +40,21 @@ def _fill(flats, it):
     return sum(v.double() for v in vals) / len(vals)
 
 
-def test_p2p_in_process_eager_and_graph(native_ext):
+def _same(flats):
+    return all(torch.equal(flats[0], f) for f in flats[1:])
+
+
+@pytest.mark.parametrize("s,two", [(2, -1), (2, 0), (3, 0), (4, 16384)])
+def test_p2p_in_process_eager_and_graph(native_ext, s, two):
+    """two = two_shot_min_bytes: -1 one-shot only, 0 two-shot for every bucket,
+    16384 two-shot for the buckets of >= 4096 elements (mixed launch)."""
     C = native_ext
     n = 200_003  # odd size: vector body + scalar tail; tiny first bucket = one block
     bounds = [0, 100, 4096, 70_000, n]
-    flats, reds = _pair(C, 2, n, bounds)
+    flats, reds = _pair(C, s, n, bounds, two_shot_min_bytes=two)
     assert reds[0].num_buckets() == 4 and reds[0].grids()[0] == 1 and reds[0].grids()[3] <= 64
+    assert reds[0].two_shot() == [0 if two < 0 or 4 * w < two else 1 for w in (100, 3996, 65_904, 130_003)]
+    ok = [0] * s
     for it in range(4):  # both epoch parities, twice
         ref = _fill(flats, it)
         torch.cuda.synchronize()
@@ -54,8 +63,8 @@ def test_p2p_in_process_eager_and_graph(native_ext):
         for r in reds:
             r.wait_all()
         torch.cuda.synchronize()
-        assert [r.status() for r in reds] == [0, 0]
-        assert torch.equal(flats[0], flats[1])  # rank-ordered sum: identical replicas
+        assert [r.status() for r in reds] == ok
+        assert _same(flats)  # rank-ordered sum: identical replicas
         torch.testing.assert_close(flats[0].cpu().double(), ref, rtol=0, atol=1e-6)
     # readiness counting launches a bucket when its last parameter is marked
     for r in reds:
@@ -88,9 +97,30 @@ def test_p2p_in_process_eager_and_graph(native_ext):
             with torch.cuda.stream(st):
                 g.replay()
         torch.cuda.synchronize()
-        assert [r.status() for r in reds] == [0, 0]
-        assert torch.equal(flats[0], flats[1])
+        assert [r.status() for r in reds] == ok
+        assert _same(flats)
         torch.testing.assert_close(flats[0].cpu().double(), ref, rtol=0, atol=1e-6)
+
+
+def test_two_shot_is_bitwise_one_shot(native_ext):
+    """Both forms sum the s contributions in rank order and scale once: the
+    two-shot result has the same bits as the one-shot one."""
+    C = native_ext
+    n, s = 1_000_001, 4
+    outs = []
+    for two in (-1, 0):
+        flats, reds = _pair(C, s, n, [0, n], two_shot_min_bytes=two)
+        for it in range(2):
+            _fill(flats, 40 + it)
+            torch.cuda.synchronize()
+            for r in reds:
+                r.launch_all()
+            for r in reds:
+                r.wait_all()
+            torch.cuda.synchronize()
+        assert [r.status() for r in reds] == [0] * s
+        outs.append(flats[2].clone())
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_missing_peer_times_out(native_ext):
@@ -104,21 +134,22 @@ def test_missing_peer_times_out(native_ext):
     assert reds[0].status() == 1
 
 
-@pytest.mark.parametrize("s", [2, 4])
-def test_p2p_multiprocess_ipc(s):
+@pytest.mark.parametrize("s,kind", [(2, "p2p"), (4, "p2p"), (3, "p2p2")])
+def test_p2p_multiprocess_ipc(s, kind):
     from multidisttorch_amd.launch import launch
 
     # several processes share the GPU: the fused 28x28 step keeps one workgroup
     # per sample (a paired sample whose partner is not resident falls back to
     # the solo form, whose f32 summation order differs at rounding level)
     env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2", "MDT_F28_PAIR": "0"}
-    rc, outs = launch([sys.executable, os.path.join(HERE, "p2p_worker.py")], s, emulate="torchrun", timeout=100,
+    rc, outs = launch([sys.executable, os.path.join(HERE, "p2p_worker.py"), kind], s, emulate="torchrun", timeout=100,
                       extra_env=env, capture=True)
     text = "\n".join(o or "" for o in outs)
     assert rc == 0, text[-4000:]
     res = [json.loads(l[7:]) for l in text.splitlines() if l.startswith("RESULT ")]
     assert len(res) == s, text[-4000:]
     for r in res:
+        assert r["two_shot"] == ([1, 1, 1] if kind == "p2p2" else [0, 0, 0]), r
         assert r["status"] == [0, 0], r
         assert r["same"], r
         assert max(r["errs"] + r["gerrs"]) < 1e-5, r

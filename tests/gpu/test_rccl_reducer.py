@@ -146,8 +146,8 @@ def test_autotune_comm_times_rccl_and_p2p(nccl_world, native_ext, tmp_path):
     make = lambda: MlpVaeTrainer(batch_size=128, device=dev, backend="hip", seed=3, use_graphs=True, graph_steps=4)
     bounds, kind, timings = autotune_comm(make, nccl_world, X, idx, candidates=(None, 0), steps=4, warmup=2,
                                           key="gpu-test", cache=str(tmp_path / "b.json"))
-    assert kind in ("rccl", "p2p")
-    assert any(k.startswith("p2p:") for k in timings) and any(k.startswith("rccl:") for k in timings)
+    assert kind in ("rccl", "p2p1")
+    assert any(k.startswith("p2p1:") for k in timings) and any(k.startswith("rccl:") for k in timings)
     hist = []
     for k in ("rccl", "p2p"):
         tr = make()

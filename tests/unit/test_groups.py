@@ -33,3 +33,17 @@ def test_partition_properties(w, k):
         g = p.group_of(r)
         if g is not None:
             assert r in p.ranks(g) and p.group_rank_of(r) == r - p.ranks(g)[0]
+
+
+def test_p2p_two_shot_rule(monkeypatch):
+    """p2p reducer kinds: one-shot at s = 2 (equal bytes per link), two-shot
+    for buckets >= MDT_P2P_TWO_SHOT_MB in groups of 3+; p2p1/p2p2 force a form."""
+    from multidisttorch_amd.parallel.ddp import P2P_KINDS, two_shot_min_bytes
+
+    monkeypatch.delenv("MDT_P2P_TWO_SHOT_MB", raising=False)
+    assert two_shot_min_bytes(P2P_KINDS["p2p"], 2) == -1
+    assert two_shot_min_bytes(P2P_KINDS["p2p"], 4) == 4 << 20
+    assert two_shot_min_bytes(P2P_KINDS["p2p1"], 8) == -1
+    assert two_shot_min_bytes(P2P_KINDS["p2p2"], 2) == 0
+    monkeypatch.setenv("MDT_P2P_TWO_SHOT_MB", "0.5")
+    assert two_shot_min_bytes(P2P_KINDS["p2p"], 3) == 1 << 19
