@@ -211,6 +211,20 @@ def main(argv=None):
         hist = tr.loss_history()
         last = float(hist[(st["step"] - 1) % len(hist)])
         ok = ok and st["step"] == a.warmup + a.steps and last == last and last < 1e9
+    # intra-group data parallelism: every replica of a trial must hold bitwise the
+    # same parameters after the timed steps (the averaged gradient is identical on
+    # every member; tests/gpu/conv_ddp_worker.py asserts the same)
+    replicas_equal = None
+    if n_per > 1 and gid is not None:
+        replicas_equal = True
+        pg = handles[gid]
+        on_dev = dist.get_backend(pg) == "nccl"
+        for tr in trainers:
+            p = tr.params.detach().clone() if on_dev else tr.params.detach().cpu()
+            got = [torch.empty_like(p) for _ in range(n_per)]
+            dist.all_gather(got, p, group=pg)
+            replicas_equal = replicas_equal and all(torch.equal(got[0], g) for g in got)
+        ok = ok and replicas_equal
     flag = torch.tensor([1.0 if ok else 0.0])
     if world > 1:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ctrl)
@@ -243,6 +257,9 @@ def main(argv=None):
                 "graphs": (not a.no_graphs),
                 "timing_barrier": tbar_kind,
                 "valid": bool(flag.item() > 0),
+                "replicas_bitwise_equal": replicas_equal,
+                "reducer": (type(trainer.reducer).__name__ if trainer is not None
+                            and getattr(trainer, "reducer", None) is not None else None),
                 # vs_baseline: the reference publishes no numbers (BASELINE.json
                 # "published": {}); the divisor is a builder-measured anchor
                 "baseline": ("NOT a published baseline: builder-measured reference-equivalent torch-eager "

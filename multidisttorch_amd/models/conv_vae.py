@@ -259,6 +259,9 @@ class ConvVaeTrainer:
         # the merged step with two workgroups per sample (conv28_pair.h): a
         # B = 128 trial fills all 256 CUs instead of 128. MDT_F28_PAIR=0 (A/B): one per sample
         self.f28_pair = os.getenv("MDT_F28_PAIR", "1") != "0"
+        # DDP: decoder buckets go out before the encoder weight gradients
+        # (MDT_DDP_OVERLAP=0, A/B only: every bucket after the whole backward)
+        self.ddp_overlap = os.getenv("MDT_DDP_OVERLAP", "1") != "0"
         self.f28_pair_delay_us = 0  # tests: delay every partner workgroup (forces the solo fallback)
         # profiling: int64 [B*16] tensors (fwd, bwd) receiving per-workgroup
         # phase-end s_memrealtime stamps (obs/f28_phases.py); None = off
@@ -1053,15 +1056,16 @@ class ConvVaeTrainer:
         dec0 = self.layer_ranges()[fd][1]
         bounds = list(red.bounds())
         nbk = len(bounds) - 1
+        early = self.ddp_overlap
         C.launch_jobs_multi(p["dec_pack"], p["dec_grid"])
         self._finalize_unit_range(p, lu[fd], lu[L])
         for k in reversed(range(nbk)):
-            if bounds[k] >= dec0:
+            if early and bounds[k] >= dec0:
                 red.launch(k)
         C.launch_jobs_multi(p["enc_pack"], p["enc_grid"])
         self._finalize_unit_range(p, lu[0], lu[fd])
         for k in reversed(range(nbk)):
-            if bounds[k] < dec0:
+            if not early or bounds[k] < dec0:
                 red.launch(k)
         red.wait_all()
         if not self.f28_skip_adam:

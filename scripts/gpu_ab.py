@@ -11,6 +11,8 @@ that step only (A/B switches such as MDT_CONV_F28=0, MDT_CONV_DIRECT=0):
   test[:PATH[:KEXPR]]                     pytest (default ``tests -m gpu``), one process
   bench[:MODEL[:B[:STEPS[:WARMUP]]]]      bench.py -> bench_<i>.json + a summary line
   driver[:ARG:ARG...]                     the driver's command: bench.py --gpus 1 --steps 20 --warmup 5 [ARGS]
+  ddp:N[:MODEL[:B[:STEPS[:WARMUP]]]]      one trial of N replicas sharing the GPU (torchrun, gloo world,
+                                          p2p data plane unless @MDT_REDUCER=... says otherwise)
   launches[:IMAGE[:B]]                    bench/conv_kernels.py (every launch of a step, alone)
   f28phases | f28parts | dconv[:B]        in-kernel stamp / per-launch tools of the fused kernels
   prof[:MODEL[:B]]                        rocprofv3 --kernel-trace --stats of a short bench run
@@ -36,7 +38,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PY = sys.executable
 
-LIMITS = {"test": 900, "bench": 240, "driver": 180, "launches": 240, "f28phases": 120, "f28parts": 120,
+LIMITS = {"test": 900, "bench": 240, "ddp": 240, "driver": 180, "launches": 240, "f28phases": 120, "f28parts": 120,
           "dconv": 120, "prof": 300, "pmc": 90, "smoke": 300}
 
 
@@ -71,6 +73,12 @@ def command(kind, args, out, i):
         return argv, ROOT, log
     if kind == "bench":
         return [PY] + bench_args(*args), ROOT, os.path.join(out, f"{i:02d}_bench.json")
+    if kind == "ddp":
+        n = args[0]
+        rest = bench_args(*(args[1:] or ["conv28"]))
+        return [PY, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", n, "--master-addr",
+                "127.0.0.1", "--master-port", str(29600 + i)] + rest + ["--gpus", n, "--ngroups", "1"], ROOT, \
+            os.path.join(out, f"{i:02d}_ddp.json")
     if kind == "driver":
         return [PY, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "20", "--warmup", "5"] + args, ROOT, \
             os.path.join(out, f"{i:02d}_driver.json")
@@ -106,13 +114,15 @@ def command(kind, args, out, i):
 
 
 def summary(kind, path):
-    if kind in ("bench", "driver"):
+    if kind in ("bench", "driver", "ddp"):
         try:
             with open(path) as f:
                 line = [l for l in f if l.startswith("{")][-1]
             d = json.loads(line)
             c = d["config"]
-            return f"{c['model']} B={c['global_batch']}: {d['ms_per_step']} ms/step, {d['value']:.0f} {d['unit']}"
+            extra = f" {c['parallelism']} {c.get('reducer')} equal={c.get('replicas_bitwise_equal')}" \
+                if kind == "ddp" else ""
+            return f"{c['model']} B={c['global_batch']}: {d['ms_per_step']} ms/step, {d['value']:.0f} {d['unit']}{extra}"
         except Exception as e:  # noqa: BLE001 - report, do not crash the run
             return f"(no JSON line: {e})"
     with open(path, errors="replace") as f:
@@ -136,10 +146,13 @@ def main():
         else:
             full = ["timeout", "-k", "10", str(limit)] + argv
         env = dict(os.environ, **env_add)
+        if kind == "ddp":  # ranks share the GPU: RCCL refuses that, so a gloo world + the p2p data plane
+            env.setdefault("DDP_BACKEND", "gloo")
+            env.setdefault("MDT_REDUCER", "p2p")
         if kind in ("prof", "pmc"):
             env["TMPDIR"] = "/tmp"
         print(f"== [{i}] {step}", flush=True)
-        json_out = kind in ("bench", "driver")  # stdout is the JSON line; stderr apart
+        json_out = kind in ("bench", "driver", "ddp")  # stdout is the JSON line; stderr apart
         with open(out, "w") as f, open(out + ".err" if json_out else os.devnull, "w") as fe:
             r = subprocess.run(full, cwd=cwd, env=env, stdout=f, stderr=fe if json_out else subprocess.STDOUT)
         print(summary(kind, out), flush=True)

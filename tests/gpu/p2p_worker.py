@@ -60,11 +60,27 @@ def main():
         gerrs.append(float((flat.cpu().double() - ref).abs().max()))
     st2 = red.status()
     red_two = red.two_shot()
-    dist.barrier()  # peers stop touching our region before it is freed
-    del g, red
+    # the same inputs through the one-shot form: bitwise the same result
+    flat.copy_(gen(r, 99).to(dev))
+    torch.cuda.synchronize()
+    red.launch_all()
+    red.wait_all()
+    torch.cuda.synchronize()
+    got = flat.clone()
+    one = make_arena_reducer(dist.group.WORLD, flat, bounds, kind="p2p1")
+    flat.copy_(gen(r, 99).to(dev))
+    torch.cuda.synchronize()
+    one.launch_all()
+    one.wait_all()
+    torch.cuda.synchronize()
+    bitwise = bool(torch.equal(got, flat))
+    st3 = one.status()
+    dist.barrier()  # peers stop touching our regions before they are freed
+    del g, red, one
     torch.cuda.synchronize()
     dist.barrier()
-    print("RESULT " + json.dumps({"rank": r, "errs": errs, "gerrs": gerrs, "status": [st, st2], "same": same,
+    print("RESULT " + json.dumps({"rank": r, "errs": errs, "gerrs": gerrs, "status": [st, st2, st3], "same": same,
+                                  "bitwise_one_shot": bitwise,
                                   "two_shot": list(red_two)}), flush=True)
     dist.destroy_process_group()
 

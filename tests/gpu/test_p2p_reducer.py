@@ -44,10 +44,15 @@ def _same(flats):
     return all(torch.equal(flats[0], f) for f in flats[1:])
 
 
-@pytest.mark.parametrize("s,two", [(2, -1), (2, 0), (3, 0), (4, 16384)])
+@pytest.mark.parametrize("s,two", [(2, -1), (2, 0), (2, 16384)])
 def test_p2p_in_process_eager_and_graph(native_ext, s, two):
     """two = two_shot_min_bytes: -1 one-shot only, 0 two-shot for every bucket,
-    16384 two-shot for the buckets of >= 4096 elements (mixed launch)."""
+    16384 two-shot for the buckets of >= 4096 elements (mixed launch).
+
+    In-process "ranks" progress only while their streams sit on different
+    hardware queues (GPU_MAX_HW_QUEUES = 4 per process): the graph-replay part
+    runs for the first case only, before more streams exist; the two-shot
+    graph replays are covered by the multi-process test (one process per rank)."""
     C = native_ext
     n = 200_003  # odd size: vector body + scalar tail; tiny first bucket = one block
     bounds = [0, 100, 4096, 70_000, n]
@@ -80,6 +85,8 @@ def test_p2p_in_process_eager_and_graph(native_ext, s, two):
         r.reset_iteration()
     torch.cuda.synchronize()
     torch.testing.assert_close(flats[1].cpu().double(), ref, rtol=0, atol=1e-6)
+    if two >= 0:
+        return
     # hipGraph capture per "rank", replays on separate streams
     graphs, streams = [], [torch.cuda.Stream() for _ in reds]
     for r, st in zip(reds, streams):
@@ -104,9 +111,11 @@ def test_p2p_in_process_eager_and_graph(native_ext, s, two):
 
 def test_two_shot_is_bitwise_one_shot(native_ext):
     """Both forms sum the s contributions in rank order and scale once: the
-    two-shot result has the same bits as the one-shot one."""
+    two-shot result has the same bits as the one-shot one (s = 2 here, one
+    stream per "rank" within the hardware-queue budget; the multi-process test
+    checks s = 3, 4)."""
     C = native_ext
-    n, s = 1_000_001, 4
+    n, s = 1_000_001, 2
     outs = []
     for two in (-1, 0):
         flats, reds = _pair(C, s, n, [0, n], two_shot_min_bytes=two)
@@ -119,7 +128,7 @@ def test_two_shot_is_bitwise_one_shot(native_ext):
                 r.wait_all()
             torch.cuda.synchronize()
         assert [r.status() for r in reds] == [0] * s
-        outs.append(flats[2].clone())
+        outs.append(flats[1].clone())
     assert torch.equal(outs[0], outs[1])
 
 
@@ -134,7 +143,7 @@ def test_missing_peer_times_out(native_ext):
     assert reds[0].status() == 1
 
 
-@pytest.mark.parametrize("s,kind", [(2, "p2p"), (4, "p2p"), (3, "p2p2")])
+@pytest.mark.parametrize("s,kind", [(2, "p2p"), (4, "p2p"), (3, "p2p2"), (4, "p2p2")])
 def test_p2p_multiprocess_ipc(s, kind):
     from multidisttorch_amd.launch import launch
 
@@ -150,6 +159,7 @@ def test_p2p_multiprocess_ipc(s, kind):
     assert len(res) == s, text[-4000:]
     for r in res:
         assert r["two_shot"] == ([1, 1, 1] if kind == "p2p2" else [0, 0, 0]), r
-        assert r["status"] == [0, 0], r
+        assert r["status"] == [0, 0, 0], r
+        assert r["bitwise_one_shot"], r
         assert r["same"], r
         assert max(r["errs"] + r["gerrs"]) < 1e-5, r
