@@ -21,6 +21,8 @@
 
 #include <algorithm>
 
+#include "conv_direct.h"
+#include "conv_dwgrad.h"
 #include "conv_igemm_dev.h"
 #include "conv_small.h"
 #include "conv_thin.h"
@@ -85,6 +87,24 @@ struct JThinConv {
   static constexpr int ID = kJobThinConv + CO + (sizeof(TIN) == 4 ? 100 : 0), LDS = thin_conv_lds_bytes<CO, 4>();
   static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
     thin_conv_body<CO, 4, TIN>(job_args<ThinConvArgs>(j), lds, b);
+  }
+};
+
+// patch-resident direct conv (the backward-data of the 64x64 / 32x32 layers):
+// shares a launch with the layer's weight gradient
+template <int CFG, class CF>
+struct JDc {
+  static constexpr int ID = kJobDconv + CFG, LDS = CF::LDS;
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    dconv_body<CF>(job_args<DcArgs>(j), lds, xcd_remap(b, j.nblk));
+  }
+};
+
+template <int CFG, class CF>
+struct JDw {
+  static constexpr int ID = kJobDwgrad + CFG, LDS = CF::LDS;
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    dwgrad_body<CF>(job_args<DwArgs>(j), lds, b);
   }
 };
 
@@ -194,7 +214,8 @@ __host__ inline bool multi_kind_ok(int k) {
 
 template <class A, class B, class C>
 __global__ void __launch_bounds__(256) jobs_k(JobPack p) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[cmax(cmax(A::LDS, B::LDS), cmax(C::LDS, 16))];
+  // 1 KB aligned: the direct-conv bodies land LDS-DMA pieces at 1 KB offsets
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[cmax(cmax(A::LDS, B::LDS), cmax(C::LDS, 16))];
   const int b = blockIdx.x;
   if (b < p.start1) A::run(p.j[0], lds, b);
   else if (b < p.start2) B::run(p.j[1], lds, b - p.start1);
@@ -239,6 +260,11 @@ using IgT2 = JIg<kModeTconv, 2, F2>;
 using IgT4 = JIg<kModeTconv, 4, F4>;
 using IgT5 = JIg<kModeTconv, 5, F5>;
 using IgT6 = JIg<kModeTconv, 6, F6>;
+using DcJS1 = JDc<0, DcS1>;
+using DcJS2 = JDc<1, DcS2>;
+using DcJT2 = JDc<2, DcT2>;
+using DcJT3 = JDc<3, DcT3>;
+using DwJ1 = JDw<0, DwL1>;
 
 // kinds sorted ascending within each entry
 const Combo kCombos[] = {
@@ -288,12 +314,31 @@ const Combo kCombos[] = {
     COMBO2(IgC4, JWtrans),
     COMBO2(IgC5, JWtrans),
     COMBO2(IgC6, JWtrans),
+    // 128x128 middle layers: direct backward-data || weight gradient (im2col
+    // for the 32x32 <-> 16x16 pair, direct for the 64x64 <-> 32x32 pair)
+    COMBO2(Wg0, DcJS2),
+    COMBO2(Wg0, DcJT2),
+    COMBO2(DcJS1, DwJ1),
+    COMBO2(DcJT3, DwJ1),
 };
 
 #undef COMBO3
 #undef COMBO2
 
 inline int cdivj(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// workgroups of a direct-conv launch (conv_igemm.hip launch_dc)
+template <class CF>
+constexpr int dc_grid(int n) { return n * CF::RB * CF::NBB; }
+inline int direct_grid(int dc, int n) {
+  switch (dc) {
+    case 0: return dc_grid<DcS1>(n);
+    case 1: return dc_grid<DcS2>(n);
+    case 2: return dc_grid<DcT2>(n);
+    case 3: return dc_grid<DcT3>(n);
+    default: return 0;
+  }
+}
 
 template <class T>
 void put_args(JobBlob* j, const T& a) {
@@ -319,9 +364,27 @@ int mdt_job_igemm(JobBlob* g, JobBlob* c, int mode, const void* A, int a_is_f32,
   if (build_igemm(mode, A, B16, d, bias, relu, y16, y32, omask, colsum, ws, &a, &q, &cb, &nc)) return 1;
   memset(g, 0, sizeof(*g));
   memset(c, 0, sizeof(*c));
-  // direct-kernel geometries have no job form yet: kind 0 sends the caller
-  // to mdt_igemm (their column-sum rows follow the direct plan)
-  const bool ok = !a_is_f32 && !q.thin && direct_cfg(mode, d, false) < 0;
+  // direct-kernel geometries: the direct body as a job (backward-data calls;
+  // the 16x16 <-> 8x8 forward-only tiles have no job form)
+  const int dc = direct_cfg(mode, d, false);
+  if (dc >= 0) {
+    if (a_is_f32 || dc > 3) return 0;  // kind 0: the caller launches it alone
+    DcArgs da{};
+    da.A = reinterpret_cast<const __bf16*>(A);
+    da.B = reinterpret_cast<const __bf16*>(B16);
+    da.y16 = reinterpret_cast<__bf16*>(y16);
+    da.y32 = y32;
+    da.bias = bias;
+    da.omask = reinterpret_cast<const __bf16*>(omask);
+    da.colsum = colsum;
+    da.relu = relu;
+    da.nimg = d.N;
+    g->kind = kJobDconv + dc;
+    g->nblk = direct_grid(dc, d.N);
+    put_args(g, da);
+    return 0;
+  }
+  const bool ok = !a_is_f32 && !q.thin;
   g->kind = ok ? kJobIgemm + mode * 100 + q.cfg : 0;
   g->nblk = q.mtiles * q.ntiles * q.ksplit * q.classes;
   g->aux[0] = q.mtiles * q.ntiles;
@@ -341,7 +404,13 @@ int mdt_job_wgrad(JobBlob* j, const void* G16, const void* X, int x_is_f32, Conv
   if (build_wgrad(G16, X, d, out, &a, &q)) return 1;
   memset(j, 0, sizeof(*j));
   if (q.cfg == 110) j->kind = kJobThinWgM + (x_is_f32 ? 1 : 0);  // MFMA thin weight gradient
-  else if (q.cfg >= 100) j->kind = 0;  // direct weight gradient (conv_dwgrad.h): its own launch
+  else if (q.cfg >= 100) {  // direct weight gradient (conv_dwgrad.h)
+    if (x_is_f32 || q.cfg != 100) return 0;  // kind 0: its own launch
+    j->kind = kJobDwgrad + (q.cfg - 100);
+    j->nblk = d.N * 4;
+    put_args(j, DwArgs{reinterpret_cast<const __bf16*>(X), reinterpret_cast<const __bf16*>(G16), out, d.N, nullptr});
+    return 0;
+  }
   else if (!q.thin) j->kind = x_is_f32 ? 0 : kJobWgrad + q.cfg;
   else j->kind = kJobWgradThin + (x_is_f32 ? 20 : 0) + q.cfg;
   j->nblk = q.cotiles * q.ktiles * q.nsplit;
