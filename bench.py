@@ -78,7 +78,8 @@ def main(argv=None):
     ap.add_argument("--model", default="conv28", choices=["mlp", "conv28", "conv128"],
                     help="conv28 = conv-VAE bf16 28x28 (BASELINE configs #2/#3, headline); conv128 = 128x128 "
                          "(config #5); mlp = the reference's MLP-VAE in fp32")
-    ap.add_argument("--graph-steps", type=int, default=10)
+    ap.add_argument("--graph-steps", type=int, default=20,
+                    help="steps per captured hipGraph (one replay covers the driver's 20-step window)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--backend", default=None, help="hip|torch (default: hip on GPU)")
     ap.add_argument("--json-out", default=None)
