@@ -215,6 +215,7 @@ def test_bench_contract_multirank(tmp_path, n, k):
     assert out["n_gpus"] == n and out["steps"] == 2 and out["warmup"] == 1
     assert out["config"]["trials"] == K and out["config"]["parallelism"] == f"groups{K}x{n // K}"
     assert out["config"]["valid"] is True
+    assert out["config"]["replicas_bitwise_equal"] is (True if n // K > 1 else None)
     assert abs(out["value"] - K * 64 * 2 / (out["ms_per_step"] * 2e-3)) / out["value"] < 0.01
 
 
@@ -235,6 +236,8 @@ def test_bench_contract_conv_groups_n8(tmp_path, model, k, bs):
     assert out["config"]["parallelism"] == f"groups{k}x{8 // k}"
     assert out["config"]["model"].startswith("conv")
     assert abs(out["value"] - k * bs * 2 / (out["ms_per_step"] * 2e-3)) / out["value"] < 0.01
+    # every replica of every trial ends bitwise equal (bench gathers the parameters)
+    assert out["config"]["replicas_bitwise_equal"] is True and out["config"]["valid"] is True
 
 
 def test_vae_hpo_conv_ckpt_and_resume(tmp_path):
