@@ -132,11 +132,13 @@ def test_two_shot_is_bitwise_one_shot(native_ext):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_missing_peer_times_out(native_ext):
+@pytest.mark.parametrize("two", [-1, 0])
+def test_missing_peer_times_out(native_ext, two):
     """Rank 1 never launches: rank 0's blocks give up after the timeout and
-    report the first bucket instead of spinning forever."""
+    report the first bucket instead of spinning forever (one-shot, and the
+    two-shot form's reduce-scatter wait)."""
     C = native_ext
-    flats, reds = _pair(C, 2, 8192, [0, 4096, 8192], timeout=0.2)
+    flats, reds = _pair(C, 2, 8192, [0, 4096, 8192], timeout=0.2, two_shot_min_bytes=two)
     reds[0].launch_all()
     reds[0].wait_all()
     torch.cuda.synchronize()
