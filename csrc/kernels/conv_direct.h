@@ -55,11 +55,19 @@ struct DcArgs {
   int nimg;
 };
 
-template <int MODE_, int CA_, int WA_, int NCOLS_, int NB_, int R_, int WM_, int S_, int AL_, int BE_, int MK_>
+// KS_ = 2: two groups of four waves split every weight stage's k-steps (group
+// g multiplies k-steps 2g and 2g + 1 of each 64-deep stage; group 1's
+// accumulators are added into group 0's before the epilogue). For the
+// deep-K layers with one output tile per CU: two waves per SIMD, so one
+// wave's LDS fragment latency hides behind the other's MFMAs.
+// HS_: weight stages per ring hand-off (wait + barrier + refill): 2 halves the
+// hand-offs and doubles the MFMAs between them (needs S >= 2 HS).
+template <int MODE_, int CA_, int WA_, int NCOLS_, int NB_, int R_, int WM_, int S_, int AL_, int BE_, int MK_,
+          int KS_ = 1, int HS_ = 1>
 struct DcCfg {
   static constexpr int MODE = MODE_, CA = CA_, WA = WA_, NCOLS = NCOLS_, NB = NB_, R = R_, S = S_;
   static constexpr int AL = AL_, BE = BE_, MK = MK_;
-  static constexpr int WAVES = 4, THREADS = 256;
+  static constexpr int KS = KS_, HS = HS_, WAVES = 4 * KS_, THREADS = 64 * WAVES;
   static constexpr bool CONV = MODE == 0;
   static constexpr int OW = CONV ? WA / 2 : WA;      // tile row width (output / class-grid pixels)
   static constexpr int OH = OW;
@@ -79,7 +87,7 @@ struct DcCfg {
   static constexpr int NBI = BROWS / 8;              // DMA instructions per stage
   static constexpr int NBW = NBI / WAVES;
   static constexpr int WM = CONV ? WM_ : 1;
-  static constexpr int WN = CONV ? WAVES / WM_ : 1;
+  static constexpr int WN = CONV ? 4 / WM_ : 1;  // per k-group of four waves
   static constexpr int TM = CONV ? MT / WM : MT;     // wave tile
   static constexpr int TN = CONV ? NB / WN : NB;
   static constexpr int FM = TM / 32, FN = TN / 32;
@@ -95,8 +103,10 @@ struct DcCfg {
   static_assert(WAVES * STG <= CS_OFF, "dconv epilogue staging");
   static_assert(CA % 16 == 0 && NBI % WAVES == 0 && FM >= 1 && FN >= 1, "dconv tile");
   static_assert(TM % 32 == 0 && TN % 32 == 0 && OH % R == 0 && NCOLS % NB == 0, "dconv tile");
-  static_assert(K % 64 == 0 && S >= 2 && NSTAGE >= S && NBW * (S - 1) <= 63, "dconv pipeline");
+  static_assert(K % 64 == 0 && S >= 2 * HS && NSTAGE >= S && NSTAGE % HS == 0 && NBW * (S - 1) <= 63,
+                "dconv pipeline");
   static_assert(MK < NCH && LDS <= 160 * 1024, "dconv LDS");
+  static_assert(KS == 1 || (KS == 2 && 4 * STG + 4 * FM * FN * 64 * 64 <= CS_OFF), "dconv k-group exchange");
 };
 
 // vmcnt wait leaving `n` (<= MAXN) newer DMA stages of NBW instructions in flight.
@@ -177,9 +187,10 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
 #pragma unroll
   for (int s = 0; s < S; ++s) issue_stage(s);  // the whole ring in flight
 
-  // ---- per-lane fragment coordinates
-  const int wm = CF::CONV ? w / CF::WN : 0, wn = CF::CONV ? w % CF::WN : 0;
-  const int cls = CF::CONV ? 0 : w;
+  // ---- per-lane fragment coordinates (wl: wave within its k-group, kg0: the group's first k-step)
+  const int wl = w & 3, kg0 = CF::KS == 2 ? 2 * (w >> 2) : 0;
+  const int wm = CF::CONV ? wl / CF::WN : 0, wn = CF::CONV ? wl % CF::WN : 0;
+  const int cls = CF::CONV ? 0 : wl;
   int ea = 0, eb = 0, oa = 0, ob = 0;
   if constexpr (!CF::CONV) {
     // class (ca, cb): output parity (oa, ob); taps (t0, t1) read A rows a + ea - t0
@@ -250,10 +261,66 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
       for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma32(af[fm], bfr[fn], acc[fm][fn]);
   };
 
-  dc_wait_stages<NBW, S - 1>(S - 1);  // the patch and stage 0 have landed (this wave's part)
+  dc_wait_stages<NBW, S - 1>(S - CF::HS);  // the patch and stages 0 .. HS-1 have landed (this wave's part)
   stage_barrier();
   dc_stamp(a.stamps, 1);
 
+#ifdef MDT_DC_STAGE_STAMPS  // per-stage timeline of the workgroup-leader wave (bench/dconv_stage_stamps.py)
+#define DC_SS(k)                                                                                          \
+  if (a.stamps && threadIdx.x == 0)                                                                        \
+    a.stamps[(size_t)gridDim.x * 8 + ((size_t)blockIdx.x * NSTAGE + st) * 4 + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define DC_SS(k)
+#endif
+#ifndef MDT_DC_STEP_AHEAD
+  // Fragments of a whole hand-off group (HS stages) are loaded one group
+  // ahead: each wave holds its NF = HS x KPW k-steps of group g in registers
+  // (set `cur`) while it reads those of group g + 1 (set `nxt`). Per group:
+  // the first half of cur's MFMAs, then the ring hand-off (wait for group
+  // g + 1, barrier, refill group g's slots with stages + S: every wave's reads
+  // of group g completed at the previous hand-off), then nxt's LDS reads, then
+  // cur's second half, under which their latency hides. sched_barrier(0) pins
+  // the order.
+  constexpr int HS = CF::HS, KPW = 4 / CF::KS, NF = HS * KPW, KH = NF / 2, NG = NSTAGE / HS;
+  bf16x8 fa0[NF][FM], fb0[NF][FN], fa1[NF][FM], fb1[NF][FN];
+  auto load_group = [&](int g, bf16x8(&fa)[NF][FM], bf16x8(&fb)[NF][FN]) {
+#pragma unroll
+    for (int h = 0; h < HS; ++h)
+#pragma unroll
+      for (int i = 0; i < KPW; ++i) load_frags(g * HS + h, kg0 + i, fa[h * KPW + i], fb[h * KPW + i]);
+  };
+  auto step = [&](int g, const bf16x8(&ca)[NF][FM], const bf16x8(&cb)[NF][FN], bf16x8(&na)[NF][FM],
+                  bf16x8(&nb_)[NF][FN]) {
+    const int st = g * HS;
+    DC_SS(0);
+#pragma unroll
+    for (int i = 0; i < KH; ++i) mma(ca[i], cb[i]);
+    __builtin_amdgcn_sched_barrier(0);
+    DC_SS(1);
+    if (g + 1 < NG) {
+      // issued: stages < min(NSTAGE, st + S); needed: stages < st + 2 HS
+      const int ahead = (st + S < NSTAGE ? st + S : NSTAGE) - st - 2 * HS;
+      dc_wait_stages<NBW, S - 1>(ahead);
+      DC_SS(2);
+      stage_barrier();
+      DC_SS(3);
+#pragma unroll
+      for (int h = 0; h < HS; ++h)
+        if (st + h + S < NSTAGE) issue_stage(st + h + S);
+      load_group(g + 1, na, nb_);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = KH; i < NF; ++i) mma(ca[i], cb[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  load_group(0, fa0, fb0);
+#pragma unroll 1
+  for (int g = 0; g < NG; g += 2) {
+    step(g, fa0, fb0, fa1, fb1);
+    if (g + 1 < NG) step(g + 1, fa1, fb1, fa0, fb0);
+  }
+#else
   // Fragments are loaded one k-step ahead of the MFMAs that use them, so LDS
   // latency hides under the previous step's MFMAs; the ring hand-off (wait for
   // stage st+1, barrier, refill slot st % S with stage st+S) sits at the last
@@ -262,9 +329,31 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
   // fragment load next to its MFMA and every k-step waits out the full LDS
   // latency (s_waitcnt lgkmcnt(0) right before each MFMA).
   bf16x8 afA[FM], bfA[FN], afB[FM], bfB[FN];
+  if constexpr (CF::KS == 2) {
+    // group g: k-steps kg0, kg0 + 1 of every stage (two MFMA steps per stage and wave)
+    load_frags(0, kg0, afA, bfA);
+#pragma unroll 1
+    for (int st = 0; st < NSTAGE; ++st) {
+      load_frags(st, kg0 + 1, afB, bfB);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(afA, bfA);
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 1 < NSTAGE) {
+        const int ahead = NSTAGE - 2 - st;
+        dc_wait_stages<NBW, S - 1>(ahead < S - 2 ? ahead : S - 2);
+        stage_barrier();
+        if (st + S < NSTAGE) issue_stage(st + S);
+        load_frags(st + 1, kg0, afA, bfA);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma(afB, bfB);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
   load_frags(0, 0, afA, bfA);
 #pragma unroll 1
   for (int st = 0; st < NSTAGE; ++st) {
+    DC_SS(0);
     load_frags(st, 1, afB, bfB);
     __builtin_amdgcn_sched_barrier(0);
     mma(afA, bfA);
@@ -277,10 +366,13 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
     __builtin_amdgcn_sched_barrier(0);
     mma(afA, bfA);
     __builtin_amdgcn_sched_barrier(0);
+    DC_SS(1);
     if (st + 1 < NSTAGE) {
       const int ahead = NSTAGE - 2 - st;
       dc_wait_stages<NBW, S - 1>(ahead < S - 2 ? ahead : S - 2);
+      DC_SS(2);
       stage_barrier();
+      DC_SS(3);
       if (st + S < NSTAGE) issue_stage(st + S);
       load_frags(st + 1, 0, afA, bfA);
     }
@@ -288,12 +380,36 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
     mma(afB, bfB);
     __builtin_amdgcn_sched_barrier(0);
   }
+  }
+#endif
+#undef DC_SS
   dc_stamp(a.stamps, 2);
 
   // ---- epilogue, per 32-row slice: fragments -> wave-private LDS staging ->
   // row-contiguous 4-column pieces per lane: bias, ReLU, mask (8-B loads),
   // column sums, 8-B bf16 / 16-B f32 stores
   stage_barrier();  // every wave is done with the patch / ring
+  const bool store_wave = CF::KS == 1 || w < 4;
+  if constexpr (CF::KS == 2) {  // group 1's accumulators into group 0's (fragment order, past the staging slices)
+    float* xg = reinterpret_cast<float*>(lds + 4 * CF::STG) + (size_t)wl * FM * FN * 16 * 64;
+    if (w >= 4) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) xg[((i * FN + j) * 16 + v) * 64 + lane] = acc[i][j][v];
+    }
+    __syncthreads();
+    if (w < 4) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) acc[i][j][v] += xg[((i * FN + j) * 16 + v) * 64 + lane];
+    }
+  }
   constexpr int TN = CF::TN, SP = CF::SPITCH;
   constexpr int LPR = TN / 4;       // lanes per row
   constexpr int RPI = 64 / LPR;     // rows per pass
@@ -304,7 +420,7 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
   if (a.bias) bv = *reinterpret_cast<const float4*>(a.bias + col0);
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int fm = 0; fm < FM; ++fm) {
+  for (int fm = 0; fm < (store_wave ? FM : 0); ++fm) {
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn)
 #pragma unroll
@@ -353,7 +469,7 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int sh = LPR; sh < 64; sh <<= 1) cs[j] += __shfl_xor(cs[j], sh, 64);
-    if (lane < LPR) *reinterpret_cast<float4*>(sc + w * TN + 4 * cq) = float4{cs[0], cs[1], cs[2], cs[3]};
+    if (lane < LPR && store_wave) *reinterpret_cast<float4*>(sc + w * TN + 4 * cq) = float4{cs[0], cs[1], cs[2], cs[3]};
     __syncthreads();
     if (tid < CF::NB) {
       float t = 0.f;
@@ -372,7 +488,7 @@ __device__ __forceinline__ void dconv_body(const DcArgs& a, uint8_t* lds, int ti
 }
 
 template <class CF>
-__global__ void __launch_bounds__(256) dconv_k(DcArgs a) {
+__global__ void __launch_bounds__(CF::THREADS) dconv_k(DcArgs a) {
   __shared__ __attribute__((aligned(1024))) uint8_t lds[CF::LDS];
   dconv_body<CF>(a, lds, xcd_remap(blockIdx.x, gridDim.x));
 }
@@ -388,8 +504,18 @@ using DcS2 = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7>;    // conv 32x32x64 ->
 using DcT2 = DcCfg<1, 128, 16, 64, 32, 4, 1, 3, 0, 0, 15>;   // tconv 16x16x128 -> 32x32x64
 using DcT3 = DcCfg<1, 64, 32, 32, 32, 4, 1, 3, 0, 1, 7>;     // tconv 32x32x64 -> 64x64x32
 // 16x16 <-> 8x8 layers: one image (conv, M = 64) / the whole 8x8 class grid
-// (tconv, 4 x 64 rows) per workgroup, 64 / 32 output channels
-using DcS3 = DcCfg<0, 128, 16, 256, 64, 8, 2, 4, 4, 0, 15>;  // conv 16x16x128 -> 8x8x256
-using DcT1 = DcCfg<1, 256, 8, 128, 32, 8, 1, 3, 8, 0, 15>;   // tconv 8x8x256 -> 16x16x128
+// (tconv, 4 x 64 rows) per workgroup, 64 / 32 output channels; one workgroup
+// per CU, so two k-groups of four waves (two waves per SIMD) and two stages
+// per hand-off over a ring of 6: enc4 forward 16.4 -> 13.0 us, dec1 12.6 ->
+// 11.4 us at B = 64 against one k-group / one stage per hand-off
+// (profiles/r3_dconv)
+//                mode CA  WA NCOLS NB  R  WM S  AL BE MK KS HS
+using DcS3 = DcCfg<0, 128, 16, 256, 64, 8, 2, 6, 4, 0, 15, 2, 2>;  // conv 16x16x128 -> 8x8x256
+using DcT1 = DcCfg<1, 256, 8, 128, 32, 8, 1, 6, 8, 0, 15, 2, 2>;   // tconv 8x8x256 -> 16x16x128
+// A/B variants (MDT_DCONV_VAR): 4 two stages per hand-off, 5 and two k-groups
+using DcS1v4 = DcCfg<0, 32, 64, 64, 64, 4, 2, 4, 0, 2, 3, 1, 2>;
+using DcS2v4 = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7, 1, 2>;
+using DcS1v5 = DcCfg<0, 32, 64, 64, 64, 4, 2, 4, 0, 2, 3, 2, 2>;
+using DcS2v5 = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7, 2, 2>;
 
 }  // namespace mdt
