@@ -498,9 +498,12 @@ __global__ void __launch_bounds__(CF::THREADS) dconv_k(DcArgs a) {
 // R = 4 rows per workgroup (two workgroups per CU, <= 80 KB LDS): measured
 // 15-18 % faster than R = 8 (one per CU) and 3-4 % faster than R = 2 (three
 // per CU, shallower weight rings) at B = 64 and 128 (profiles/r2_dconv).
-//                mode CA  WA NCOLS NB  R  WM S  AL BE MK
-using DcS1 = DcCfg<0, 32, 64, 64, 64, 4, 2, 4, 0, 2, 3>;     // conv 64x64x32 -> 32x32x64
-using DcS2 = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7>;    // conv 32x32x64 -> 16x16x128
+// The convs take two stages per hand-off (HS = 2): 11.5 -> 11.0 us (64x64)
+// and 12.3 -> 10.6 us (32x32) at B = 64 (profiles/r3_dconv2); two k-groups
+// there were slower (14.2 / 13.5 us: two 512-thread workgroups per CU).
+//                mode CA  WA NCOLS NB  R  WM S  AL BE MK KS HS
+using DcS1 = DcCfg<0, 32, 64, 64, 64, 4, 2, 4, 0, 2, 3, 1, 2>;     // conv 64x64x32 -> 32x32x64
+using DcS2 = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7, 1, 2>;    // conv 32x32x64 -> 16x16x128
 using DcT2 = DcCfg<1, 128, 16, 64, 32, 4, 1, 3, 0, 0, 15>;   // tconv 16x16x128 -> 32x32x64
 using DcT3 = DcCfg<1, 64, 32, 32, 32, 4, 1, 3, 0, 1, 7>;     // tconv 32x32x64 -> 64x64x32
 // 16x16 <-> 8x8 layers: one image (conv, M = 64) / the whole 8x8 class grid
@@ -512,10 +515,5 @@ using DcT3 = DcCfg<1, 64, 32, 32, 32, 4, 1, 3, 0, 1, 7>;     // tconv 32x32x64 -
 //                mode CA  WA NCOLS NB  R  WM S  AL BE MK KS HS
 using DcS3 = DcCfg<0, 128, 16, 256, 64, 8, 2, 6, 4, 0, 15, 2, 2>;  // conv 16x16x128 -> 8x8x256
 using DcT1 = DcCfg<1, 256, 8, 128, 32, 8, 1, 6, 8, 0, 15, 2, 2>;   // tconv 8x8x256 -> 16x16x128
-// A/B variants (MDT_DCONV_VAR): 4 two stages per hand-off, 5 and two k-groups
-using DcS1v4 = DcCfg<0, 32, 64, 64, 64, 4, 2, 4, 0, 2, 3, 1, 2>;
-using DcS2v4 = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7, 1, 2>;
-using DcS1v5 = DcCfg<0, 32, 64, 64, 64, 4, 2, 4, 0, 2, 3, 2, 2>;
-using DcS2v5 = DcCfg<0, 64, 32, 128, 64, 4, 2, 4, 0, 1, 7, 2, 2>;
 
 }  // namespace mdt

@@ -68,14 +68,6 @@ static bool direct_small() {
   return on;
 }
 
-static int dconv_var() {
-  static const int v = [] {
-    const char* e = getenv("MDT_DCONV_VAR");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 int direct_cfg(int mode, const ConvDesc& d, bool fwd) {
   static const bool on = [] {
     const char* e = getenv("MDT_CONV_DIRECT");
@@ -382,16 +374,8 @@ int launch_direct(int cfg, const void* A, const void* B16, const ConvDesc& d, co
   a.relu = relu;
   a.nimg = d.N;
   switch (cfg) {
-    case 0:
-      if (dconv_var() == 4) launch_dc<DcS1v4>(a, s);
-      else if (dconv_var() == 5) launch_dc<DcS1v5>(a, s);
-      else launch_dc<DcS1>(a, s);
-      break;
-    case 1:
-      if (dconv_var() == 4) launch_dc<DcS2v4>(a, s);
-      else if (dconv_var() == 5) launch_dc<DcS2v5>(a, s);
-      else launch_dc<DcS2>(a, s);
-      break;
+    case 0: launch_dc<DcS1>(a, s); break;
+    case 1: launch_dc<DcS2>(a, s); break;
     case 2: launch_dc<DcT2>(a, s); break;
     case 3: launch_dc<DcT3>(a, s); break;
     case 4: launch_dc<DcS3>(a, s); break;
