@@ -124,7 +124,6 @@ enum JobKindBase : int {
   kJobWtrans = 5004,
   kJobLossStep = 5005,   // loss reduction + step advance (fused 28x28 step)
   kJobDconv = 6000,      // + direct cfg       (patch-resident direct conv, conv_direct.h)
-  kJobDwgrad = 6100,     // + dwgrad cfg       (direct weight gradient, conv_dwgrad.h)
 };
 
 // Up to kMaxMultiJobs jobs of any kind of the multi-job kernel (jobs_multi_k).

@@ -500,8 +500,8 @@ int mdt_wgrad(const void* G16, const void* X, int x_is_f32, ConvDesc d, float* o
   if (q.cfg >= 100) {
     if (x_is_f32) return 3;
     const DwArgs da{reinterpret_cast<const __bf16*>(X), reinterpret_cast<const __bf16*>(G16), out, d.N, g_dc_stamps};
-    if (q.cfg == 100) hipLaunchKernelGGL(dwgrad_k<DwL1>, dim3(d.N * 4), dim3(256), 0, s, da);
-    else if (q.cfg == 101) hipLaunchKernelGGL(dwgrad_k<DwL2>, dim3(d.N * 4), dim3(256), 0, s, da);
+    if (q.cfg == 100) hipLaunchKernelGGL(dwgrad_k<DwL1>, dim3(d.N * 4), dim3(DwL1::THREADS), 0, s, da);
+    else if (q.cfg == 101) hipLaunchKernelGGL(dwgrad_k<DwL2>, dim3(d.N * 4), dim3(DwL2::THREADS), 0, s, da);
     else return 2;
     return (int)hipGetLastError();
   }

@@ -100,14 +100,6 @@ struct JDc {
   }
 };
 
-template <int CFG, class CF>
-struct JDw {
-  static constexpr int ID = kJobDwgrad + CFG, LDS = CF::LDS;
-  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
-    dwgrad_body<CF>(job_args<DwArgs>(j), lds, b);
-  }
-};
-
 struct JColsum {
   static constexpr int ID = kJobColsum, LDS = 0;
   static __device__ __forceinline__ void run(const JobBlob& j, uint8_t*, int b) { colsum_body(job_args<ColsumArgs>(j), b); }
@@ -260,11 +252,8 @@ using IgT2 = JIg<kModeTconv, 2, F2>;
 using IgT4 = JIg<kModeTconv, 4, F4>;
 using IgT5 = JIg<kModeTconv, 5, F5>;
 using IgT6 = JIg<kModeTconv, 6, F6>;
-using DcJS1 = JDc<0, DcS1>;
 using DcJS2 = JDc<1, DcS2>;
 using DcJT2 = JDc<2, DcT2>;
-using DcJT3 = JDc<3, DcT3>;
-using DwJ1 = JDw<0, DwL1>;
 
 // kinds sorted ascending within each entry
 const Combo kCombos[] = {
@@ -314,12 +303,11 @@ const Combo kCombos[] = {
     COMBO2(IgC4, JWtrans),
     COMBO2(IgC5, JWtrans),
     COMBO2(IgC6, JWtrans),
-    // 128x128 middle layers: direct backward-data || weight gradient (im2col
-    // for the 32x32 <-> 16x16 pair, direct for the 64x64 <-> 32x32 pair)
+    // 128x128 32x32 <-> 16x16 layers: direct backward-data || im2col weight
+    // gradient (the 64x64 <-> 32x32 pair's direct weight gradient runs 8-wave
+    // workgroups in its own launch: 15.9 -> 14.2 us, profiles/r3_dconv2)
     COMBO2(Wg0, DcJS2),
     COMBO2(Wg0, DcJT2),
-    COMBO2(DcJS1, DwJ1),
-    COMBO2(DcJT3, DwJ1),
 };
 
 #undef COMBO3
@@ -404,11 +392,7 @@ int mdt_job_wgrad(JobBlob* j, const void* G16, const void* X, int x_is_f32, Conv
   if (build_wgrad(G16, X, d, out, &a, &q)) return 1;
   memset(j, 0, sizeof(*j));
   if (q.cfg == 110) j->kind = kJobThinWgM + (x_is_f32 ? 1 : 0);  // MFMA thin weight gradient
-  else if (q.cfg >= 100) {  // direct weight gradient (conv_dwgrad.h)
-    if (x_is_f32 || q.cfg != 100) return 0;  // kind 0: its own launch
-    j->kind = kJobDwgrad + (q.cfg - 100);
-    j->nblk = d.N * 4;
-    put_args(j, DwArgs{reinterpret_cast<const __bf16*>(X), reinterpret_cast<const __bf16*>(G16), out, d.N, nullptr});
+  else if (q.cfg >= 100) {  // direct weight gradient (conv_dwgrad.h): 512-thread workgroups, its own launch
     return 0;
   }
   else if (!q.thin) j->kind = x_is_f32 ? 0 : kJobWgrad + q.cfg;
