@@ -191,10 +191,21 @@ __device__ __forceinline__ void run_multi_job(const JobBlob& j, uint8_t* lds, in
 __global__ void __launch_bounds__(256) jobs_multi_k(const JobPackN* __restrict__ p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kMultiLds];
   const int b = blockIdx.x;
+  // every start in ONE batch of scalar loads, then count the jobs this block
+  // is past (starts ascend over [0, n)): a while loop over p->start was one
+  // dependent load per job in front of the table's later (longest) jobs
+  int st[kMaxMultiJobs];
+#pragma unroll
+  for (int k = 0; k < kMaxMultiJobs; ++k) st[k] = p->start[k];
   const int n = p->n;
-  int i = 0;
-  while (i + 1 < n && b >= p->start[i + 1]) ++i;
-  run_multi_job(p->j[i], lds, b - p->start[i]);
+  int i = 0, s0 = st[0];
+#pragma unroll
+  for (int k = 1; k < kMaxMultiJobs; ++k)
+    if (k < n && b >= st[k]) {
+      i = k;
+      s0 = st[k];
+    }
+  run_multi_job(p->j[i], lds, b - s0);
 }
 
 __host__ inline bool multi_kind_ok(int k) {

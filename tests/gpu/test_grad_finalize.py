@@ -41,3 +41,52 @@ def test_grad_finalize_vec4_units_match_scalar_units(ns, native_ext):
     for a, b in zip(by[(256, True)][1:], by[(1024, True)][1:]):
         assert torch.equal(a, b)
     assert not torch.equal(by[(1024, True)][1], P0)  # Adam actually updated the parameters
+
+
+def _emulated_sum(slab, rp):
+    """The finalize kernel's summation order in float32 (conv_small.h): thread
+    row rl sums slabs rl, rl + rp, ... into 4 interleaved accumulators (full
+    quads, the remainder into the first), then row 0 adds the rp row sums in
+    order starting from 0."""
+    ns = slab.shape[0]
+    z = torch.zeros(slab.shape[1], dtype=torch.float32)
+    g = z.clone()
+    for rl in range(rp):
+        ks = list(range(rl, ns, rp))
+        a = [z.clone() for _ in range(4)]
+        q = len(ks) // 4
+        for i in range(q):
+            for j in range(4):
+                a[j] = a[j] + slab[ks[4 * i + j]]
+        for k in range(4 * q, len(ks)):
+            a[0] = a[0] + slab[ks[k]]
+        g = g + ((a[0] + a[1]) + (a[2] + a[3]))
+    return g
+
+
+@pytest.mark.parametrize("ns,cnt", [(5, 16), (20, 128), (131, 16), (131, 256), (300, 64), (3, 1024), (16, 1024),
+                                    (20, 1024)])
+def test_grad_finalize_matches_emulated_order(ns, cnt, native_ext):
+    """Bitwise: the batched-load path (<= 16 slabs per thread) and the loop
+    path (more) both sum in the documented order -- units of `cnt` elements,
+    rp = 256 / cnt partial rows per column (cnt 1024: 4 elements per thread)."""
+    C = native_ext
+    dev = torch.device("cuda")
+    numel = 2048 + 4
+    slab = torch.randn(ns, numel)
+    ds = slab.to(dev).reshape(-1)
+    segs = C.make_grad_segs([[0, numel, ds.data_ptr(), ns, 0, 0, 0, 0, -1]], 0)
+    units = [[0, st, min(cnt, numel - st)] for st in range(0, numel, cnt)]
+    state = C.TrialState(0)
+    state.set_step(False, 1)
+    G = torch.zeros(numel, device=dev)
+    P, M, V = torch.zeros(numel, device=dev), torch.zeros(numel, device=dev), torch.zeros(numel, device=dev)
+    w16 = torch.zeros(numel, dtype=torch.bfloat16, device=dev)
+    C.grad_finalize(P, G, M, V, w16, segs, C.make_grad_units(units, 0), len(units), state.train_state,
+                    state.hparams, False)
+    torch.cuda.synchronize()
+    got = G.cpu()
+    for st, n in [(u[1], u[2]) for u in units]:
+        rp = 1 if n > 256 else 256 // n  # a short tail unit takes the scalar path
+        want = _emulated_sum(slab[:, st:st + n], rp)
+        assert torch.equal(got[st:st + n], want), (st, n, rp)
