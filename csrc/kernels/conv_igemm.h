@@ -123,6 +123,7 @@ enum JobKindBase : int {
   kJobFinalize = 5003,
   kJobWtrans = 5004,
   kJobLossStep = 5005,   // loss reduction + step advance (fused 28x28 step)
+  kJobComm = 5006,       // fused xGMI all-reduce + Adam over finalize units (comm_jobs.h)
   kJobDconv = 6000,      // + direct cfg       (patch-resident direct conv, conv_direct.h)
 };
 

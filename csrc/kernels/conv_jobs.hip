@@ -24,6 +24,7 @@
 #include "conv_direct.h"
 #include "conv_dwgrad.h"
 #include "conv_igemm_dev.h"
+#include "comm_jobs.h"
 #include "conv_small.h"
 #include "conv_thin.h"
 #include "conv_thin_wg.h"
@@ -127,6 +128,14 @@ struct JWtrans {
   }
 };
 
+// gradient all-reduce push / reduce+Adam over finalize units (comm_jobs.h)
+struct JComm {
+  static constexpr int ID = kJobComm, LDS = kCommLds;
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int b) {
+    comm_unit_body(job_args<CommJobArgs>(j), lds, b);
+  }
+};
+
 struct JLossStep {
   static constexpr int ID = kJobLossStep, LDS = 64;
   static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int) {
@@ -151,7 +160,7 @@ struct JobPackN {
 constexpr int kMultiLds = cmax(cmax(cmax(wgrad_lds_bytes<W0>(), wgrad_lds_bytes<W1>()),
                                     cmax(wgrad_lds_bytes<W3>(), wgrad_lds_bytes<W4>())),
                                cmax(cmax(wgrad_lds_bytes<W2>(), wgrad_lds_bytes<W5>()),
-                                    cmax(JFinalize::LDS, JColsum::LDS + 64)));
+                                    cmax(cmax(JFinalize::LDS, JComm::LDS), JColsum::LDS + 64)));
 
 template <int CFG, class TC>
 __device__ __forceinline__ bool run_wg_cfg(const JobBlob& j, uint8_t* lds, int b) {
@@ -178,6 +187,7 @@ __device__ __forceinline__ void run_multi_job(const JobBlob& j, uint8_t* lds, in
     case kJobLossStep: JLossStep::run(j, lds, lb); break;
     case kJobLoss: JLoss::run(j, lds, lb); break;
     case kJobFinalize: JFinalize::run(j, lds, lb); break;
+    case kJobComm: JComm::run(j, lds, lb); break;
     case kJobColsum: JColsum::run(j, lds, lb); break;
     default: break;
   }
@@ -212,7 +222,7 @@ __host__ inline bool multi_kind_ok(int k) {
   if (k >= kJobWgrad && k <= kJobWgrad + 5) return true;
   if (k >= kJobWgradThin && k <= kJobWgradThin + 5) return true;
   if (k >= kJobWgradThin + 20 && k <= kJobWgradThin + 25) return true;
-  return k == kJobLossStep || k == kJobLoss || k == kJobFinalize || k == kJobColsum;
+  return k == kJobLossStep || k == kJobLoss || k == kJobFinalize || k == kJobColsum || k == kJobComm;
 }
 
 template <class A, class B, class C>
@@ -460,6 +470,22 @@ int mdt_job_finalize(JobBlob* j, float* P, float* G, float* Mo, float* Vo, void*
   put_args(j, FinalizeArgs{P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16), reinterpret_cast<const GradSeg*>(segs),
                            reinterpret_cast<const GradUnit*>(units), reinterpret_cast<const TrainState*>(st),
                            reinterpret_cast<const HParams*>(hp), do_adam});
+  return 0;
+}
+
+int mdt_job_comm(JobBlob* j, float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs, const void* units,
+                 int nunits, const void* st, const void* hp, int do_adam, const void* ctx, int mode) {
+  memset(j, 0, sizeof(*j));
+  if (nunits <= 0 || !ctx || mode < kCommPush || mode > kCommPushReduce) return 1;
+  j->kind = kJobComm;
+  j->nblk = nunits;
+  CommJobArgs a{};
+  a.fa = FinalizeArgs{P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16), reinterpret_cast<const GradSeg*>(segs),
+                      reinterpret_cast<const GradUnit*>(units), reinterpret_cast<const TrainState*>(st),
+                      reinterpret_cast<const HParams*>(hp), do_adam};
+  a.ctx = reinterpret_cast<const CommCtx*>(ctx);
+  a.mode = mode;
+  put_args(j, a);
   return 0;
 }
 

@@ -315,6 +315,51 @@ struct FinalizeArgs {
 
 constexpr int kFinalizeThreads = 256;
 
+// Partial-slab sums shared by the finalize bodies here and the fused
+// all-reduce jobs (comm_jobs.h): one summation order everywhere, so a
+// gradient finalized on its own and one finalized inside a collective job
+// carry the same bits.
+// 4 consecutive elements (vec4 units): 4 interleaved accumulators over the slabs
+__device__ __forceinline__ f32x4 slab_sum4(const float* p, long long n, int nsplit) {
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  f32x4 a0 = z, a1 = z, a2 = z, a3 = z;
+  int s = 0;
+  for (; s + 3 < nsplit; s += 4) {
+    a0 += *reinterpret_cast<const f32x4*>(p + (long long)s * n);
+    a1 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 1) * n);
+    a2 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 2) * n);
+    a3 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 3) * n);
+  }
+  for (; s < nsplit; ++s) a0 += *reinterpret_cast<const f32x4*>(p + (long long)s * n);
+  return z + ((a0 + a1) + (a2 + a3));
+}
+// one element (tail of a vec4 unit), same order as one lane of slab_sum4
+__device__ __forceinline__ float slab_sum1(const float* p, long long n, int nsplit) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 3 < nsplit; s += 4) {
+    a0 += p[(long long)s * n];
+    a1 += p[(long long)(s + 1) * n];
+    a2 += p[(long long)(s + 2) * n];
+    a3 += p[(long long)(s + 3) * n];
+  }
+  for (; s < nsplit; ++s) a0 += p[(long long)s * n];
+  return 0.f + ((a0 + a1) + (a2 + a3));
+}
+// scalar units: slabs rl, rl + rp, ... of one column (row lane rl of rp)
+__device__ __forceinline__ float slab_partial(const float* p, long long n, int nsplit, int rl, int rp) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = rl;
+  for (; s + 3 * rp < nsplit; s += 4 * rp) {
+    a0 += p[(long long)s * n];
+    a1 += p[(long long)(s + rp) * n];
+    a2 += p[(long long)(s + 2 * rp) * n];
+    a3 += p[(long long)(s + 3 * rp) * n];
+  }
+  for (; s < nsplit; s += rp) a0 += p[(long long)s * n];
+  return (a0 + a1) + (a2 + a3);
+}
+
 // Units of more than 256 elements (planned when a segment has <= 16 partial
 // slabs and 16-B aligned rows): each thread finalizes 4 consecutive elements
 // with 16-B loads/stores -- same per-element summation order as the scalar
@@ -331,18 +376,7 @@ __device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const 
   if (left >= 4) {
     f32x4 g;
     if (sg.slab) {
-      const float* p = sg.slab + e0;
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      f32x4 a0 = z, a1 = z, a2 = z, a3 = z;
-      int s = 0;
-      for (; s + 3 < sg.nsplit; s += 4) {
-        a0 += *reinterpret_cast<const f32x4*>(p + (long long)s * n);
-        a1 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 1) * n);
-        a2 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 2) * n);
-        a3 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 3) * n);
-      }
-      for (; s < sg.nsplit; ++s) a0 += *reinterpret_cast<const f32x4*>(p + (long long)s * n);
-      g = z + ((a0 + a1) + (a2 + a3));
+      g = slab_sum4(sg.slab + e0, n, sg.nsplit);
       if (!a.do_adam) *reinterpret_cast<f32x4*>(a.G + o) = g;
     } else {
       g = *reinterpret_cast<const f32x4*>(a.G + o);
@@ -371,17 +405,7 @@ __device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const 
   for (int j = 0; j < left; ++j) {  // segment tail (< 4 elements)
     float g;
     if (sg.slab) {
-      const float* p = sg.slab + e0 + j;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-      int s = 0;
-      for (; s + 3 < sg.nsplit; s += 4) {
-        a0 += p[(long long)s * n];
-        a1 += p[(long long)(s + 1) * n];
-        a2 += p[(long long)(s + 2) * n];
-        a3 += p[(long long)(s + 3) * n];
-      }
-      for (; s < sg.nsplit; ++s) a0 += p[(long long)s * n];
-      g = 0.f + ((a0 + a1) + (a2 + a3));
+      g = slab_sum1(sg.slab + e0 + j, n, sg.nsplit);
       if (!a.do_adam) a.G[o + j] = g;
     } else {
       g = a.G[o + j];
@@ -406,22 +430,7 @@ __device__ __forceinline__ void grad_finalize_body(const FinalizeArgs& a, float*
   }
   const int t = threadIdx.x, cnt = u.count, rp = kFinalizeThreads / cnt;
   const int col = t % cnt, rl = t / cnt;
-  float acc = 0.f;
-  if (sg.slab && rl < rp) {
-    const float* p = sg.slab + u.start + col;
-    const long long n = sg.numel;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int s = rl;
-    for (; s + 3 * rp < sg.nsplit; s += 4 * rp) {
-      a0 += p[(long long)s * n];
-      a1 += p[(long long)(s + rp) * n];
-      a2 += p[(long long)(s + 2 * rp) * n];
-      a3 += p[(long long)(s + 3 * rp) * n];
-    }
-    for (; s < sg.nsplit; s += rp) a0 += p[(long long)s * n];
-    acc = (a0 + a1) + (a2 + a3);
-  }
-  red[t] = acc;
+  red[t] = (sg.slab && rl < rp) ? slab_partial(sg.slab + u.start + col, sg.numel, sg.nsplit, rl, rp) : 0.f;
   __syncthreads();
   if (rl == 0) {
     const long long o = sg.off + u.start + col;

@@ -28,6 +28,22 @@ struct P2PArgs {
   long long timeout_ticks;              // s_memrealtime ticks (100 MHz)
 };
 
+// Device descriptor of the all-reduce JOBS (comm_jobs.h) over a gradient
+// arena of `numel` elements; built by XgmiP2PReducer.comm_ctx().
+struct CommCtx {
+  float* peer_recv[kP2PMaxRanks];      // every rank's receive region (device VA in this process)
+  unsigned* peer_flags[kP2PMaxRanks];  // every rank's flag array
+  unsigned* ep_push;                   // [numel] local epochs of the push phase
+  unsigned* ep_red;                    // [numel] local epochs of the reduce phase
+  int* status;                         // 0 ok; else 1 + 1000000 + arena offset of a unit whose wait timed out
+  long long numel;                     // gradient arena elements (receive stride)
+  int me, s;
+  float scale;                         // 1/s (averaging) or a test pre-multiplier
+  long long timeout_ticks;             // s_memrealtime ticks (100 MHz)
+};
+
+enum : int { kCommPush = 1, kCommReduce = 2, kCommPushReduce = 3 };
+
 }  // namespace mdt
 
 extern "C" int mdt_p2p_allreduce(const mdt::P2PArgs* a, int grid, hipStream_t stream);

@@ -50,6 +50,8 @@ int mdt_job_igemm(mdt::JobBlob* g, mdt::JobBlob* c, int mode, const void* A, int
 int mdt_job_finalize(mdt::JobBlob* j, float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs,
                      const void* units, int nunits, const void* st, const void* hp, int do_adam);
 int mdt_job_wtrans(mdt::JobBlob* j, const void* w16, void* w16t, const void* segs, const void* units, int nunits);
+int mdt_job_comm(mdt::JobBlob* j, float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs,
+                 const void* units, int nunits, const void* st, const void* hp, int do_adam, const void* ctx, int mode);
 int mdt_combine_reparam(const float* slab, int ks, const float* bias, float* mulv, float* eps, void* z16, float* z32,
                         int B, int Z, const void* st, const void* hp, unsigned stream, float* kld_part, hipStream_t s);
 int mdt_combine_reparam_blocks(int ks, int B, int Z);
@@ -560,6 +562,23 @@ void grad_finalize(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::T
      "grad_finalize");
 }
 
+// Record a fused all-reduce job (csrc/kernels/comm_jobs.h) over `nunits`
+// finalize units: mode 1 push, 2 reduce(+Adam), 3 both. `ctx` is the device
+// address from XgmiP2PReducer.comm_ctx(). Jobs only: they run inside a
+// jobs_multi_k launch next to other work of the step.
+void comm_job(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::Tensor w16, const at::Tensor& segs,
+              const at::Tensor& units, int64_t nunits, const at::Tensor& state, const at::Tensor& hparams,
+              bool do_adam, int64_t ctx, int64_t mode, Job* job) {
+  TORCH_CHECK(job != nullptr, "comm_job: records into a Job (no stand-alone launch)");
+  TORCH_CHECK(units.numel() >= nunits * (int64_t)sizeof(GradUnit), "comm_job: unit table too small");
+  TORCH_CHECK(P.numel() == G.numel() && M.numel() == G.numel() && V.numel() == G.numel() && w16.numel() == G.numel(),
+              "comm_job: arenas differ in size");
+  rc(mdt_job_comm(&job->main, P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(),
+                  w16.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits, state.data_ptr(),
+                  hparams.data_ptr(), do_adam ? 1 : 0, reinterpret_cast<const void*>((intptr_t)ctx), (int)mode),
+     "job_comm");
+}
+
 void wtrans(const at::Tensor& w16, at::Tensor w16t, const at::Tensor& segs, const at::Tensor& units, int64_t nunits,
             Job* job) {
   check_bf16(w16, "w16");
@@ -732,6 +751,9 @@ void bind_conv(pybind11::module& m) {
   m.def("grad_finalize", &grad_finalize, py::arg("P"), py::arg("G"), py::arg("M"), py::arg("V"), py::arg("w16"),
         py::arg("segs"), py::arg("units"), py::arg("nunits"), py::arg("state"), py::arg("hparams"),
         py::arg("do_adam"), py::arg("job") = py::none());
+  m.def("comm_job", &comm_job, py::arg("P"), py::arg("G"), py::arg("M"), py::arg("V"), py::arg("w16"),
+        py::arg("segs"), py::arg("units"), py::arg("nunits"), py::arg("state"), py::arg("hparams"),
+        py::arg("do_adam"), py::arg("ctx"), py::arg("mode"), py::arg("job"));
   m.def("wtrans", &wtrans, py::arg("w16"), py::arg("w16t"), py::arg("segs"), py::arg("units"), py::arg("nunits"),
         py::arg("job") = py::none());
   m.def("combine_reparam", &combine_reparam);

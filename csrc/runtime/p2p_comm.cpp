@@ -24,6 +24,11 @@
 //     bucket instead of hanging the GPU.
 // `connect_local` maps peers that live in the same process (single-GPU tests
 // run s "ranks" on one device, each with its own stream).
+// With `fused` the region also holds the receive slots / flags / epochs of the
+// all-reduce JOBS (csrc/kernels/comm_jobs.h): models that issue their own
+// backward launches put the push and the reduce+Adam of the gradient arena
+// into those launches instead of calling launch()/wait() (one stream, no
+// events); `comm_ctx()` is the device descriptor those jobs take.
 #include <hip/hip_runtime_api.h>
 
 #include <cstring>
@@ -36,8 +41,8 @@ namespace mdt {
 class XgmiP2PReducer : public StreamBuckets {
  public:
   XgmiP2PReducer(int64_t rank, int64_t size, at::Tensor flat, std::vector<int64_t> bounds, bool average,
-                 double scale, int64_t max_blocks, double timeout_s, int64_t two_shot_min_bytes)
-      : StreamBuckets(std::move(flat), std::move(bounds)), me_((int)rank), s_((int)size) {
+                 double scale, int64_t max_blocks, double timeout_s, int64_t two_shot_min_bytes, bool fused)
+      : StreamBuckets(std::move(flat), std::move(bounds)), me_((int)rank), s_((int)size), fused_(fused) {
     TORCH_CHECK(s_ >= 1 && s_ <= kP2PMaxRanks, "XgmiP2PReducer: group size must be 1..", kP2PMaxRanks);
     TORCH_CHECK(me_ >= 0 && me_ < s_, "XgmiP2PReducer: rank out of range");
     TORCH_CHECK(flat_.scalar_type() == torch::kFloat32, "XgmiP2PReducer: f32 gradient arena required");
@@ -69,6 +74,13 @@ class XgmiP2PReducer : public StreamBuckets {
     ep_byte_ = flags_byte_ + al(foff * 4);
     status_byte_ = ep_byte_ + al(eoff * 4);
     bytes_ = status_byte_ + 256;
+    if (fused_) {  // comm_jobs.h: recv [2][s][numel] f32 | flags [s][numel] u32 | epochs [2][numel] u32
+      const long long n = flat_.numel();
+      frecv_byte_ = bytes_;
+      fflags_byte_ = frecv_byte_ + al(2LL * s_ * n * 4);
+      fep_byte_ = fflags_byte_ + al((long long)s_ * n * 4);
+      bytes_ = fep_byte_ + al(2LL * n * 4);
+    }
     DeviceGuard dg(device_);
     MDT_HIP_CHECK(hipExtMallocWithFlags(&base_, (size_t)bytes_, hipDeviceMallocUncached));
     MDT_HIP_CHECK(hipMemset((char*)base_ + flags_byte_, 0, (size_t)(bytes_ - flags_byte_)));
@@ -80,6 +92,7 @@ class XgmiP2PReducer : public StreamBuckets {
   ~XgmiP2PReducer() override {
     DeviceGuard dg(device_);
     (void)hipStreamSynchronize(stream_);
+    if (ctx_) (void)hipFree(ctx_);
     for (int p = 0; p < s_; ++p)
       if (p != me_ && peer_base_[p] && opened_[p]) (void)hipIpcCloseMemHandle(peer_base_[p]);
     if (base_) (void)hipFree(base_);
@@ -127,6 +140,33 @@ class XgmiP2PReducer : public StreamBuckets {
     return v;
   }
   double scale() const { return scale_; }
+  bool fused() const { return fused_; }
+
+  // Device address of the CommCtx the fused all-reduce jobs take (built once,
+  // after connect; a one-rank group needs no connect).
+  int64_t comm_ctx() {
+    TORCH_CHECK(fused_, "XgmiP2PReducer: built without fused=True");
+    TORCH_CHECK(connected_ || s_ == 1, "XgmiP2PReducer: connect() before comm_ctx()");
+    if (!ctx_) {
+      DeviceGuard dg(device_);
+      CommCtx c{};
+      for (int p = 0; p < kP2PMaxRanks; ++p) {
+        c.peer_recv[p] = p < s_ ? (float*)((char*)peer_base_[p] + frecv_byte_) : nullptr;
+        c.peer_flags[p] = p < s_ ? (unsigned*)((char*)peer_base_[p] + fflags_byte_) : nullptr;
+      }
+      c.ep_push = (unsigned*)((char*)base_ + fep_byte_);
+      c.ep_red = c.ep_push + flat_.numel();
+      c.status = (int*)((char*)base_ + status_byte_);
+      c.numel = flat_.numel();
+      c.me = me_;
+      c.s = s_;
+      c.scale = scale_;
+      c.timeout_ticks = timeout_ticks_;
+      MDT_HIP_CHECK(hipMalloc(&ctx_, sizeof(CommCtx)));
+      MDT_HIP_CHECK(hipMemcpy(ctx_, &c, sizeof(CommCtx), hipMemcpyHostToDevice));
+    }
+    return (int64_t)(uintptr_t)ctx_;
+  }
   std::vector<int64_t> grids() const { return std::vector<int64_t>(grid_.begin(), grid_.end()); }
   std::vector<int64_t> two_shot() const { return std::vector<int64_t>(two_.begin(), two_.end()); }
 
@@ -159,6 +199,9 @@ class XgmiP2PReducer : public StreamBuckets {
 
  private:
   int me_, s_;
+  bool fused_ = false;
+  void* ctx_ = nullptr;
+  long long frecv_byte_ = 0, fflags_byte_ = 0, fep_byte_ = 0;
   float scale_ = 1.0f;
   long long timeout_ticks_ = 0;
   void* base_ = nullptr;
@@ -173,16 +216,18 @@ class XgmiP2PReducer : public StreamBuckets {
 void bind_p2p(pybind11::module& m) {
   namespace py = pybind11;
   auto c = py::class_<XgmiP2PReducer>(m, "XgmiP2PReducer")
-               .def(py::init<int64_t, int64_t, at::Tensor, std::vector<int64_t>, bool, double, int64_t, double, int64_t>(),
+               .def(py::init<int64_t, int64_t, at::Tensor, std::vector<int64_t>, bool, double, int64_t, double, int64_t, bool>(),
                     py::arg("rank"), py::arg("size"), py::arg("flat"), py::arg("bounds"), py::arg("average") = true,
                     py::arg("scale") = 0.0, py::arg("max_blocks") = 64, py::arg("timeout_s") = 60.0,
-                    py::arg("two_shot_min_bytes") = -1)
+                    py::arg("two_shot_min_bytes") = -1, py::arg("fused") = false)
                .def("ipc_handle", &XgmiP2PReducer::ipc_handle)
                .def("local_base", &XgmiP2PReducer::local_base)
                .def("region_bytes", &XgmiP2PReducer::region_bytes)
                .def("connect", &XgmiP2PReducer::connect)
                .def("connect_local", &XgmiP2PReducer::connect_local)
                .def("status", &XgmiP2PReducer::status)
+               .def("fused", &XgmiP2PReducer::fused)
+               .def("comm_ctx", &XgmiP2PReducer::comm_ctx)
                .def("scale", &XgmiP2PReducer::scale)
                .def("grids", &XgmiP2PReducer::grids)
                .def("two_shot", &XgmiP2PReducer::two_shot);

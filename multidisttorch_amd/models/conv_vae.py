@@ -267,6 +267,7 @@ class ConvVaeTrainer:
         # phase-end s_memrealtime stamps (obs/f28_phases.py); None = off
         self.f28_stamps = (None, None)
         self._fused_launches = 0
+        self._comm_packs = {}
         self._data = None
         torch.manual_seed(self.seed if init_seed is None else init_seed)
         ref = TorchConvVAE(self.spec, image, channels, z)
@@ -383,9 +384,31 @@ class ConvVaeTrainer:
 
     def attach_reducer(self, reducer):
         """Reducer over ``self.grads`` whose bucket bounds fall on layer starts
-        (see ``bucket_bounds``); buckets launch as their layers' backward ends."""
+        (see ``bucket_bounds``); buckets launch as their layers' backward ends.
+        A fused xGMI reducer (``XgmiP2PReducer(fused=True)``, kind "xgmi")
+        instead contributes all-reduce JOBS to the step's own launches
+        (csrc/kernels/comm_jobs.h): no second stream, no events."""
         self.reducer = reducer
         self._graphs.clear()
+        self._plans28.clear()
+        self._comm_packs = {}
+
+    def _comm_ctx(self):
+        """Device address of the fused reducer's CommCtx, or 0 (no reducer, or
+        one that runs its collectives on its own stream)."""
+        red = self.reducer
+        if red is None or not hasattr(red, "comm_ctx") or not red.fused():
+            return 0
+        return int(red.comm_ctx())
+
+    def _comm_job(self, segs, units, u0, u1, mode, adam):
+        """A recorded all-reduce job over finalize units [u0, u1) of a plan."""
+        st = self.state
+        j = self.C.Job()
+        self.C.comm_job(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, segs,
+                        units.narrow(0, u0 * 12, (u1 - u0) * 12), u1 - u0, st.train_state, st.hparams, adam,
+                        self._comm_ctx(), mode, j)
+        return j
 
     def layer_ranges(self):
         """[(layer, begin, end)] arena range of each layer's (weight, bias)."""
@@ -1046,6 +1069,15 @@ class ConvVaeTrainer:
             C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
                             p["nunits"], st.train_state, st.hparams, not self.f28_skip_adam)
             return
+        if self._comm_ctx():
+            # fused xGMI all-reduce (comm_jobs.h), one stream: decoder weight
+            # gradients | encoder weight gradients || decoder push (its bytes
+            # cross the links while the encoder's are computed) | encoder
+            # push+reduce || decoder reduce, both with Adam + bf16 cast.
+            # MDT_DDP_OVERLAP=0: all weight gradients | push+reduce+Adam.
+            for pack, grid in self._comm_packs28(M, p):
+                C.launch_jobs_multi(pack, grid)
+            return
         # DDP (reference: the Reducer's bucket all-reduces launched from the
         # autograd hooks while backward continues, /root/reference/vae-hpo.py:72,
         # :130): decoder weight gradients -> their finalize -> every bucket
@@ -1071,6 +1103,35 @@ class ConvVaeTrainer:
         if not self.f28_skip_adam:
             C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
                         st.train_state, st.hparams, True)
+
+    def _comm_packs28(self, M, p):
+        """Job tables of the fused-reducer 28x28 step after the f28_step_k
+        launch: [(device pack, grid)], built once per (M, Adam, overlap)."""
+        adam = not self.f28_skip_adam
+        key = (M, adam, self.ddp_overlap)
+        packs = self._comm_packs.get(key)
+        if packs is not None:
+            return packs
+        C, dev = self.C, self.device
+        lu, fd, L = p["layer_units"], p["first_dec"], len(self.spec)
+        segs, units = p["segs"], p["units"]
+        jobs = p["jobs"]  # six weight-gradient jobs (enc1, enc2, enc_head, dec_fc, dec1, dec2) + loss/step
+        names = ["enc1", "enc2", "enc_head", "dec_fc", "dec1", "dec2"]
+        enc = [jobs[i] for i, n in enumerate(names) if not n.startswith("dec")]
+        dec = [jobs[i] for i, n in enumerate(names) if n.startswith("dec")] + [jobs[len(names)]]
+        if self.ddp_overlap:
+            tables = [dec,
+                      enc + [self._comm_job(segs, units, lu[fd], lu[L], 1, adam)],
+                      [self._comm_job(segs, units, lu[0], lu[fd], 3, adam),
+                       self._comm_job(segs, units, lu[fd], lu[L], 2, adam)]]
+        else:
+            tables = [jobs, [self._comm_job(segs, units, lu[0], lu[L], 3, adam)]]
+        packs = []
+        for t in tables:
+            pack, grid = C.pack_jobs_multi(t)
+            packs.append((pack.to(dev), grid))
+        self._comm_packs[key] = packs
+        return packs
 
     def _finalize_unit_range(self, p, u0, u1):
         """Slab reduction into the gradient arena (no Adam) of finalize units [u0, u1)."""

@@ -216,6 +216,8 @@ def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: b
     if kind == "rccl":
         size = dist.get_world_size(pg)
         return native.require().RcclBucketReducer(rccl_comm_ptr(pg, flat.device), size, flat, b, average, scale)
+    if kind == "xgmi":
+        return make_p2p_reducer(pg, flat, b, average, two_shot="never", fused=True, scale=scale)
     if kind in P2P_KINDS:
         return make_p2p_reducer(pg, flat, b, average, two_shot=P2P_KINDS[kind])
     if kind == "c10d" and native.available():
@@ -243,7 +245,8 @@ def two_shot_min_bytes(rule: str, group_size: int) -> int:
 
 
 def make_p2p_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: bool = True,
-                     max_blocks: Optional[int] = None, timeout_s: Optional[float] = None, two_shot: str = "auto"):
+                     max_blocks: Optional[int] = None, timeout_s: Optional[float] = None, two_shot: str = "auto",
+                     fused: bool = False, scale: float = 0.0):
     """Peer-to-peer bucket all-reduce over xGMI (csrc/runtime/p2p_comm.cpp).
 
     Every group member allocates an uncached receive region, exports it with
@@ -255,7 +258,11 @@ def make_p2p_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: boo
     (reduce-scatter to chunk owners + all-gather, 2/s of the bucket per link;
     ``two_shot``: "auto" | "never" | "always", see ``two_shot_min_bytes``).
     All ranks of the group must share one node. Selected with
-    ``MDT_REDUCER=p2p`` (or ``kind="p2p"/"p2p1"/"p2p2"``); RCCL stays the default.
+    ``MDT_REDUCER=p2p`` (or ``kind="p2p"/"p2p1"/"p2p2"``).
+    ``fused`` (kind "xgmi") also allocates the receive slots of the all-reduce
+    JOBS (csrc/kernels/comm_jobs.h) that models with their own backward
+    launches (ConvVaeTrainer) put into those launches: one stream, no events;
+    ``scale`` replaces the 1/s pre-multiplier (tests).
     """
     if not flat.is_cuda:
         raise RuntimeError("the p2p reducer needs a GPU gradient arena")
@@ -263,8 +270,8 @@ def make_p2p_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: boo
     s, r = dist.get_world_size(pg), dist.get_rank(pg)
     max_blocks = max_blocks or int(os.getenv("MDT_P2P_BLOCKS", "64"))
     timeout_s = timeout_s or float(os.getenv("MDT_P2P_TIMEOUT_S", "60"))
-    red = C.XgmiP2PReducer(r, s, flat, [int(x) for x in bounds], average, 0.0, max_blocks, timeout_s,
-                           two_shot_min_bytes(two_shot, s))
+    red = C.XgmiP2PReducer(r, s, flat, [int(x) for x in bounds], average, float(scale), max_blocks, timeout_s,
+                           two_shot_min_bytes(two_shot, s), fused)
     if s > 1:
         h = red.ipc_handle()
         if dist.get_backend(pg) == "nccl":

@@ -18,6 +18,7 @@ that step only (A/B switches such as MDT_CONV_F28=0, MDT_CONV_DIRECT=0):
   prof[:MODEL[:B]]                        rocprofv3 --kernel-trace --stats of a short bench run
   pmc:MODEL:B:CTR+CTR...                  one rocprofv3 --pmc pass (keep within the per-block limits)
   smoke                                   __graft_entry__.smoke()
+  py:SCRIPT[:ARG...]                      python SCRIPT ARG... (diagnostics under bench/)
 
 Every step runs under its own ``timeout -k 10``; the first failing step ends
 the run with its exit status, so nothing else touches the GPU after a fault,
@@ -39,7 +40,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PY = sys.executable
 
 LIMITS = {"test": 900, "bench": 240, "ddp": 240, "driver": 180, "launches": 240, "f28phases": 120, "f28parts": 120,
-          "dconv": 120, "prof": 300, "pmc": 90, "smoke": 300}
+          "dconv": 120, "prof": 300, "pmc": 90, "smoke": 300, "py": 300}
 
 
 def parse(step):
@@ -108,6 +109,8 @@ def command(kind, args, out, i):
         d = os.path.join(out, f"{i:02d}_pmc")
         return ["rocprofv3", "--pmc"] + ctrs + ["--kernel-trace", "--output-format", "csv", "-d", d, "-o", "pmc",
                                                "--", PY] + bench_args(model, b, "6", "2") + ["--no-graphs"], "/tmp", log
+    if kind == "py":
+        return [PY, os.path.join(ROOT, args[0])] + args[1:], ROOT, log
     if kind == "smoke":
         return [PY, "-c", "import __graft_entry__ as g; g.smoke(); print('smoke ok')"], ROOT, log
     raise SystemExit(f"unknown step kind {kind!r}")
