@@ -89,6 +89,9 @@ def main(argv=None):
                          "the headline config is T=1 (K = N trials)")
     a = ap.parse_args(argv)
 
+    from multidisttorch_amd.runtime.env import apply_cu_split
+
+    apply_cu_split()  # one-GPU multi-rank rehearsals only (MDT_CU_SPLIT=1), before HIP initialises
     from multidisttorch_amd.runtime import setup_ddp, global_barrier, control_group
     from multidisttorch_amd.parallel.groups import setup_ddp_groups
     from multidisttorch_amd.hpo.trial import default_sweep
@@ -207,11 +210,18 @@ def main(argv=None):
     value = samples / dt
     # sanity: training actually progressed and the loss is finite
     ok = True
+    health = []
     for tr in trainers:
         st = tr.read_state()
         hist = tr.loss_history()
         last = float(hist[(st["step"] - 1) % len(hist)])
         ok = ok and st["step"] == a.warmup + a.steps and last == last and last < 1e9
+        # in-kernel failures that do not show up in the loss: a paired-workgroup
+        # exchange or an xGMI all-reduce wait that timed out (health_error)
+        msg = tr.health_error() if hasattr(tr, "health_error") else None
+        if msg:
+            health.append(msg)
+            ok = False
     # intra-group data parallelism: every replica of a trial must hold bitwise the
     # same parameters after the timed steps (the averaged gradient is identical on
     # every member; tests/gpu/conv_ddp_worker.py asserts the same)
@@ -258,6 +268,7 @@ def main(argv=None):
                 "graphs": (not a.no_graphs),
                 "timing_barrier": tbar_kind,
                 "valid": bool(flag.item() > 0),
+                "health": health or None,
                 "replicas_bitwise_equal": replicas_equal,
                 "reducer": (type(trainer.reducer).__name__ if trainer is not None
                             and getattr(trainer, "reducer", None) is not None else None),

@@ -36,7 +36,7 @@ __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, P
   const int n = (int)blockIdx.x % pc.M;
   g32i* word = (g32i*)(pc.pairw + n);
   int ticket = 0, seen = 1;
-  if (pc.delay_us && (int)blockIdx.x >= pc.M && threadIdx.x == 0) {  // tests: a partner that comes late
+  if (pc.delay_us > 0 && (int)blockIdx.x >= pc.M && threadIdx.x == 0) {  // tests: a partner that comes late
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * (unsigned)pc.delay_us) __builtin_amdgcn_s_sleep(8);
   }
@@ -70,6 +70,13 @@ __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, P
     lds_barrier();
     bwd_body<StepLayout, true>(ba, lds, n);
     return;
+  }
+  if (pc.delay_us < 0 && mode == kModeRole1 && n == 0) {  // tests: a paired half that stalls (sweep timeout)
+    if (threadIdx.x == 0) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * (unsigned)(-pc.delay_us)) __builtin_amdgcn_s_sleep(64);
+    }
+    lds_barrier();
   }
   pair_rest<StepLayout>(lds, n, mode == kModeRole1 ? 1 : 0);
 }

@@ -50,7 +50,9 @@ struct PairCtl {
   unsigned* err;           // [1] bit 0: an exchange sweep timed out
   int M;
   int pair;                // 1: grid = 2M (pairs), 0: grid = M (solo)
-  int delay_us;            // tests: workgroups >= M wait this long before their ticket (forces solo)
+  int delay_us;            // tests: > 0 workgroups >= M wait this long before their ticket (forces solo);
+                           //        < 0 sample 0's role-1 half stalls -delay_us after pairing (forces a
+                           //        sweep timeout of its partner: `err` bit 0)
 };
 
 // granule offsets inside one (sample, role) slab
@@ -81,9 +83,12 @@ using g32i = __attribute__((address_space(1))) int;
 // and the partner's sc1 (L1-bypassing) polls hit it there. Read from the
 // hardware at run time, not assumed from dispatch order: with different XCDs
 // every store stays agent scope.
+#ifndef MDT_F28_NEAR_WG  // A/B build flag only (round-4 measurement, profiles/r4_near_scope)
+#define MDT_F28_NEAR_WG 0
+#endif
 __device__ __forceinline__ void xput(unsigned long long* g, uint32_t tag, uint32_t v, bool near) {
   const unsigned long long x = ((unsigned long long)tag << 32) | v;
-  if (near)
+  if (near && MDT_F28_NEAR_WG)
     __hip_atomic_store((g64*)g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   else
     __hip_atomic_store((g64*)g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -122,7 +127,7 @@ __device__ __forceinline__ void xget(unsigned long long* base, const int (&gi)[N
 #pragma unroll
   for (int k = 0; k < N; ++k)
     if (gi[k] >= 0) {
-      if (near)
+      if (near && MDT_F28_NEAR_WG)
         __hip_atomic_store((g64*)(base + gi[k]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       else
         __hip_atomic_store((g64*)(base + gi[k]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

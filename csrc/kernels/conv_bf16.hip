@@ -115,26 +115,39 @@ __global__ void step_begin_k(TrainState* st, const HParams* hp) {
 }
 
 // ------------------------------------------------ optimizer tail ----
-// Adam (optional) + bf16 cast over every segment; used for the initial cast,
-// after checkpoint loads and after a DDP all-reduce.
+// Adam (optional) + bf16 cast over the whole flat arena; used for the initial
+// cast, after checkpoint loads and after a stream-side DDP all-reduce. One
+// 16-B stream over [0, total): the 64-element padding between segments is
+// zero in P, G, m and v and stays zero under Adam (m = v = 0, p = 0 - 0), so
+// no per-segment loop is needed (the per-segment form was 15 us for the 28x28
+// model's 0.37 M parameters: one dependent pass per segment).
 __global__ void __launch_bounds__(256) adam_cast_k(float* P, const float* G, float* Mo, float* Vo, __bf16* w16,
-                                                   const GradSeg* segs, int nseg, const TrainState* st,
-                                                   const HParams* hp, int do_adam) {
+                                                   long long total, const TrainState* st, const HParams* hp,
+                                                   int do_adam) {
   __shared__ AdamC cs;
-  const AdamC c = adam_consts_block(st, hp, &cs);
-  for (int s = 0; s < nseg; ++s) {
-    const GradSeg sg = segs[s];
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < sg.numel;
-         i += (long long)gridDim.x * blockDim.x) {
-      const long long o = sg.off + i;
-      float p = P[o];
-      if (do_adam) {
-        float m = Mo[o], v = Vo[o];
-        adam_update(p, m, v, G[o], c);
-        P[o] = p; Mo[o] = m; Vo[o] = v;
+  AdamC c{};
+  if (do_adam) c = adam_consts_block(st, hp, &cs);
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  const long long n4 = total >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 p = reinterpret_cast<const f32x4*>(P)[i];
+    if (do_adam) {
+      const f32x4 g = reinterpret_cast<const f32x4*>(G)[i];
+      f32x4 m = reinterpret_cast<const f32x4*>(Mo)[i], v = reinterpret_cast<const f32x4*>(Vo)[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float pj = p[j], mj = m[j], vj = v[j];
+        adam_update(pj, mj, vj, g[j], c);
+        p[j] = pj; m[j] = mj; v[j] = vj;
       }
-      w16[o] = (__bf16)p;
+      reinterpret_cast<f32x4*>(P)[i] = p;
+      reinterpret_cast<f32x4*>(Mo)[i] = m;
+      reinterpret_cast<f32x4*>(Vo)[i] = v;
     }
+    bf16x4 h;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h[j] = (__bf16)p[j];
+    reinterpret_cast<bf16x4*>(w16)[i] = h;
   }
 }
 
@@ -217,12 +230,14 @@ int mdt_step_begin(void* st, const void* hp, hipStream_t s) {
 
 int mdt_adam_cast(float* P, const float* G, float* Mo, float* Vo, void* w16, const void* segs, int nseg,
                   long long total, const void* st, const void* hp, int do_adam, hipStream_t s) {
-  int blocks = cdivh(total, 256 * 4);
-  if (blocks > 2048) blocks = 2048;
+  (void)segs;
+  (void)nseg;
+  if (total % 4 || ((uintptr_t)P | (uintptr_t)G | (uintptr_t)Mo | (uintptr_t)Vo) % 16 || (uintptr_t)w16 % 8) return 1;
+  int blocks = cdivh(total / 4, 256);
+  if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(adam_cast_k, dim3(blocks), dim3(256), 0, s, P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16),
-                     reinterpret_cast<const GradSeg*>(segs), nseg, reinterpret_cast<const TrainState*>(st),
-                     reinterpret_cast<const HParams*>(hp), do_adam);
+  hipLaunchKernelGGL(adam_cast_k, dim3(blocks), dim3(256), 0, s, P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16), total,
+                     reinterpret_cast<const TrainState*>(st), reinterpret_cast<const HParams*>(hp), do_adam);
   return (int)hipGetLastError();
 }
 

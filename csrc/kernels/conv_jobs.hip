@@ -155,6 +155,7 @@ struct JobPackN {
   JobBlob j[kMaxMultiJobs];
   int start[kMaxMultiJobs + 1];
   int n;
+  unsigned long long* stamps;  // profiling (null = off): per workgroup {start, end} s_memrealtime
 };
 
 constexpr int kMultiLds = cmax(cmax(cmax(wgrad_lds_bytes<W0>(), wgrad_lds_bytes<W1>()),
@@ -215,7 +216,17 @@ __global__ void __launch_bounds__(256) jobs_multi_k(const JobPackN* __restrict__
       i = k;
       s0 = st[k];
     }
+  unsigned long long* stamps = p->stamps;
+  unsigned long long t0 = 0;
+  if (stamps) t0 = __builtin_amdgcn_s_memrealtime();
   run_multi_job(p->j[i], lds, b - s0);
+  if (stamps) {  // which job ran where and when: overlap of jobs inside one launch (bench/ddp_structure.py)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      stamps[2 * b] = t0;
+      stamps[2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 __host__ inline bool multi_kind_ok(int k) {
@@ -529,6 +540,11 @@ int mdt_launch_jobs(const JobBlob* jobs, int n, hipStream_t s) {
 // `dst` (host memory, mdt_jobs_multi_bytes() bytes; the caller uploads it once).
 // Returns the grid size, 0 for an unsupported kind, -1 for bad input.
 int mdt_jobs_multi_bytes() { return (int)sizeof(JobPackN); }
+
+int mdt_pack_jobs_multi_stamps(void* img, void* stamps) {
+  reinterpret_cast<JobPackN*>(img)->stamps = reinterpret_cast<unsigned long long*>(stamps);
+  return 0;
+}
 
 int mdt_pack_jobs_multi(const JobBlob* jobs, int n, void* dst) {
   if (n < 1 || n > kMaxMultiJobs) return -1;

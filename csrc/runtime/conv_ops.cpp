@@ -67,6 +67,7 @@ int mdt_job_loss(mdt::JobBlob* j, const float* bce_part, int nb, const float* kl
 int mdt_launch_jobs(const mdt::JobBlob* jobs, int n, hipStream_t s);
 int mdt_jobs_multi_bytes();
 int mdt_pack_jobs_multi(const mdt::JobBlob* jobs, int n, void* dst);
+int mdt_pack_jobs_multi_stamps(void* img, void* stamps);
 int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s);
 int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train, hipStream_t s);
 int mdt_f28_backward(const long long* p, int M, hipStream_t s);
@@ -344,7 +345,8 @@ bool launch_jobs(const std::vector<Job*>& jobs) {
 // Pack recorded jobs (any supported kinds, up to 8) into a job table for ONE
 // jobs_multi_k launch: returns (uint8 CPU tensor image, grid). The caller keeps
 // the table in device memory for the lifetime of the plan (graph replays).
-std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs) {
+std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs,
+                                                const c10::optional<at::Tensor>& stamps) {
   TORCH_CHECK(!jobs.empty() && jobs.size() <= 8, "pack_jobs_multi takes 1..8 jobs");
   std::vector<JobBlob> v;
   for (auto* j : jobs) {
@@ -355,6 +357,11 @@ std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs) {
   auto img = torch::zeros({(int64_t)mdt_jobs_multi_bytes()}, torch::kUInt8);
   const int grid = mdt_pack_jobs_multi(v.data(), (int)v.size(), img.data_ptr());
   TORCH_CHECK(grid > 0, "pack_jobs_multi: unsupported job kind or bad job (", grid, ")");
+  if (stamps.has_value() && stamps->defined()) {  // profiling: [grid][2] int64 per-workgroup start / end stamps
+    TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == torch::kInt64 && stamps->numel() >= 2 * grid,
+                "pack_jobs_multi: stamps must be an int64 CUDA tensor of >= 2 * grid elements");
+    mdt_pack_jobs_multi_stamps(img.data_ptr(), stamps->data_ptr());
+  }
   return {img, (int64_t)grid};
 }
 
@@ -539,6 +546,8 @@ at::Tensor make_tr_units(const std::vector<std::vector<int64_t>>& units, int64_t
 
 void adam_cast(at::Tensor P, const at::Tensor& G, at::Tensor M, at::Tensor V, at::Tensor w16, const at::Tensor& segs,
                int64_t nseg, const at::Tensor& state, const at::Tensor& hparams, bool do_adam) {
+  TORCH_CHECK(G.numel() == P.numel() && M.numel() == P.numel() && V.numel() == P.numel() && w16.numel() == P.numel(),
+              "adam_cast: P, G, m, v and w16 must be arenas of one size");
   rc(mdt_adam_cast(P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(),
                    w16.data_ptr(), segs.data_ptr(), (int)nseg, P.numel(), state.data_ptr(), hparams.data_ptr(),
                    do_adam ? 1 : 0, cur()),
@@ -701,9 +710,10 @@ void bind_conv(pybind11::module& m) {
   py::class_<Job>(m, "Job")
       .def(py::init<>())
       .def_property_readonly("kind", &Job::kind)
+      .def_property_readonly("nblk", [](const Job& j) { return j.main.nblk; })
       .def_property_readonly("has_post", &Job::has_post);
   m.def("launch_jobs", &launch_jobs);
-  m.def("pack_jobs_multi", &pack_jobs_multi, py::arg("jobs"));
+  m.def("pack_jobs_multi", &pack_jobs_multi, py::arg("jobs"), py::arg("stamps") = py::none());
   m.def("launch_jobs_multi", &launch_jobs_multi);
   m.def("f28_forward", &f28_forward, py::arg("tensors"), py::arg("B"), py::arg("M"), py::arg("stream"),
         py::arg("train"));

@@ -66,11 +66,22 @@ class StreamBuckets {
   int64_t num_buckets() const { return (int64_t)bounds_.size() - 1; }
   std::vector<int64_t> bounds() const { return bounds_; }
 
+  // inline mode: collectives go on the CALLER's stream, in issue order, with
+  // no events -- no cross-queue dependency inside a replayed graph (each costs
+  // 5-12 us on this stack, profiles/r3_rccl_graph); wait() is then a no-op.
+  void set_inline(bool v) { inline_ = v; }
+  bool is_inline() const { return inline_; }
+
   void launch(int64_t b) {
     TORCH_CHECK(b >= 0 && b < num_buckets(), "bucket index out of range");
     TORCH_CHECK(!inflight_[b], "bucket ", b, " launched twice in one iteration");
     DeviceGuard g(device_);
     hipStream_t cur = c10::hip::getCurrentHIPStream(device_).stream();
+    if (inline_) {
+      issue(b, cur);
+      ++launched_total_;
+      return;
+    }
     MDT_HIP_CHECK(hipEventRecord(ready_[b], cur));  // gradients of bucket b are final
     MDT_HIP_CHECK(hipStreamWaitEvent(stream_, ready_[b], 0));
     issue(b, stream_);
@@ -124,6 +135,7 @@ class StreamBuckets {
   std::vector<int64_t> bounds_;
   int device_ = 0;
   hipStream_t stream_ = nullptr;
+  bool inline_ = false;
 
  private:
   std::vector<hipEvent_t> ready_, done_;
@@ -147,7 +159,9 @@ void def_bucket_api(Cls& c) {
       .def("mark_ready", &T::mark_ready)
       .def("reset_iteration", &T::reset_iteration)
       .def("pending", &T::pending)
-      .def("launched_count", &T::launched_count);
+      .def("launched_count", &T::launched_count)
+      .def("set_inline", &T::set_inline)
+      .def("is_inline", &T::is_inline);
 }
 
 }  // namespace mdt

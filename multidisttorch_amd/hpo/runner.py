@@ -39,7 +39,7 @@ from ..parallel.autotune import autotune_comm
 from ..parallel.ddp import broadcast_params, make_arena_reducer
 from ..parallel.groups import print0
 from ..runtime.bootstrap import bound_device, global_barrier
-from ..runtime.faults import (InjectedFault, TrialTimeout, agree_healthy, fault_step, group_timeout_s, guarded,
+from ..runtime.faults import (InjectedFault, TrialCorrupted, TrialTimeout, agree_healthy, fault_step, group_timeout_s, guarded,
                               heartbeat_s, maybe_inject, trial_watch)
 from ..utils.images import flush_images, save_image_async
 from .trial import TrialSpec
@@ -236,6 +236,14 @@ def _wait_epoch(trainer, group, device, events, watch=None):
         raise TrialTimeout(f"p2p all-reduce gave up waiting for a peer (status {int(red.status())})")
 
 
+def _check_health(trainer):
+    """Fail the trial on a kernel-reported corruption (ConvVaeTrainer.health_error)."""
+    fn = getattr(trainer, "health_error", None)
+    msg = fn() if fn is not None else None
+    if msg:
+        raise TrialCorrupted(msg)
+
+
 def _train_epoch(trainer, epoch: int, n_shard: int, n_dataset: int, opts: RunOptions, group,
                  step0: Optional[int] = None, tag: str = "", fault_at: Optional[int] = None, watch=None) -> float:
     B = opts.batch_size
@@ -252,6 +260,7 @@ def _train_epoch(trainer, epoch: int, n_shard: int, n_dataset: int, opts: RunOpt
     elif nb > LOSS_RING:
         raise ValueError(f"{nb} batches per epoch exceed the {LOSS_RING}-entry loss ring of a packed trial; "
                          f"use a larger --batch-size or --trials-per-group 1")
+    _check_health(trainer)
     hist = trainer.loss_history()
     st = trainer.read_state()
     if not opts.quiet_train_log:

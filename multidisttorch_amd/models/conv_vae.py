@@ -262,12 +262,19 @@ class ConvVaeTrainer:
         # DDP: decoder buckets go out before the encoder weight gradients
         # (MDT_DDP_OVERLAP=0, A/B only: every bucket after the whole backward)
         self.ddp_overlap = os.getenv("MDT_DDP_OVERLAP", "1") != "0"
-        self.f28_pair_delay_us = 0  # tests: delay every partner workgroup (forces the solo fallback)
+        # tests: > 0 delays every partner workgroup (forces the solo fallback); < 0 stalls sample 0's
+        # role-1 half after pairing (forces an exchange timeout: f28_err, health_error());
+        # MDT_F28_TEST_STALL_US=N sets -N (fault drills through the HPO runner / bench)
+        self.f28_pair_delay_us = -int(os.getenv("MDT_F28_TEST_STALL_US", "0"))
         # profiling: int64 [B*16] tensors (fwd, bwd) receiving per-workgroup
         # phase-end s_memrealtime stamps (obs/f28_phases.py); None = off
         self.f28_stamps = (None, None)
         self._fused_launches = 0
         self._comm_packs = {}
+        self._comm_tables = {}
+        # profiling: int64 tensors ([grid][2] each) receiving per-workgroup start/end
+        # stamps of the fused-reducer step's job launches (bench/ddp_structure.py); None = off
+        self.comm_stamps = None
         self._data = None
         torch.manual_seed(self.seed if init_seed is None else init_seed)
         ref = TorchConvVAE(self.spec, image, channels, z)
@@ -392,6 +399,28 @@ class ConvVaeTrainer:
         self._graphs.clear()
         self._plans28.clear()
         self._comm_packs = {}
+        self._comm_tables = {}
+
+    def health_error(self) -> Optional[str]:
+        """Silent-corruption check after an epoch (host sync): a paired-workgroup
+        exchange of the fused 28x28 step that timed out (the step then trained on
+        zero-filled partial sums, and an all-reduce would make the replicas agree
+        on the corrupted gradient) or a reducer wait that gave up on a peer.
+        None when healthy."""
+        if self.backend != "hip":
+            return None
+        msgs = []
+        if self.f28:
+            err = int(self.f28_err.item())
+            if err:
+                msgs.append(f"fused 28x28 step: a paired-workgroup exchange timed out (f28_err={err}); "
+                            f"the trial trained on incomplete partial sums")
+        red = self.reducer
+        if red is not None and hasattr(red, "status"):
+            st = int(red.status())
+            if st:
+                msgs.append(f"xGMI all-reduce gave up waiting for a peer (status {st})")
+        return "; ".join(msgs) or None
 
     def _comm_ctx(self):
         """Device address of the fused reducer's CommCtx, or 0 (no reducer, or
@@ -1089,15 +1118,29 @@ class ConvVaeTrainer:
         bounds = list(red.bounds())
         nbk = len(bounds) - 1
         early = self.ddp_overlap
+        if hasattr(red, "set_inline"):
+            red.set_inline(not early)
+        if not early:
+            # one stream: all weight gradients | finalize | the bucket
+            # collectives in issue order on the compute stream (no events) | Adam
+            C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
+            self._finalize_unit_range(p, lu[0], lu[L])
+            for k in reversed(range(nbk)):
+                red.launch(k)
+            red.wait_all()
+            if not self.f28_skip_adam:
+                C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
+                            st.train_state, st.hparams, True)
+            return
         C.launch_jobs_multi(p["dec_pack"], p["dec_grid"])
         self._finalize_unit_range(p, lu[fd], lu[L])
         for k in reversed(range(nbk)):
-            if early and bounds[k] >= dec0:
+            if bounds[k] >= dec0:
                 red.launch(k)
         C.launch_jobs_multi(p["enc_pack"], p["enc_grid"])
         self._finalize_unit_range(p, lu[0], lu[fd])
         for k in reversed(range(nbk)):
-            if not early or bounds[k] < dec0:
+            if bounds[k] < dec0:
                 red.launch(k)
         red.wait_all()
         if not self.f28_skip_adam:
@@ -1126,9 +1169,11 @@ class ConvVaeTrainer:
                        self._comm_job(segs, units, lu[fd], lu[L], 2, adam)]]
         else:
             tables = [jobs, [self._comm_job(segs, units, lu[0], lu[L], 3, adam)]]
+        self._comm_tables[key] = tables
         packs = []
-        for t in tables:
-            pack, grid = C.pack_jobs_multi(t)
+        for i, t in enumerate(tables):
+            st = self.comm_stamps[i] if self.comm_stamps is not None and i < len(self.comm_stamps) else None
+            pack, grid = C.pack_jobs_multi(t, stamps=st)
             packs.append((pack.to(dev), grid))
         self._comm_packs[key] = packs
         return packs

@@ -117,9 +117,12 @@ def local_size_from_env(env: Optional[Mapping[str, str]] = None) -> Optional[int
             counts = parse_slurm_tasks_per_node(v)
         except ValueError:
             continue
-        node = e.get("SLURM_NODEID")
-        if node not in (None, "") and 0 <= int(node) < len(counts):
-            return counts[int(node)]
+        try:
+            node = int(e.get("SLURM_NODEID", ""))
+        except ValueError:  # unset or malformed: fall through to the same-count rule
+            node = -1
+        if 0 <= node < len(counts):
+            return counts[node]
         if len(set(counts)) == 1:  # same count on every node: the node id does not matter
             return counts[0]
     return None
@@ -235,3 +238,31 @@ def discover(env: Optional[Mapping[str, str]] = None, ndev: Optional[int] = None
     addr, port = discover_master(e)
     lr = local_rank_from_env(e, wr, ndev)
     return LaunchInfo(ws, wr, lr, addr, port, _launcher_name(e), local_size_from_env(e))
+
+
+def cu_split_mask(local_rank: int, local_size: int, device: int = 0, ncu: int = 256) -> str:
+    """``HSA_CU_MASK`` value giving local rank r of s ranks that share ONE GPU
+    the disjoint CU range [r*ncu/s, (r+1)*ncu/s) of device ``device``."""
+    if local_size < 1 or not 0 <= local_rank < local_size:
+        raise ValueError(f"bad local rank {local_rank} of {local_size}")
+    per = ncu // local_size
+    lo = local_rank * per
+    return f"{device}:{lo}-{lo + per - 1}"
+
+
+def apply_cu_split(env: Optional[Mapping[str, str]] = None) -> Optional[str]:
+    """Rehearsal helper (``MDT_CU_SPLIT=1``): several ranks sharing one GPU each
+    get a disjoint share of its compute units through ``HSA_CU_MASK``, so one
+    rank's collective jobs spinning on a peer's flags can never occupy the CUs
+    that peer needs to produce them (on a real node every rank owns a GPU and
+    this is off). Must run before the process initialises HIP; returns the
+    mask set, or None."""
+    e = _env(env)
+    if e.get("MDT_CU_SPLIT", "0") != "1":
+        return None
+    size = local_size_from_env(e)
+    if not size or size <= 1:
+        return None
+    mask = cu_split_mask(local_rank_from_env(e, init_comm_size_and_rank(e)[1], None), size)
+    os.environ["HSA_CU_MASK"] = mask
+    return mask

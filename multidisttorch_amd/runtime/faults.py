@@ -42,7 +42,7 @@ import traceback
 from contextlib import contextmanager
 from typing import Dict, Optional
 
-__all__ = ["InjectedFault", "TrialTimeout", "maybe_inject", "fault_step", "guarded", "group_timeout_s",
+__all__ = ["InjectedFault", "TrialTimeout", "TrialCorrupted", "maybe_inject", "fault_step", "guarded", "group_timeout_s",
            "heartbeat_s", "parse_fault", "create_health_groups", "health_group", "trial_watch", "agree_healthy",
            "TrialWatch"]
 
@@ -53,6 +53,12 @@ class InjectedFault(RuntimeError):
 
 class TrialTimeout(RuntimeError):
     """A replica's epoch did not complete within the group timeout (a peer is gone)."""
+
+
+class TrialCorrupted(RuntimeError):
+    """A kernel reported that the epoch's results are not trustworthy (an
+    in-kernel exchange or all-reduce wait timed out); the trial fails instead
+    of reporting healthy numbers."""
 
 
 _HEALTH: Dict[int, object] = {}

@@ -27,6 +27,9 @@ def main():
     image, graphs = int(sys.argv[1]), sys.argv[2] == "1"
     bucket_mb = None if sys.argv[3] == "none" else float(sys.argv[3])
     kind = sys.argv[4] if len(sys.argv) > 4 else "p2p"
+    from multidisttorch_amd.runtime.env import apply_cu_split
+
+    apply_cu_split()  # MDT_CU_SPLIT=1: disjoint CU shares per rank (before HIP initialises)
     dist.init_process_group("gloo")
     r, s = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)

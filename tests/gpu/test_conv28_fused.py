@@ -326,3 +326,79 @@ def test_f28_pair_two_trials_packed(native_ext):
         assert np.all(np.isfinite(h)) and h[-5:].mean() < 0.8 * h[:5].mean(), h
         assert int(tr.f28_err.item()) == 0
         assert int(tr.f28_pairw.abs().sum()) == 0 and int(tr.f28_xg.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("pair", [False, True])
+def test_f28_run_to_run_bitwise(pair, native_ext):
+    """The same trial trained twice (fresh trainers, eager, 8 steps, with an
+    unrelated stream of kernels running beside the second one to perturb
+    dispatch timing) must give bitwise the same losses and parameters."""
+    dev = torch.device("cuda")
+    X = torch.rand(4 * 128, 784, generator=torch.Generator().manual_seed(3)).to(dev)
+    idx = torch.arange(4 * 128, device=dev, dtype=torch.int32)
+    res = []
+    for noisy in (False, True, False):
+        tr = _trainer(seed=4, use_graphs=False, lr=2e-3)
+        tr.f28_pair = pair
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 4)
+        side = torch.cuda.Stream()
+        junk = torch.rand(4096, 4096, device=dev)
+        for _ in range(8):
+            if noisy:
+                with torch.cuda.stream(side):
+                    junk = junk @ junk
+                    junk = junk / junk.norm()
+            tr.train_steps(1)
+        torch.cuda.synchronize()
+        res.append((tr.loss_history()[:8].copy(), tr.params.clone()))
+    for h, p in res[1:]:
+        np.testing.assert_array_equal(h, res[0][0])
+        assert torch.equal(p, res[0][1])
+
+
+def test_f28_exchange_timeout_is_reported(native_ext):
+    """A paired half that stalls past the exchange bound (test-only stall of
+    sample 0's role-1 workgroup): its partner's sweep times out, sets f28_err,
+    and the trainer's health check reports the corruption instead of staying
+    silent (the step trained on zero-filled partial sums)."""
+    dev = torch.device("cuda")
+    X = torch.rand(2 * 128, 784, generator=torch.Generator().manual_seed(5)).to(dev)
+    idx = torch.arange(2 * 128, device=dev, dtype=torch.int32)
+    tr = _trainer(seed=2, use_graphs=False)
+    assert tr.health_error() is None
+    tr.f28_pair_delay_us = -400000  # 0.4 s > the 0.25 s sweep bound
+    tr.bind_train_data(X, idx)
+    tr.set_cursor(0, 2)
+    tr.train_steps(1)
+    torch.cuda.synchronize()
+    assert int(tr.f28_err.item()) & 1
+    msg = tr.health_error()
+    assert msg and "exchange timed out" in msg, msg
+
+
+def test_f28_exchange_timeout_fails_bench_and_trial(tmp_path):
+    """The same fault through the two production entry points: bench.py's
+    record is marked invalid and vae-hpo.py reports the trial as failed."""
+    import json
+    import os
+    import re
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29631", MDT_F28_TEST_STALL_US="400000")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--graph-steps", "2"], capture_output=True, text=True, timeout=300, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["config"]["valid"] is False and out["config"]["health"], out["config"]
+    env["MASTER_PORT"] = "29632"
+    r = subprocess.run([sys.executable, os.path.join(root, "vae-hpo.py"), "--ngroups", "1", "--epochs", "1",
+                        "--model", "conv", "--train-samples", "512", "--test-samples", "256", "--no-results"],
+                       capture_output=True, text=True, timeout=300, cwd=str(tmp_path), env=env)
+    text = r.stdout + r.stderr
+    assert r.returncode == 0, text[-4000:]
+    assert "FAILED: TrialCorrupted" in text, text[-4000:]
+    agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
+    assert agg["failed_trials"] == [0], agg

@@ -138,3 +138,19 @@ def test_bind_refuses_more_rccl_ranks_than_gpus(monkeypatch):
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
     iso = E.discover({"WORLD_SIZE": "8", "RANK": "5", "LOCAL_RANK": "5", "LOCAL_WORLD_SIZE": "8"}, ndev=1)
     assert B._bind_local_device(iso, "nccl") == torch.device("cuda", 0)
+
+
+def test_cu_split_mask_and_slurm_nodeid_guard(monkeypatch):
+    from multidisttorch_amd.runtime.env import apply_cu_split, cu_split_mask, local_size_from_env
+
+    assert cu_split_mask(0, 2) == "0:0-127" and cu_split_mask(1, 2) == "0:128-255"
+    assert cu_split_mask(3, 4) == "0:192-255"
+    with pytest.raises(ValueError):
+        cu_split_mask(2, 2)
+    env = {"MDT_CU_SPLIT": "1", "LOCAL_RANK": "1", "LOCAL_WORLD_SIZE": "4", "RANK": "1", "WORLD_SIZE": "4"}
+    monkeypatch.setenv("HSA_CU_MASK", "unset")  # recorded, so the undo removes what apply_cu_split writes
+    assert apply_cu_split(env) == "0:64-127"
+    assert apply_cu_split({"LOCAL_RANK": "1", "LOCAL_WORLD_SIZE": "4"}) is None  # off by default
+    # a malformed SLURM_NODEID no longer raises: the same-count rule applies
+    assert local_size_from_env({"SLURM_TASKS_PER_NODE": "4(x2)", "SLURM_NODEID": "x"}) == 4
+    assert local_size_from_env({"SLURM_TASKS_PER_NODE": "4,2", "SLURM_NODEID": "bad"}) is None
