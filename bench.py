@@ -117,6 +117,11 @@ def main(argv=None):
         handles = setup_ddp_groups(K, verbose=False)
         ctrl = control_group()
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cpu":
+        # CPU ranks (config #1): split the host's cores between the ranks of this
+        # node instead of every rank spinning up one thread per core
+        local_n = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(1, local_n)))
     n_per = world // K
     gid = rank // n_per if rank < K * n_per else None
 

@@ -13,6 +13,7 @@ void probe_empty(int64_t blocks, int64_t threads);
 void bind_conv(pybind11::module& m);
 void bind_rccl(pybind11::module& m);
 void bind_p2p(pybind11::module& m);
+void bind_cpu(pybind11::module& m);
 }  // namespace mdt
 
 PYBIND11_MODULE(_C, m) {
@@ -24,6 +25,7 @@ PYBIND11_MODULE(_C, m) {
   mdt::bind_conv(m);
   mdt::bind_rccl(m);
   mdt::bind_p2p(m);
+  mdt::bind_cpu(m);
 
   py::class_<mdt::MlpVaeEngine>(m, "MlpVaeEngine")
       .def(py::init<int64_t, int64_t, int64_t, int64_t, int64_t>(), py::arg("batch"),

@@ -108,6 +108,17 @@ FILE_FLAGS = {
 }
 
 
+# Host files with their own flags: the native CPU step (config #1) vectorises
+# its fused elementwise loops (sqrt/div for Adam under IEEE rules; exp/log via
+# glibc's libmvec in the fast-math loss file only: under -ffast-math GCC's
+# vectorised Adam produced NaN for zero gradients); AVX2 + FMA only, which
+# every x86-64 host of an MI355X node has.
+HOST_FILE_FLAGS = {
+    "cpu_mlp.cpp": ["-O3", "-mavx2", "-mfma", "-fno-math-errno"],
+    "cpu_mlp_bce.cpp": ["-O3", "-mavx2", "-mfma", "-ffast-math"],
+}
+
+
 def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     inc, tlib, abi = _torch_paths()
     os.makedirs(BUILD, exist_ok=True)
@@ -131,8 +142,9 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
         jobsl.append((cmd, s, obj, _stamp([s] + hdrs, flags + ["force" if force else ""])))
     for s in host:
         obj = os.path.join(BUILD, os.path.basename(s) + ".o")
-        cmd = ["g++"] + host_flags + ["-c", s, "-o", obj]
-        jobsl.append((cmd, s, obj, _stamp([s] + hdrs, host_flags + ["force" if force else ""])))
+        flags = host_flags + HOST_FILE_FLAGS.get(os.path.basename(s), [])
+        cmd = ["g++"] + flags + ["-c", s, "-o", obj]
+        jobsl.append((cmd, s, obj, _stamp([s] + hdrs, flags + ["force" if force else ""])))
     objs, changed = [], False
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         futs = [ex.submit(_compile, *j) for j in jobsl]

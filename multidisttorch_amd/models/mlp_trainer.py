@@ -216,23 +216,49 @@ class MlpVaeTrainer:
             # Adam fused into the weight-gradient epilogues of B3
             e.backward(X, idx, M, 0, True)
 
+    _CPU_ORDER = ("fc1.weight", "fc1.bias", "fc21.weight", "fc21.bias", "fc22.weight", "fc22.bias",
+                  "fc3.weight", "fc3.bias", "fc4.weight", "fc4.bias")
+
+    def _cpu_native(self):
+        """The fused native CPU step (csrc/runtime/cpu_mlp.cpp) when the torch
+        backend runs on the host and the extension is built; None otherwise
+        (stock torch ops, ``reference_step``)."""
+        if self.device.type != "cpu" or not native.available():
+            return None
+        if getattr(self, "_cpu", None) is None:
+            self._cpu = native.require().MlpCpuStep(self.B, self.D, self.H, self.Z)
+            v, g = self.named_parameters(), self.named_grads()
+            self._cpu_w = [v[n] for n in self._CPU_ORDER]
+            self._cpu_g = [g[n] for n in self._CPU_ORDER]
+        return self._cpu
+
     @torch.no_grad()
     def _step_torch(self, M: int):
         X, idx = self._data[0], self._data[1]
         st = self._st
-        rows = idx[st["cursor"] * self.B: st["cursor"] * self.B + M].long()
-        x = X[rows]
-        eps = torch.from_numpy(reparam_eps(M, self.Z, self.seed, self.rng_stream, st["step"])).to(self.device)
-        f = reference_step(self.named_parameters(), self.named_grads(), x, eps, self.hp["kl_beta"])
+        h = self.hp
+        cpu = self._cpu_native()
+        if cpu is not None:
+            loss = cpu.forward_backward(self._cpu_w, self._cpu_g, X, idx, st["cursor"] * self.B, M, self.seed,
+                                        self.rng_stream, st["step"], h["kl_beta"])
+        else:
+            rows = idx[st["cursor"] * self.B: st["cursor"] * self.B + M].long()
+            x = X[rows]
+            eps = torch.from_numpy(reparam_eps(M, self.Z, self.seed, self.rng_stream, st["step"])).to(self.device)
+            f = reference_step(self.named_parameters(), self.named_grads(), x, eps, h["kl_beta"])
+            loss = None
         if self.reducer is not None:
             self.reducer.launch(1)
             self.reducer.launch(0)
             self.reducer.wait_all()
-        h = self.hp
-        reference_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, st["step"] + 1,
-                        h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"], h["grad_scale"],
-                        self.decoupled_wd)
-        loss = float(f["loss"])
+        if cpu is not None:
+            cpu.adam(self.params, self.grads, self.exp_avg, self.exp_avg_sq, st["step"] + 1, h["lr"], h["beta1"],
+                     h["beta2"], h["eps"], h["weight_decay"], h["grad_scale"], self.decoupled_wd)
+        else:
+            reference_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, st["step"] + 1,
+                            h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"], h["grad_scale"],
+                            self.decoupled_wd)
+            loss = float(f["loss"])
         self._hist[st["step"] % LOSS_HIST] = loss
         st["epoch_loss"] += loss
         st["epoch_count"] += 1
@@ -341,14 +367,22 @@ class MlpVaeTrainer:
                     first = self.engine.act("recon", M).clone()
             else:
                 st = self._st_eval
-                rows = idx[b * self.B: b * self.B + M].long()
-                x = X[rows]
-                eps = torch.from_numpy(reparam_eps(M, self.Z, self.seed, EVAL_STREAM + self.rng_stream,
-                                                   st["step"])).to(self.device)
-                f = reference_forward(self.named_parameters(), x, eps, self.hp["kl_beta"])
-                if want_first_recon and b == 0:
-                    first = f["p"].clone()
-                loss = float(f["loss"])
+                cpu = self._cpu_native()
+                if cpu is not None:  # fused native forward + loss (csrc/runtime/cpu_mlp.cpp)
+                    loss = cpu.forward_backward(self._cpu_w, self._cpu_g, X, idx, b * self.B, M, self.seed,
+                                                EVAL_STREAM + self.rng_stream, st["step"], self.hp["kl_beta"],
+                                                backward=False)
+                    if want_first_recon and b == 0:
+                        first = cpu.recon()
+                else:
+                    rows = idx[b * self.B: b * self.B + M].long()
+                    x = X[rows]
+                    eps = torch.from_numpy(reparam_eps(M, self.Z, self.seed, EVAL_STREAM + self.rng_stream,
+                                                       st["step"])).to(self.device)
+                    f = reference_forward(self.named_parameters(), x, eps, self.hp["kl_beta"])
+                    if want_first_recon and b == 0:
+                        first = f["p"].clone()
+                    loss = float(f["loss"])
                 self._hist_eval[st["step"] % LOSS_HIST] = loss
                 st["epoch_loss"] += loss
                 st["epoch_count"] += 1
