@@ -78,13 +78,25 @@ using g64 = __attribute__((address_space(1))) unsigned long long;
 using g32i = __attribute__((address_space(1))) int;
 
 // `near`: both workgroups of the pair run on ONE XCD (their HW_REG_XCC_ID
-// match, exchanged in X1), so they share one L2: the granule goes out as an
-// sc0 store that stays in that L2 instead of an sc1 write-through to memory,
-// and the partner's sc1 (L1-bypassing) polls hit it there. Read from the
-// hardware at run time, not assumed from dispatch order: with different XCDs
-// every store stays agent scope.
-#ifndef MDT_F28_NEAR_WG  // A/B build flag only (round-4 measurement, profiles/r4_near_scope)
-#define MDT_F28_NEAR_WG 0
+// match, exchanged in X1), so they share one L2: the granule goes out as a
+// plain (workgroup-scope) store that stays in that L2 instead of an sc1
+// write-through to memory, and the partner's sc1 (L1-bypassing, agent-scope)
+// polls hit it there. Read from the hardware at run time, not assumed from
+// dispatch order: with different XCDs every store stays agent scope.
+// Why this is sound on gfx950 although the HIP scoped model gives a
+// workgroup-scope store no visibility to another workgroup: the vector L1 is
+// write-through -- a plain store leaves the CU for the XCD's L2 and keeps the
+// line there (MI355X_MICROARCH.md, "stores of each flavour") -- the consumer
+// never reads its own L1 (sc1 loads), and {tag, payload} is ONE 8-byte store,
+// so there is no payload/flag ordering to lose. Measured (profiles/r4_near_scope):
+// agent scope on the near path costs +1.1-1.3 us per 64 us step (driver
+// command 0.0652-0.0653 vs 0.0640-0.0642 ms). Stress coverage: pairs run under
+// a concurrent GEMM stream and a packed second trial, near pairs counted from
+// the stamps, results bitwise run to run (tests/gpu/test_conv28_fused.py,
+// bench/diag_determinism.py). MDT_HIP_EXTRA_FLAGS=-DMDT_F28_NEAR_WG=0 builds
+// the agent-scope form.
+#ifndef MDT_F28_NEAR_WG  // 0: agent scope on the near path too (A/B build, profiles/r4_near_scope)
+#define MDT_F28_NEAR_WG 1
 #endif
 __device__ __forceinline__ void xput(unsigned long long* g, uint32_t tag, uint32_t v, bool near) {
   const unsigned long long x = ((unsigned long long)tag << 32) | v;

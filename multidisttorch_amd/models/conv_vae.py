@@ -259,9 +259,14 @@ class ConvVaeTrainer:
         # the merged step with two workgroups per sample (conv28_pair.h): a
         # B = 128 trial fills all 256 CUs instead of 128. MDT_F28_PAIR=0 (A/B): one per sample
         self.f28_pair = os.getenv("MDT_F28_PAIR", "1") != "0"
-        # DDP: decoder buckets go out before the encoder weight gradients
-        # (MDT_DDP_OVERLAP=0, A/B only: every bucket after the whole backward)
-        self.ddp_overlap = os.getenv("MDT_DDP_OVERLAP", "1") != "0"
+        # DDP on the fused 28x28 step: the decoder bucket goes out before the
+        # encoder weight gradients (True), or every bucket after the whole
+        # backward on one stream (False); "auto" (default): overlap only when
+        # the decoder bucket's transfer over one xGMI link outweighs the
+        # measured cost of splitting the weight-gradient launch
+        # (parallel/ddp.py::overlap_pays, profiles/r4_ddp_fused)
+        ov = os.getenv("MDT_DDP_OVERLAP", "auto")
+        self.ddp_overlap = None if ov == "auto" else ov != "0"
         # tests: > 0 delays every partner workgroup (forces the solo fallback); < 0 stalls sample 0's
         # role-1 half after pairing (forces an exchange timeout: f28_err, health_error());
         # MDT_F28_TEST_STALL_US=N sets -N (fault drills through the HPO runner / bench)
@@ -1117,7 +1122,7 @@ class ConvVaeTrainer:
         dec0 = self.layer_ranges()[fd][1]
         bounds = list(red.bounds())
         nbk = len(bounds) - 1
-        early = self.ddp_overlap
+        early = self._overlap28(fused=False)
         if hasattr(red, "set_inline"):
             red.set_inline(not early)
         if not early:
@@ -1151,7 +1156,8 @@ class ConvVaeTrainer:
         """Job tables of the fused-reducer 28x28 step after the f28_step_k
         launch: [(device pack, grid)], built once per (M, Adam, overlap)."""
         adam = not self.f28_skip_adam
-        key = (M, adam, self.ddp_overlap)
+        overlap = self._overlap28(fused=True)
+        key = (M, adam, overlap)
         packs = self._comm_packs.get(key)
         if packs is not None:
             return packs
@@ -1162,7 +1168,7 @@ class ConvVaeTrainer:
         names = ["enc1", "enc2", "enc_head", "dec_fc", "dec1", "dec2"]
         enc = [jobs[i] for i, n in enumerate(names) if not n.startswith("dec")]
         dec = [jobs[i] for i, n in enumerate(names) if n.startswith("dec")] + [jobs[len(names)]]
-        if self.ddp_overlap:
+        if overlap:
             tables = [dec,
                       enc + [self._comm_job(segs, units, lu[fd], lu[L], 1, adam)],
                       [self._comm_job(segs, units, lu[0], lu[fd], 3, adam),
@@ -1177,6 +1183,17 @@ class ConvVaeTrainer:
             packs.append((pack.to(dev), grid))
         self._comm_packs[key] = packs
         return packs
+
+    def _overlap28(self, fused: bool) -> bool:
+        """Resolve MDT_DDP_OVERLAP (``ddp_overlap``; None = auto) for the fused
+        28x28 DDP step: the split costs ~6 us with the fused xGMI jobs and
+        ~31 us with RCCL on its own stream (profiles/r4_ddp_fused)."""
+        if self.ddp_overlap is not None:
+            return bool(self.ddp_overlap)
+        from ..parallel.ddp import overlap_pays
+
+        dec0 = next(b for l, b, e in self.layer_ranges() if l.name.startswith("dec"))
+        return overlap_pays(4 * (self.numel - dec0), 6.0 if fused else 31.0)
 
     def _finalize_unit_range(self, p, u0, u1):
         """Slab reduction into the gradient arena (no Adam) of finalize units [u0, u1)."""

@@ -10,9 +10,11 @@ trainer of the same configuration (so the real trial's state is untouched),
 the per-rank times are max-reduced over the group so every member picks the
 same layout, and the winner is cached per (model, group size, batch, arena).
 ``autotune_comm`` searches the reducer too: RCCL's ring (``rccl``) against the
-one-shot hipIpc push over all s-1 xGMI links (``p2p1``) and, for groups of 3+,
-the two-shot reduce-scatter + all-gather form (``p2p2``, both in
-csrc/runtime/p2p_comm.cpp) for every layout, when the group is on GPUs of one node.
+one-shot hipIpc push over all s-1 xGMI links (``p2p1``), the same push fused
+into the step's own launches (``xgmi``, csrc/kernels/comm_jobs.h) and, for
+groups of 3+, the two-shot reduce-scatter + all-gather form (``p2p2``) and the
+mixed one (``p2p``: two-shot for big buckets only), for every layout, when the
+group is on GPUs of one node.
 """
 
 from __future__ import annotations
@@ -77,7 +79,9 @@ def comm_kinds(pg, device: torch.device) -> List[Optional[str]]:
     dist.all_gather_object(hosts, socket.gethostname(), group=pg)
     if len(set(hosts)) != 1:
         return ["rccl"]
-    return ["rccl", "p2p1"] + (["p2p2"] if len(hosts) >= 3 else [])
+    # groups of 3+: the mixed "p2p" kind (two-shot only for buckets >= MDT_P2P_TWO_SHOT_MB)
+    # as well as all-one-shot and all-two-shot
+    return ["rccl", "p2p1", "xgmi"] + (["p2p", "p2p2"] if len(hosts) >= 3 else [])
 
 
 def autotune_buckets(make_trainer: Callable[[], object], pg, X: torch.Tensor, idx: torch.Tensor,

@@ -149,6 +149,7 @@ def test_conv_bucket_launches_interleave_with_backward(nccl_world, native_ext, i
     B = 128 if image == 28 else 32
     X, idx = _data(image, 2, B, dev)
     tr = _trainer(image, B, dev, graphs=False)
+    tr.ddp_overlap = True  # the overlap schedule (the auto rule picks one stream for the 28x28 RCCL step)
     if image == 28:
         assert tr.f28
         tr.f28 = f28
@@ -188,8 +189,9 @@ def test_conv_step_graph_issues_real_collectives(nccl_world, native_ext, image, 
     nb, steps = 4, 8
     X, idx = _data(image, nb, B, dev)
     runs = {}
-    for mode in ("single", "scaled"):
+    for mode, overlap in (("single", None), ("scaled", True), ("scaled", False)):
         tr = _trainer(image, B, dev, True)
+        tr.ddp_overlap = overlap
         if image == 28:
             tr.f28 = f28
         if mode == "scaled":
@@ -200,11 +202,13 @@ def test_conv_step_graph_issues_real_collectives(nccl_world, native_ext, image, 
         tr.set_cursor(0, nb)
         tr.train_steps(steps)
         torch.cuda.synchronize()
-        runs[mode] = (tr.params.clone(), tr.loss_history()[:steps].copy())
+        runs[(mode, overlap)] = (tr.params.clone(), tr.loss_history()[:steps].copy())
         if mode == "scaled":
             assert red.launched_count() == 5 * red.num_buckets() and red.num_buckets() >= 2
-    np.testing.assert_allclose(runs["scaled"][1], runs["single"][1], rtol=1e-5)
-    torch.testing.assert_close(runs["scaled"][0], runs["single"][0], rtol=1e-5, atol=1e-6)
+            assert red.is_inline() == (image == 28 and f28 and not overlap)  # one-stream schedule: no events
+    for ov in (True, False):
+        np.testing.assert_allclose(runs[("scaled", ov)][1], runs[("single", None)][1], rtol=1e-5)
+        torch.testing.assert_close(runs[("scaled", ov)][0], runs[("single", None)][0], rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("model", ["conv28", "mlp"])
