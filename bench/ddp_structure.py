@@ -110,7 +110,7 @@ def main():
              ["enc1 wgrad", "enc2 wgrad", "enc_head wgrad", "decoder push (all-reduce)"],
              ["encoder push+reduce+Adam", "decoder reduce+Adam"]]
     packs = tr._comm_packs28(B, p)
-    tables = tr._comm_tables[(B, True, True)]  # (M, Adam, overlap)
+    tables = tr._comm_tables[(B, True, True, False)]  # (M, Adam, overlap, split tail)
     lines, t_base = [], None
     stamps = [st.view(-1, 2).cpu().tolist() for st in tr.comm_stamps]
     t_base = min(x[0] for s in stamps for x in s)

@@ -554,23 +554,30 @@ __device__ __forceinline__ void fwd_rest(const FwdArgs& a, uint8_t* lds, int n) 
       // independent accumulators: a single fmaf chain of 56 dependent steps
       // per row, plus two converts per product, bounded this phase (PMC:
       // ~7k VALU instructions per wave in the fused step)
-      float dq[4] = {0.f, 0.f, 0.f, 0.f};
+      // two K halves, [0, 1536) = loads i < 3 and [1536, 3136) = loads i >= 3,
+      // each summed exactly as one half of the paired step sums it (same lane
+      // chunks, same accumulator order, one wave_sum each), then (half 0 +
+      // half 1) + bias: the solo fallback is bitwise the paired form
+      float dq[4] = {0.f, 0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         if (512 * i + 8 * lane < kFlat) {
-          dq[0] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 0, 1),
-                                                  __builtin_shufflevector(vc[i], vc[i], 0, 1), dq[0], false);
-          dq[1] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 2, 3),
-                                                  __builtin_shufflevector(vc[i], vc[i], 2, 3), dq[1], false);
-          dq[2] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 4, 5),
-                                                  __builtin_shufflevector(vc[i], vc[i], 4, 5), dq[2], false);
-          dq[3] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 6, 7),
-                                                  __builtin_shufflevector(vc[i], vc[i], 6, 7), dq[3], false);
+          float(&q)[4] = i < 3 ? dq : dr;
+          q[0] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 0, 1),
+                                                 __builtin_shufflevector(vc[i], vc[i], 0, 1), q[0], false);
+          q[1] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 2, 3),
+                                                 __builtin_shufflevector(vc[i], vc[i], 2, 3), q[1], false);
+          q[2] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 4, 5),
+                                                 __builtin_shufflevector(vc[i], vc[i], 4, 5), q[2], false);
+          q[3] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av[i], av[i], 6, 7),
+                                                 __builtin_shufflevector(vc[i], vc[i], 6, 7), q[3], false);
         }
       }
-      float d = (dq[0] + dq[1]) + (dq[2] + dq[3]);
-      d = wave_sum(d);
-      if (lane == 0) Hs[w + 8 * c] = d + Bias[kBh + w + 8 * c];
+      float d0 = (dq[0] + dq[1]) + (dq[2] + dq[3]);
+      float d1 = (dr[0] + dr[1]) + (dr[2] + dr[3]);
+      d0 = wave_sum(d0);
+      d1 = wave_sum(d1);
+      if (lane == 0) Hs[w + 8 * c] = (d0 + d1) + Bias[kBh + w + 8 * c];
 #pragma unroll
       for (int i = 0; i < 7; ++i) vc[i] = vn[i];
     }
@@ -723,8 +730,8 @@ constexpr int kBW4 = kBG + 784 * 4;         // f32 [16][32] dec2 weights, tap-ma
 constexpr int kBGD1 = kBW4 + 512 * 4;       // bf16 img14 [196][32]
 constexpr int kBGD0 = kBGD1 + 196 * 64;     // bf16 [3136]
 constexpr int kBDM = kBGD0 + kFlat * 2;     // f32 [64] d[mu|lv]
-constexpr int kBDZR = kBDM + 64 * 4;        // f32 [8][32] dz wave partials
-constexpr int kBGA2 = kBDZR + 256 * 4;      // bf16 [3136]
+constexpr int kBDZR = kBDM + 64 * 4;        // f32 [2][8][32] dz wave partials (two K halves)
+constexpr int kBGA2 = kBDZR + 512 * 4;      // bf16 [3136]
 constexpr int kBGA2F = kBGA2 + kFlat * 2;   // f32 [3136] (colsum source)
 constexpr int kBCS = kBGA2F + kFlat * 4;    // f32 [8][64] colsum scratch
 constexpr int kBW2 = kBCS + 512 * 4;        // 16 x 4 KB enc2 tap images
@@ -870,10 +877,13 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds, int n) 
   stamp(a.stamps, 3);
   // ---- Q3: dec_fc backward-data dz = g . Wd (VALU over [3136][32] rows) ----
   {
-    const int c8 = lane & 3, jr = lane >> 2;
-    float acc[8];
+    const int jr = lane >> 2;
+    // two K halves (rows [0, 1536) = row groups it < 12, [1536, 3136) = it >= 12),
+    // each accumulated and reduced exactly as one half of the paired step
+    // (conv28_pair.h Q3); Q4 adds them in the paired order: bitwise the same dz
+    float acc[8], acc1[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int e = 0; e < 8; ++e) acc[e] = acc1[e] = 0.f;
     // 25 row groups of 128 (3136 rows): 2 chunks of 13 loads
     stream2_pre<13, 2>(
         wd0, wd_ld,
@@ -881,22 +891,35 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds, int n) 
           const int jj = it * 128 + w * 16 + jr;
           if (jj < kFlat) {
             const float g = (float)GD0s[jj];
+            if (it < 12) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] = fmaf(g, (float)wv[e], acc[e]);
+              for (int e = 0; e < 8; ++e) acc[e] = fmaf(g, (float)wv[e], acc[e]);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) acc1[e] = fmaf(g, (float)wv[e], acc1[e]);
+            }
           }
         });
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float v = acc[e];
+      float v = acc[e], u = acc1[e];
       v += __shfl_xor(v, 4, 64);
+      u += __shfl_xor(u, 4, 64);
       v += __shfl_xor(v, 8, 64);
+      u += __shfl_xor(u, 8, 64);
       v += __shfl_xor(v, 16, 64);
+      u += __shfl_xor(u, 16, 64);
       v += __shfl_xor(v, 32, 64);
+      u += __shfl_xor(u, 32, 64);
       acc[e] = v;
+      acc1[e] = u;
     }
     if (lane < 4) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) DZR[w * 32 + 8 * lane + e] = acc[e];
+      for (int e = 0; e < 8; ++e) {
+        DZR[w * 32 + 8 * lane + e] = acc[e];
+        DZR[256 + w * 32 + 8 * lane + e] = acc1[e];
+      }
     }
   }
   // Q5's first 16 head-weight loads, in flight across the barrier and Q4
@@ -910,9 +933,12 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds, int n) 
   // ---- Q4: reparameterisation backward -> d[mu | logvar]
   if (tid < 32) {
     const int c = tid;
-    float dz = 0.f;
+    float dz0 = 0.f, dz1 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) dz += DZR[i * 32 + c];
+    for (int i = 0; i < 8; ++i) dz0 += DZR[i * 32 + c];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dz1 += DZR[256 + i * 32 + c];
+    const float dz = dz0 + dz1;  // the paired step's (role-0 part + role-1 part)
     const float beta = a.hp->kl_beta;
     // merged step: mu | logvar and eps from the forward's LDS (H, Red); else from memory
     const float* Hm = reinterpret_cast<const float*>(lds + L::H);
@@ -935,16 +961,24 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds, int n) 
   // ---- Q5: head backward-data g = dmulv . Wh (VALU over 392 chunks of 8) x enc2 ReLU mask
   if (tid < kFlat / 8) {
     const int k0 = 8 * tid;
-    float acc[8];
+    float acc[8], acc1[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-    // 64 weight rows: 4 chunks of 16 loads
+    for (int e = 0; e < 8; ++e) acc[e] = acc1[e] = 0.f;
+    // 64 weight rows: 4 chunks of 16 loads; rows 0..31 and 32..63 in two
+    // accumulators added at the end, the paired step's two row groups
     stream2_pre<16, 4>(wh5, wh_ld,
                    [&](int o, const bf16x8& wv) {
                      const float dm = DMs[o];
+                     if (o < 32) {
 #pragma unroll
-                     for (int e = 0; e < 8; ++e) acc[e] = fmaf(dm, (float)wv[e], acc[e]);
+                       for (int e = 0; e < 8; ++e) acc[e] = fmaf(dm, (float)wv[e], acc[e]);
+                     } else {
+#pragma unroll
+                       for (int e = 0; e < 8; ++e) acc1[e] = fmaf(dm, (float)wv[e], acc1[e]);
+                     }
                    });
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = acc[e] + acc1[e];
     const bf16x8 mk = MERGED ? *reinterpret_cast<const bf16x8*>(lds + L::A2 + 2 * k0)
                              : *reinterpret_cast<const bf16x8*>(a.a2 + (size_t)n * kFlat + k0);
     bf16x8 o;
@@ -959,12 +993,16 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds, int n) 
   }
   w2r.store(W2s);
   lds_barrier();
-  if (tid < 64) {  // enc2 bias partials: sum over the 49 pixels in order
-    float s = 0.f;
-    for (int p = 0; p < 49; ++p) s += GA2F[p * 64 + tid];
-    a.db2_part[(size_t)n * 64 + tid] = s;
-    // the [2][M][64] layout of the paired step (a row per half): zero second row
-    if (a.db2_m2) a.db2_part[(size_t)(a.db2_m2 + n) * 64 + tid] = 0.f;
+  if (tid < 64) {  // enc2 bias partials: pixels 0..23 and 24..48 in order, a row per half as the paired step
+    float s0 = 0.f, s1 = 0.f;
+    for (int p = 0; p < 24; ++p) s0 += GA2F[p * 64 + tid];
+    for (int p = 24; p < 49; ++p) s1 += GA2F[p * 64 + tid];
+    if (a.db2_m2) {  // [2][M][64]
+      a.db2_part[(size_t)n * 64 + tid] = s0;
+      a.db2_part[(size_t)(a.db2_m2 + n) * 64 + tid] = s1;
+    } else {
+      a.db2_part[(size_t)n * 64 + tid] = s0 + s1;
+    }
   }
 
   stamp(a.stamps, 6);
@@ -1011,7 +1049,7 @@ struct StepLayout {
   static constexpr int W4 = W1 + 512 * 4;        // f32 [16][32], both halves
   static constexpr int X = W4 + 512 * 4;         // f32 [784]
   static constexpr int DM = X;                   //   bwd d[mu|lv] (X dead after P7)
-  static constexpr int DZR = X + 64 * 4;         //   bwd dz partials
+  static constexpr int DZR = X + 64 * 4;         //   bwd dz partials [2][8][32]
   static constexpr int G = X + 784 * 4;          // f32 [784] dlogits (P7 -> Q1)
   static constexpr int A1 = G + 784 * 4;         // bf16 img14: enc1 out (P2 input, Q6 mask)
   static constexpr int A2 = A1 + 196 * 64;       // bf16 [3136] enc2 out (P3 input, Q5 mask)
@@ -1034,7 +1072,7 @@ struct StepLayout {
   static_assert(W1 % 16 == 0 && X % 16 == 0 && G % 16 == 0 && A1 % 16 == 0 && A2 % 16 == 0 && D0 % 16 == 0 &&
                     Dummy % 16 == 0 && Bd % 16 == 0 && CSB % 16 == 0 && D1 % 16 == 0 && LDS <= 163840,
                 "step LDS map");
-  static_assert(196 * 64 <= kFlat * 4 && 64 * 4 + 256 * 4 <= 784 * 4 && kFlat * 2 <= 8192, "step LDS aliases");
+  static_assert(196 * 64 <= kFlat * 4 && 64 * 4 + 512 * 4 <= 784 * 4 && kFlat * 2 <= 8192, "step LDS aliases");
 };
 
 

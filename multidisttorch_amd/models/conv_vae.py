@@ -280,6 +280,12 @@ class ConvVaeTrainer:
         # profiling: int64 tensors ([grid][2] each) receiving per-workgroup start/end
         # stamps of the fused-reducer step's job launches (bench/ddp_structure.py); None = off
         self.comm_stamps = None
+        # one-GPU multi-process rehearsals (eager only): push and reduce in separate
+        # launches with ``comm_phase_hook()`` (e.g. device sync + host barrier)
+        # between them, so no rank's reduce ever spins on a peer that shares
+        # the GPU (tests/gpu/conv_ddp_worker.py)
+        self.comm_split_tail = False
+        self.comm_phase_hook = None
         self._data = None
         torch.manual_seed(self.seed if init_seed is None else init_seed)
         ref = TorchConvVAE(self.spec, image, channels, z)
@@ -1109,8 +1115,11 @@ class ConvVaeTrainer:
             # cross the links while the encoder's are computed) | encoder
             # push+reduce || decoder reduce, both with Adam + bf16 cast.
             # MDT_DDP_OVERLAP=0: all weight gradients | push+reduce+Adam.
-            for pack, grid in self._comm_packs28(M, p):
+            packs = self._comm_packs28(M, p)
+            for i, (pack, grid) in enumerate(packs):
                 C.launch_jobs_multi(pack, grid)
+                if self.comm_phase_hook is not None and i == len(packs) - 2:
+                    self.comm_phase_hook()
             return
         # DDP (reference: the Reducer's bucket all-reduces launched from the
         # autograd hooks while backward continues, /root/reference/vae-hpo.py:72,
@@ -1156,8 +1165,8 @@ class ConvVaeTrainer:
         """Job tables of the fused-reducer 28x28 step after the f28_step_k
         launch: [(device pack, grid)], built once per (M, Adam, overlap)."""
         adam = not self.f28_skip_adam
-        overlap = self._overlap28(fused=True)
-        key = (M, adam, overlap)
+        overlap = self._overlap28(fused=True) and not self.comm_split_tail
+        key = (M, adam, overlap, self.comm_split_tail)
         packs = self._comm_packs.get(key)
         if packs is not None:
             return packs
@@ -1168,7 +1177,10 @@ class ConvVaeTrainer:
         names = ["enc1", "enc2", "enc_head", "dec_fc", "dec1", "dec2"]
         enc = [jobs[i] for i, n in enumerate(names) if not n.startswith("dec")]
         dec = [jobs[i] for i, n in enumerate(names) if n.startswith("dec")] + [jobs[len(names)]]
-        if overlap:
+        if self.comm_split_tail:
+            tables = [jobs, [self._comm_job(segs, units, lu[0], lu[L], 1, adam)],
+                      [self._comm_job(segs, units, lu[0], lu[L], 2, adam)]]
+        elif overlap:
             tables = [dec,
                       enc + [self._comm_job(segs, units, lu[fd], lu[L], 1, adam)],
                       [self._comm_job(segs, units, lu[0], lu[fd], 3, adam),

@@ -62,6 +62,12 @@ def main():
         tr.refresh_weights()
         red = make_arena_reducer(dist.group.WORLD, tr.grads, tr.bucket_bounds(bucket_mb), kind=kind)
         tr.attach_reducer(red)
+        if kind == "xgmi" and image == 28:
+            # ranks share one GPU: a reduce spinning on a peer's push could hold the CUs that
+            # peer needs, so push and reduce go in separate launches with a host barrier between
+            # (eager steps; on a node every rank owns its GPU and the reduce waits in-kernel)
+            tr.comm_split_tail = True
+            tr.comm_phase_hook = lambda: (torch.cuda.synchronize(), dist.barrier())
         tr.bind_train_data(X, idx)
         tr.set_cursor(0, nb)
         same_each = []

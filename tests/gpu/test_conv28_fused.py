@@ -402,3 +402,35 @@ def test_f28_exchange_timeout_fails_bench_and_trial(tmp_path):
     assert "FAILED: TrialCorrupted" in text, text[-4000:]
     agg = json.loads(re.search(r"MDT_AGGREGATE (.*)", text).group(1))
     assert agg["failed_trials"] == [0], agg
+
+
+def test_f28_pair_and_solo_are_bitwise_equal(native_ext):
+    """The one-workgroup fallback sums every K-split partial (head forward,
+    dec_fc backward, head backward row groups, enc2 bias rows) in the paired
+    step's order, so which form a sample takes -- a matter of dispatch timing
+    under contention -- never changes the bits."""
+    dev = torch.device("cuda")
+    X = torch.rand(4 * 128, 784, generator=torch.Generator().manual_seed(8)).to(dev)
+    idx = torch.arange(4 * 128, device=dev, dtype=torch.int32)
+    res = {}
+    for pair in (True, False):
+        tr = _trainer(seed=11, use_graphs=False)
+        tr.f28_pair = pair
+        tr.f28_skip_adam = True
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 4)
+        tr.train_steps(1)
+        torch.cuda.synchronize()
+        snap = {"grads": tr.grads.clone(), "dmulv": tr.dmulv.clone(), "mulv": tr.mulv.clone(),
+                "bias": tr.f28_bias.clone(), "part": tr.f28_part.clone()}
+        snap.update({"gact." + k: v.clone() for k, v in tr.gacts.items()})
+        snap.update({"act." + k: v.clone() for k, v in tr.acts.items()})
+        tr.f28_skip_adam = False
+        tr.train_steps(5)
+        torch.cuda.synchronize()
+        snap["loss"] = torch.from_numpy(tr.loss_history()[:6].copy())
+        snap["params"] = tr.params.clone()
+        res[pair] = snap
+    diff = {k: (res[True][k].float() - res[False][k].float()).abs().max().item() for k in res[True]
+            if not torch.equal(res[True][k], res[False][k])}
+    assert not diff, diff

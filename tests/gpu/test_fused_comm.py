@@ -73,13 +73,8 @@ def test_fused_reducer_one_rank_is_bitwise_reducer_free(native_ext, graphs, pair
     assert int(tr.f28_err.item()) == 0
     assert red.launched_count() == 0  # no stream-side collectives: everything ran as jobs
     assert np.isfinite(h0).all() and tr.read_state()["step"] == steps
-    if pair:
-        np.testing.assert_array_equal(h1, h0)
-        assert torch.equal(p1, p0), (p1 - p0).abs().max().item()
-    else:
-        # one workgroup per sample: not run-to-run bitwise on this stack (see
-        # test_conv28_fused.py::test_f28_solo_run_to_run), so rounding-level only
-        np.testing.assert_allclose(h1, h0, rtol=1e-4)
+    np.testing.assert_array_equal(h1, h0)
+    assert torch.equal(p1, p0), (p1 - p0).abs().max().item()
 
 
 @pytest.mark.parametrize("overlap", [True, False])
