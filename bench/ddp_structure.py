@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--model", default="conv28", choices=["conv28", "conv128"],
+                    help="conv128: the layer-by-layer 128x128 step at B=64 (config #5 model)")
+    ap.add_argument("--bucket-mb", type=float, default=None, help="RCCL bucket cap (default: decoder | encoder)")
     a = ap.parse_args()
     from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
     from multidisttorch_amd.parallel.ddp import make_arena_reducer
@@ -56,19 +59,21 @@ def main():
     dev = torch.device("cuda", 0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     pg = dist.group.WORLD
-    B, nb = 128, 16
-    X = torch.rand(nb * B, 784, generator=torch.Generator().manual_seed(3)).to(dev)
+    img = 28 if a.model == "conv28" else 128
+    B, nb = (128, 16) if img == 28 else (64, 8)
+    X = torch.rand(nb * B, img * img, generator=torch.Generator().manual_seed(3)).to(dev)
     idx = torch.arange(nb * B, device=dev, dtype=torch.int32)
 
     def make(kind, overlap=True):
-        tr = ConvVaeTrainer(batch_size=B, image=28, z=32, device=dev, backend="hip", seed=4, lr=2e-3,
-                            use_graphs=True, graph_steps=a.steps)
+        tr = ConvVaeTrainer(batch_size=B, image=img, z=32 if img == 28 else 64, device=dev, backend="hip", seed=4,
+                            lr=2e-3, use_graphs=True, graph_steps=a.steps)
         tr.ddp_overlap = overlap
+        bounds = tr.bucket_bounds(a.bucket_mb)
         if kind == "rccl":
-            tr.attach_reducer(make_arena_reducer(pg, tr.grads, tr.default_bucket_bounds(), kind="rccl", scale=2.0))
+            tr.attach_reducer(make_arena_reducer(pg, tr.grads, bounds, kind="rccl", scale=2.0))
             tr.set_hparams(grad_scale=0.5)
         elif kind == "xgmi":
-            tr.attach_reducer(make_arena_reducer(pg, tr.grads, tr.default_bucket_bounds(), kind="xgmi"))
+            tr.attach_reducer(make_arena_reducer(pg, tr.grads, bounds, kind="xgmi"))
         tr.bind_train_data(X, idx)
         tr.set_cursor(0, nb)
         return tr
@@ -87,14 +92,23 @@ def main():
         assert tr.health_error() is None, tr.health_error()
         return best * 1e6
 
-    out = {}
-    for name, kind, ov in (("none", None, True), ("rccl_overlap", "rccl", True), ("rccl_inline", "rccl", False),
-                           ("xgmi_overlap", "xgmi", True), ("xgmi_flat", "xgmi", False)):
+    out = {"model": a.model, "batch": B}
+    variants = (("none", None, True), ("rccl_overlap", "rccl", True), ("rccl_inline", "rccl", False),
+                ("xgmi_overlap", "xgmi", True), ("xgmi_flat", "xgmi", False))
+    if img == 128:  # layer path: RCCL buckets on their own stream as layers complete; fused pushes in the launches
+        variants = (("none", None, True), ("rccl", "rccl", True), ("xgmi", "xgmi", True))
+    for name, kind, ov in variants:
         tr = make(kind, ov)
         out[name] = round(timeit(tr), 2)
         print(f"{name:14s} {out[name]:8.2f} us/step  ratio {out[name] / out['none']:.3f}", flush=True)
         del tr
     out["ratio"] = {k: round(v / out["none"], 3) for k, v in out.items() if isinstance(v, float)}
+    if img != 28:
+        if a.json:
+            with open(a.json, "w") as f:
+                json.dump(out, f, indent=1)
+        dist.destroy_process_group()
+        return
 
     # in-launch overlap evidence: per-workgroup stamps of the fused-reducer step's job launches
     tr = make("xgmi", True)

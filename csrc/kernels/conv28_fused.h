@@ -664,7 +664,9 @@ __device__ __forceinline__ void fwd_rest(const FwdArgs& a, uint8_t* lds, int n) 
   for (int pix = tid; pix < 784; pix += kThreads) {
     const int oy = pix / 28, ox = pix - 28 * (pix / 28);
     const int ca = oy & 1, cb = ox & 1, jy = oy >> 1, jx = ox >> 1;
-    float t = Bias[kB4];
+    // channels 0..15 and 16..31 in two partial sums added last, as the
+    // paired step's two halves (conv28_pair.h P7, exchanged in X3)
+    float th[2] = {0.f, 0.f};
 #pragma unroll 1
     for (int ty = 0; ty < 2; ++ty)
 #pragma unroll
@@ -678,6 +680,7 @@ __device__ __forceinline__ void fwd_rest(const FwdArgs& a, uint8_t* lds, int n) 
           for (int ch = 0; ch < 4; ++ch) {
             const bf16x8 dv = dp[ch];
             const float4 w0 = wp[2 * ch], w1 = wp[2 * ch + 1];
+            float& t = th[ch >> 1];
             t = fmaf((float)dv[0], w0.x, t); t = fmaf((float)dv[1], w0.y, t);
             t = fmaf((float)dv[2], w0.z, t); t = fmaf((float)dv[3], w0.w, t);
             t = fmaf((float)dv[4], w1.x, t); t = fmaf((float)dv[5], w1.y, t);
@@ -685,6 +688,7 @@ __device__ __forceinline__ void fwd_rest(const FwdArgs& a, uint8_t* lds, int n) 
           }
         }
       }
+    const float t = Bias[kB4] + (th[0] + th[1]);
     const float x = Xs[pix];
     const float p = 1.f / (1.f + expf(-t));
     const float g = p - x;

@@ -340,6 +340,24 @@ const Combo kCombos[] = {
     // workgroups in its own launch: 15.9 -> 14.2 us, profiles/r3_dconv2)
     COMBO2(Wg0, DcJS2),
     COMBO2(Wg0, DcJT2),
+    // intra-group DDP with the fused xGMI all-reduce (comm_jobs.h): a backward
+    // launch also pushes the gradients the previous launches completed; the
+    // tail reduces + applies Adam (two comm jobs) after the first layer's
+    // weight gradient pushed the rest
+    COMBO3(IgC1, Wg0, JComm),
+    COMBO3(IgC4, Wg0, JComm),
+    COMBO3(IgC5, Wg0, JComm),
+    COMBO3(IgC6, Wg0, JComm),
+    COMBO3(IgT1, Wg0, JComm),
+    COMBO3(IgT2, Wg0, JComm),
+    COMBO3(IgT4, Wg0, JComm),
+    COMBO3(IgT5, Wg0, JComm),
+    COMBO3(IgT6, Wg0, JComm),
+    COMBO3(Wg0, JComm, DcJS2),
+    COMBO3(Wg0, JComm, DcJT2),
+    COMBO2(TwF, JComm),
+    COMBO2(WgT5f, JComm),
+    COMBO2(JComm, JComm),
 };
 
 #undef COMBO3

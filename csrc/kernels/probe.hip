@@ -33,6 +33,15 @@ __global__ void probe_latency(const int* idx, int hops, unsigned long long* out)
 
 __global__ void probe_empty() {}
 
+// Fill every CU's LDS (the whole 160 KB, one 1024-thread workgroup per CU at
+// a time) with a pattern: an uninitialised-LDS read in a later kernel then
+// shows up as a changed result (tests: the fused step under a poisoned LDS).
+__global__ void __launch_bounds__(1024) probe_lds_poison(unsigned pattern) {
+  extern __shared__ unsigned lds_all[];
+  for (int i = threadIdx.x; i < 160 * 1024 / 4; i += blockDim.x) lds_all[i] = pattern;
+  __syncthreads();
+}
+
 }  // namespace mdt
 
 extern "C" int mdt_probe_clock(unsigned long long* out, int iters, hipStream_t s) {
@@ -47,5 +56,13 @@ extern "C" int mdt_probe_latency(const int* idx, int hops, unsigned long long* o
 
 extern "C" int mdt_probe_empty(int blocks, int threads, hipStream_t s) {
   hipLaunchKernelGGL(mdt::probe_empty, dim3(blocks), dim3(threads), 0, s);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mdt_probe_lds_poison(unsigned pattern, int blocks, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&mdt::probe_lds_poison),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return (int)attr;
+  hipLaunchKernelGGL(mdt::probe_lds_poison, dim3(blocks), dim3(1024), 160 * 1024, s, pattern);
   return (int)hipGetLastError();
 }

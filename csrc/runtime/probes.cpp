@@ -5,6 +5,7 @@
 extern "C" int mdt_probe_clock(unsigned long long* out, int iters, hipStream_t s);
 extern "C" int mdt_probe_latency(const int* idx, int hops, unsigned long long* out, hipStream_t s);
 extern "C" int mdt_probe_empty(int blocks, int threads, hipStream_t s);
+extern "C" int mdt_probe_lds_poison(unsigned pattern, int blocks, hipStream_t s);
 
 namespace mdt {
 
@@ -25,6 +26,12 @@ void probe_latency(at::Tensor idx, int64_t hops, at::Tensor out) {
 void probe_empty(int64_t blocks, int64_t threads) {
   TORCH_CHECK(mdt_probe_empty((int)blocks, (int)threads, c10::hip::getCurrentHIPStream().stream()) == 0,
               "probe_empty");
+}
+
+void probe_lds_poison(int64_t pattern, int64_t blocks) {
+  TORCH_CHECK(blocks > 0 && blocks <= 65536, "probe_lds_poison: blocks");
+  TORCH_CHECK(mdt_probe_lds_poison((unsigned)pattern, (int)blocks, c10::hip::getCurrentHIPStream().stream()) == 0,
+              "probe_lds_poison");
 }
 
 }  // namespace mdt

@@ -441,10 +441,11 @@ class ConvVaeTrainer:
             return 0
         return int(red.comm_ctx())
 
-    def _comm_job(self, segs, units, u0, u1, mode, adam):
-        """A recorded all-reduce job over finalize units [u0, u1) of a plan."""
+    def _comm_job(self, segs, units, u0, u1, mode, adam, job=None):
+        """A recorded all-reduce job over finalize units [u0, u1) of a plan
+        (into ``job`` when given)."""
         st = self.state
-        j = self.C.Job()
+        j = self.C.Job() if job is None else job
         self.C.comm_job(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, segs,
                         units.narrow(0, u0 * 12, (u1 - u0) * 12), u1 - u0, st.train_state, st.hparams, adam,
                         self._comm_ctx(), mode, j)
@@ -856,6 +857,13 @@ class ConvVaeTrainer:
         st = self.state
         g = self.dlog16
         red = self.reducer
+        # fused xGMI all-reduce (comm_jobs.h): a backward launch with a free job
+        # slot also pushes the layers the previous launches completed
+        # (``pending``); the tail pushes the rest, reduces and applies Adam
+        fused = red is not None and self.fuse_jobs and bool(self._comm_ctx())
+        pend_lo = pend_hi = len(spec)  # layers [pend_lo, pend_hi) complete, not yet pushed
+        if fused:
+            red = None
         if red is not None:
             bounds = list(red.bounds())
             starts = {b: i for i, (l, b, e) in enumerate(self.layer_ranges())}
@@ -937,14 +945,21 @@ class ConvVaeTrainer:
                 break
             if spread and len(fns) == 2 and i + 1 < fin_hi and self._run_with_finalize(fns, M, i + 1, fin_hi):
                 fin_hi = i + 1
+            elif fused and len(fns) in (1, 2) and pend_lo < pend_hi and \
+                    self._run_with_comm(fns, M, pend_lo, pend_hi):
+                pend_hi = pend_lo
             else:
                 self._run_group(fns)
             for f in after:
                 f()
+            if fused:
+                pend_lo = i  # layer i's gradients are complete now
             if prev is None:
                 assert not carry
                 if red is not None:
                     self._maybe_launch_bucket(red, bounds, starts, 0, M)
+                if fused:
+                    self._comm_tail(M, pend_lo, pend_hi)
                 break
             g = gin
 
@@ -964,6 +979,47 @@ class ConvVaeTrainer:
         if os.getenv("MDT_JOBS_DEBUG"):
             print(f"[jobs] no finalize fusion: kinds={sorted(j.kind for j in jobs)}", file=sys.stderr, flush=True)
         return False
+
+    def _run_with_comm(self, fns, M, lo, hi):
+        """Launch the jobs ``fns`` plus the push (comm_jobs.h, mode 1) of layers
+        [lo, hi) as ONE kernel; False (nothing launched) when that combination
+        has no instantiation."""
+        jobs = [self.C.Job() for _ in range(len(fns) + 1)]
+        for f, j in zip(fns, jobs):
+            f(j)
+        p = self._plan(M)
+        lu = p["layer_units"]
+        self._comm_job(p["segs"], p["units"], lu[lo], lu[hi], 1, True, job=jobs[-1])
+        if all(j.kind > 0 for j in jobs) and self.C.launch_jobs(jobs):
+            self._fused_launches += 1
+            return True
+        if os.getenv("MDT_JOBS_DEBUG"):
+            print(f"[jobs] no comm fusion: kinds={sorted(j.kind for j in jobs)}", file=sys.stderr, flush=True)
+        return False
+
+    def _comm_tail(self, M, lo, hi):
+        """After the first layer's backward launch: push+reduce+Adam of the
+        layers not pushed yet ([lo, hi), the first layer included) || reduce+Adam
+        of the ones pushed by the backward launches ([hi, L)), one launch."""
+        p, L = self._plan(M), len(self.spec)
+        lu = p["layer_units"]
+        jobs = [self._comm_job(p["segs"], p["units"], lu[lo], lu[hi], 3, True)]
+        if hi < L:
+            jobs.append(self._comm_job(p["segs"], p["units"], lu[hi], lu[L], 2, True))
+        if len(jobs) == 2:
+            ok = self.C.launch_jobs(jobs)
+            assert ok, "jobs_k<JComm, JComm> missing from conv_jobs.hip"
+        else:
+            pack, grid = self._comm_single_pack(("tail", M, lo, hi), jobs[0])
+            self.C.launch_jobs_multi(pack, grid)
+
+    def _comm_single_pack(self, key, job):
+        """Device job table of a single comm job (cached by ``key``: replayed
+        graphs keep reading it)."""
+        if key not in self._comm_packs:
+            pack, grid = self.C.pack_jobs_multi([job])
+            self._comm_packs[key] = (pack.to(self.device), grid)
+        return self._comm_packs[key]
 
     def _wt_deferred(self):
         """The transposed weight copies (w16t) of a step's update are written by
@@ -1016,11 +1072,13 @@ class ConvVaeTrainer:
             return
         # intra-group DDP: the backward finalizes + launches each gradient bucket
         # as it completes (loss reduction in its first launch); Adam after the
-        # all-reduces
+        # all-reduces. Fused xGMI reducer: pushes ride in the backward launches,
+        # the tail reduces + applies Adam (no stream-side collectives to wait for)
         self._backward_hip(M, with_loss=True)
-        self.reducer.wait_all()
-        C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
-                    st.train_state, st.hparams, True)
+        if not (self.fuse_jobs and self._comm_ctx()):
+            self.reducer.wait_all()
+            C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
+                        st.train_state, st.hparams, True)
         self._transpose_weights()
 
     # ----------------------------------------------------------- fused 28x28

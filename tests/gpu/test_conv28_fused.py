@@ -434,3 +434,28 @@ def test_f28_pair_and_solo_are_bitwise_equal(native_ext):
     diff = {k: (res[True][k].float() - res[False][k].float()).abs().max().item() for k in res[True]
             if not torch.equal(res[True][k], res[False][k])}
     assert not diff, diff
+
+
+@pytest.mark.parametrize("pair", [False, True])
+def test_f28_no_uninitialised_lds_reads(pair, native_ext):
+    """Every LDS word the fused step reads is written in the same launch:
+    poisoning every CU's LDS (NaN / a large finite pattern) before each step
+    leaves the results bitwise unchanged."""
+    dev = torch.device("cuda")
+    X = torch.rand(4 * 128, 784, generator=torch.Generator().manual_seed(4)).to(dev)
+    idx = torch.arange(4 * 128, device=dev, dtype=torch.int32)
+    res = []
+    for pattern in (None, 0x7FC00000, 0x4B000000):  # clean, quiet NaN, 8388608.0
+        tr = _trainer(seed=12, use_graphs=False)
+        tr.f28_pair = pair
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 4)
+        for _ in range(4):
+            if pattern is not None:
+                tr.C.probe_lds_poison(pattern, 2048)
+            tr.train_steps(1)
+        torch.cuda.synchronize()
+        res.append((tr.loss_history()[:4].copy(), tr.params.clone()))
+    for h, p in res[1:]:
+        np.testing.assert_array_equal(h, res[0][0])
+        assert torch.equal(p, res[0][1])

@@ -143,3 +143,38 @@ def test_fused_ddp_step_cost_vs_reducer_free(native_ext):
     ddp = _time_steps(tr, X, idx, nb)
     print(f"\nreducer-free {base:.1f} us/step, fused one-rank DDP {ddp:.1f} us/step, ratio {ddp / base:.3f}")
     assert ddp <= 1.2 * base, (base, ddp)
+
+
+@pytest.mark.parametrize("image", [128, 28])
+def test_fused_reducer_layer_path_bitwise(native_ext, image):
+    """The layer-by-layer step (128x128; 28x28 with MDT_CONV_F28=0) with the
+    fused reducer on one rank: pushes ride in the backward launches, the tail
+    reduces + applies Adam; bitwise the reducer-free step, eager and graphs."""
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    dev = torch.device("cuda", 0)
+    B = 32 if image == 128 else 128
+    nb, steps = 4, 6
+    X = torch.rand(nb * B, image * image, generator=torch.Generator().manual_seed(5)).to(dev)
+    idx = torch.arange(nb * B, device=dev, dtype=torch.int32)
+    for graphs in (False, True):
+        out = []
+        for fused in (False, True):
+            tr = ConvVaeTrainer(batch_size=B, image=image, z=32 if image == 28 else 64, device=dev, backend="hip",
+                                seed=6, lr=2e-3, use_graphs=graphs, graph_steps=3)
+            tr.f28 = False
+            if fused:
+                red = _fused_reducer(tr)
+                tr.attach_reducer(red)
+            tr.bind_train_data(X, idx)
+            tr.set_cursor(0, nb)
+            tr.train_steps(steps)
+            tr._ensure_wt()  # the reducer-free 28x28 layer path defers the last step's transposes
+            torch.cuda.synchronize()
+            out.append((tr.loss_history()[:steps].copy(), tr.params.clone(), tr.w16t.clone()))
+            if fused:
+                assert int(red.status()) == 0 and red.launched_count() == 0
+                assert tr._fused_launches > 0
+        np.testing.assert_array_equal(out[1][0], out[0][0])
+        assert torch.equal(out[1][1], out[0][1]), (out[1][1] - out[0][1]).abs().max().item()
+        assert torch.equal(out[1][2], out[0][2])  # transposed copies of the updated weights
