@@ -283,12 +283,13 @@ __device__ __forceinline__ void conv14to7(const uint8_t* in_img, BFrag bfrag, Pr
 // class rows = 49 pixels (jy, jx) with (oy, ox) = (2jy + a, 2jx + b), k = 2x2
 // taps (ky = 1 - a + 2ty, iy = jy + a - ty) x 64 channels, cols = 32. A from the
 // img49 LDS image `in`, B via tr_frag from the per-tap images `wimg`.
-// 32 items (class, m-tile, n-tile), four per wave. `cs` (optional) receives
-// the per-column sums of the epilogue values of this wave's items.
+// 32 items (class, m-tile, n-tile), four per wave. `cs[q]` receives the
+// per-column sum of the epilogue values of this wave's item of class q
+// (column 16 nj + (lane & 15), nj = w & 1; m-tile (w >> 1) & 3), kept per
+// item so a caller can add them in the paired step's order.
 template <class Pre, class Epi>
-__device__ __forceinline__ void tconv7to14(const uint8_t* in, const uint8_t* wimg, Pre pre, Epi epi, float (&cs)[2]) {
+__device__ __forceinline__ void tconv7to14(const uint8_t* in, const uint8_t* wimg, Pre pre, Epi epi, float (&cs)[4]) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  cs[0] = cs[1] = 0.f;
   // items it = w + 8q: class q, m-tile (w >> 1) & 3, n-tile w & 1 (fixed per wave)
   const int mt = (w >> 1) & 3, nj = w & 1;
   float pv[4][4];
@@ -327,7 +328,7 @@ __device__ __forceinline__ void tconv7to14(const uint8_t* in, const uint8_t* wim
     }
     s += __shfl_xor(s, 16, 64);
     s += __shfl_xor(s, 32, 64);
-    cs[nj] += s;
+    cs[q] = s;
   }
 }
 
@@ -648,7 +649,7 @@ __device__ __forceinline__ void fwd_rest(const FwdArgs& a, uint8_t* lds, int n) 
   stamp(a.stamps, 6);
   // ---- P6: dec1 (convT 64 -> 32, 7x7 -> 14x14, MFMA), ReLU
   {
-    float cs[2];
+    float cs[4];
     tconv7to14(D0u, W3s, [&](int, int co) { return Bias[kB3 + co]; }, [&](int pix, int co, float v, float bias) {
       const __bf16 o = (__bf16)fmaxf(v + bias, 0.f);
       D1s[pix * 32 + co] = o;
@@ -1012,7 +1013,7 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds, int n) 
   stamp(a.stamps, 6);
   // ---- Q6: enc2 backward-data (convT 64 -> 32 with the conv weights, 7 -> 14) x enc1 ReLU mask
   {
-    float cs[2];
+    float cs[4];
     tconv7to14(GA2u, W2s,
                [&](int pix, int co) {
                  if constexpr (MERGED)  // enc1's output is still in LDS (img14)
@@ -1026,16 +1027,23 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds, int n) 
       a.ga1[e] = (__bf16)g;
       return g;
     }, cs);
+    // item sums S[q][mt][col] (col = 16 nj + lane), combined below in the
+    // paired step's order: half nj, wave i = (m-tile i & 3, classes i >> 2 and
+    // (i >> 2) + 2) -- conv28_pair.h tconv7to14_half + its enc1-bias sum
     if (lane < 16) {
-      CS[w * 64 + lane] = cs[0];
-      CS[w * 64 + 16 + lane] = cs[1];
+      const int mt = (w >> 1) & 3, col = 16 * (w & 1) + lane;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) CS[(q * 4 + mt) * 32 + col] = cs[q];
     }
   }
   lds_barrier();
   if (tid < 32) {
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s += CS[i * 64 + tid];
+    for (int i = 0; i < 8; ++i) {
+      const int mt = i & 3, q = i >> 2;
+      s += CS[(q * 4 + mt) * 32 + tid] + CS[((q + 2) * 4 + mt) * 32 + tid];
+    }
     a.db1_part[(size_t)n * 32 + tid] = s;
   }
   stamp(a.stamps, 7);

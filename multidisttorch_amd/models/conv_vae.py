@@ -1075,10 +1075,12 @@ class ConvVaeTrainer:
         # all-reduces. Fused xGMI reducer: pushes ride in the backward launches,
         # the tail reduces + applies Adam (no stream-side collectives to wait for)
         self._backward_hip(M, with_loss=True)
-        if not (self.fuse_jobs and self._comm_ctx()):
-            self.reducer.wait_all()
-            C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
-                        st.train_state, st.hparams, True)
+        if self.fuse_jobs and self._comm_ctx():
+            self._wtrans_layers(1, len(self.spec))  # the first layer's copy is never read
+            return
+        self.reducer.wait_all()
+        C.adam_cast(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, self.segs, self.nseg,
+                    st.train_state, st.hparams, True)
         self._transpose_weights()
 
     # ----------------------------------------------------------- fused 28x28

@@ -421,8 +421,13 @@ def test_f28_pair_and_solo_are_bitwise_equal(native_ext):
         tr.set_cursor(0, 4)
         tr.train_steps(1)
         torch.cuda.synchronize()
+        B = 128
+        fb, fp = tr.f28_bias, tr.f28_part
         snap = {"grads": tr.grads.clone(), "dmulv": tr.dmulv.clone(), "mulv": tr.mulv.clone(),
-                "bias": tr.f28_bias.clone(), "part": tr.f28_part.clone()}
+                "dlog32": tr.dlog32.clone(),
+                "bias.dbd": fb[:B * 3136].clone(), "bias.db3": fb[B * 3136:B * 3168].clone(),
+                "bias.db2": fb[B * 3168:B * 3296].clone(), "bias.db1": fb[B * 3296:].clone(),
+                "part.bce": fp[:B].clone(), "part.kld": fp[B:2 * B].clone(), "part.db4": fp[2 * B:].clone()}
         snap.update({"gact." + k: v.clone() for k, v in tr.gacts.items()})
         snap.update({"act." + k: v.clone() for k, v in tr.acts.items()})
         tr.f28_skip_adam = False
