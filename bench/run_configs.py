@@ -78,6 +78,22 @@ def run_bench(nproc: int, args, steps: int, warmup: int, env_extra=None, timeout
     return json.loads(line)
 
 
+def ddp_structure(model: str, timeout: int = 600):
+    """Per-step time of the reducer-free step and of the DDP step with forced
+    one-rank collectives (RCCL, fused xGMI jobs), and their ratios."""
+    out = os.path.join("/tmp", f"mdt_ddp_structure_{model}_{os.getpid()}.json")
+    cmd = [sys.executable, os.path.join(ROOT, "bench", "ddp_structure.py"), "--model", model, "--steps", "10",
+           "--json", out]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    if r.returncode != 0 or not os.path.exists(out):
+        return {"error": f"rc={r.returncode}", "tail": (r.stdout + r.stderr)[-1000:]}
+    with open(out) as f:
+        d = json.load(f)
+    os.unlink(out)
+    d.pop("xgmi_overlap_job_spans", None)
+    return d
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="bench_configs.json")
@@ -93,8 +109,14 @@ def main(argv=None):
     for k in sorted(only):
         c = CONFIGS[k]
         if c["gpus"] > ngpu:
-            results["configs"][k] = {"desc": c["desc"], "skipped": f"needs {c['gpus']} GPUs, have {ngpu}"}
-            print(f"config #{k}: skipped ({c['gpus']} GPUs needed)", flush=True)
+            rec = {"desc": c["desc"], "skipped": f"needs {c['gpus']} GPUs, have {ngpu}"}
+            if k in (4, 5) and ngpu >= 1:
+                # what one GPU CAN measure: the intra-group DDP step's structure cost
+                # with every collective forced on a one-rank group (bench/ddp_structure.py)
+                rec["one_gpu_ddp_structure"] = ddp_structure("conv28" if k == 4 else "conv128")
+            results["configs"][k] = rec
+            print(f"config #{k}: skipped ({c['gpus']} GPUs needed); one-GPU DDP structure: "
+                  f"{json.dumps(rec.get('one_gpu_ddp_structure'))[:300]}", flush=True)
             continue
         res = run_bench(c["nproc"], c["args"], a.steps, a.warmup, c.get("env"))
         res["desc"] = c["desc"]
