@@ -607,8 +607,8 @@ __device__ __forceinline__ void fwd_rest(const FwdArgs& a, uint8_t* lds, int n) 
                                        a.hp->seed_lo, a.hp->seed_hi);
       const float ep = normal_from_bits(bits.x, bits.y);
       const float sd = expf(0.5f * lv);
-      const float zz = mu + ep * sd;
-      kl = 1.f + lv - mu * mu - sd * sd;
+      const float zz = fmaf(ep, sd, mu);
+      kl = fmaf(-sd, sd, fmaf(-mu, mu, 1.f + lv));  // explicit: one rounding sequence in both bodies
       Zs[c] = (__bf16)zz;
       reinterpret_cast<float*>(lds + L::Red)[c] = ep;  // the merged step's Q4 (Red is free after P3)
       if (a.train) {
@@ -694,7 +694,7 @@ __device__ __forceinline__ void fwd_rest(const FwdArgs& a, uint8_t* lds, int n) 
     const float p = 1.f / (1.f + expf(-t));
     const float g = p - x;
     const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));
-    loss += x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
+    loss += fmaf(x, fminf(sp_pos - t, 100.f), (1.f - x) * fminf(sp_pos, 100.f));  // explicit fma (see kl)
     gsum += g;
     if (a.train) a.dlog[(size_t)n * 784 + pix] = g;
     if constexpr (L::G >= 0) reinterpret_cast<float*>(lds + L::G)[pix] = g;  // the merged step's backward

@@ -467,8 +467,8 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
       Hs[c] = mu;
       Hs[32 + c] = lv;
       const float sd = expf(0.5f * lv);
-      const float zz = mu + ep * sd;
-      kl = 1.f + lv - mu * mu - sd * sd;
+      const float zz = fmaf(ep, sd, mu);
+      kl = fmaf(-sd, sd, fmaf(-mu, mu, 1.f + lv));  // explicit: one rounding sequence in both bodies
       Zs[c] = (__bf16)zz;
       Eps[c] = ep;
       if (train && r == 0) {
@@ -592,7 +592,7 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
         const float p = 1.f / (1.f + expf(-t));
         const float g = p - x;
         const float sp_pos = fmaxf(t, 0.f) + log1pf(expf(-fabsf(t)));
-        loss += x * fminf(sp_pos - t, 100.f) + (1.f - x) * fminf(sp_pos, 100.f);
+        loss += fmaf(x, fminf(sp_pos - t, 100.f), (1.f - x) * fminf(sp_pos, 100.f));  // explicit fma (see kl)
         gsum += g;
         Gs[pix] = g;
         if (train && (pix >= 392) == (r == 1)) dlp[pix] = g;
