@@ -1,0 +1,61 @@
+"""Host-side DDP policy of round 4 (parallel/ddp.py, models/conv_vae.py):
+when the first-ready bucket is issued early, which reducer kind a group gets,
+and the conv trainer's resolution of MDT_DDP_OVERLAP."""
+import pytest
+
+from multidisttorch_amd.parallel.ddp import overlap_pays
+
+
+def test_overlap_pays_thresholds():
+    # 28x28 decoder bucket: 133,248 f32 gradients = 0.53 MB -> 3.5 us on one 153 GB/s link
+    dec28 = 4 * 133248
+    assert not overlap_pays(dec28, 6.0)       # fused jobs: the split costs 6 us
+    assert not overlap_pays(dec28, 31.0)      # RCCL on its own stream: 31 us
+    # a 16 MB bucket (~110 us on one link) hides behind both
+    assert overlap_pays(16 << 20, 6.0) and overlap_pays(16 << 20, 31.0)
+    # faster links shrink the transfer
+    assert overlap_pays(2 << 20, 6.0, link_gbps=153.0) and not overlap_pays(2 << 20, 6.0, link_gbps=1000.0)
+
+
+def test_conv_trainer_overlap_resolution(monkeypatch):
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    monkeypatch.delenv("MDT_DDP_OVERLAP", raising=False)
+    tr = ConvVaeTrainer(batch_size=8, image=28, backend="torch", seed=0)
+    assert tr.ddp_overlap is None  # auto
+    assert tr._overlap28(fused=True) is False and tr._overlap28(fused=False) is False
+    monkeypatch.setenv("MDT_DDP_OVERLAP", "1")
+    tr = ConvVaeTrainer(batch_size=8, image=28, backend="torch", seed=0)
+    assert tr._overlap28(fused=True) is True
+    monkeypatch.setenv("MDT_DDP_OVERLAP", "0")
+    tr = ConvVaeTrainer(batch_size=8, image=28, backend="torch", seed=0)
+    assert tr._overlap28(fused=False) is False
+
+
+def test_reducer_kind_env_override(monkeypatch):
+    import torch
+
+    from multidisttorch_amd.parallel import ddp
+
+    monkeypatch.setenv("MDT_REDUCER", "p2p2")
+    assert ddp.reducer_kind(None, torch.zeros(4)) == "p2p2"
+
+
+def test_health_error_is_none_on_the_cpu_backend():
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    tr = ConvVaeTrainer(batch_size=4, image=28, backend="torch", seed=0)
+    assert tr.health_error() is None
+
+
+def test_runner_fails_a_trial_on_reported_corruption():
+    from multidisttorch_amd.hpo.runner import _check_health
+    from multidisttorch_amd.runtime.faults import TrialCorrupted
+
+    class Fake:
+        def health_error(self):
+            return "fused 28x28 step: a paired-workgroup exchange timed out (f28_err=1)"
+
+    with pytest.raises(TrialCorrupted, match="exchange timed out"):
+        _check_health(Fake())
+    _check_health(object())  # trainers without the check pass
