@@ -11,6 +11,7 @@ void probe_clock(at::Tensor out, int64_t iters);
 void probe_latency(at::Tensor idx, int64_t hops, at::Tensor out);
 void probe_empty(int64_t blocks, int64_t threads);
 void probe_lds_poison(int64_t pattern, int64_t blocks);
+void probe_cu_ids(at::Tensor out);
 void bind_conv(pybind11::module& m);
 void bind_rccl(pybind11::module& m);
 void bind_p2p(pybind11::module& m);
@@ -23,6 +24,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("probe_clock", &mdt::probe_clock);
   m.def("probe_latency", &mdt::probe_latency);
   m.def("probe_empty", &mdt::probe_empty);
+  m.def("probe_cu_ids", &mdt::probe_cu_ids);
   m.def("probe_lds_poison", &mdt::probe_lds_poison, py::arg("pattern"), py::arg("blocks") = 1024);
   mdt::bind_conv(m);
   mdt::bind_rccl(m);

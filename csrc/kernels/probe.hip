@@ -42,7 +42,26 @@ __global__ void __launch_bounds__(1024) probe_lds_poison(unsigned pattern) {
   __syncthreads();
 }
 
+// Where each workgroup ran: (XCC id << 16) | HW_ID bits (CU, SH, SE) of wave 0.
+// Rehearsal check of HSA_CU_MASK (runtime/env.py::apply_cu_split).
+__global__ void probe_cu_ids(unsigned* out) {
+  if (threadIdx.x != 0) return;
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  // HW_ID: cu_id [11:8], sh_id [12], se_id [15:13]
+  out[blockIdx.x] = (xcc << 16) | (hw & 0xff00u);
+  // keep the workgroup resident long enough that the grid spreads over every allowed CU
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < 2000ull) __builtin_amdgcn_s_sleep(8);
+}
+
 }  // namespace mdt
+
+extern "C" int mdt_probe_cu_ids(unsigned* out, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(mdt::probe_cu_ids, dim3(blocks), dim3(64), 0, s, out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mdt_probe_clock(unsigned long long* out, int iters, hipStream_t s) {
   hipLaunchKernelGGL(mdt::probe_clock, dim3(1), dim3(64), 0, s, out, iters);

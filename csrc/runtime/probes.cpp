@@ -6,6 +6,7 @@ extern "C" int mdt_probe_clock(unsigned long long* out, int iters, hipStream_t s
 extern "C" int mdt_probe_latency(const int* idx, int hops, unsigned long long* out, hipStream_t s);
 extern "C" int mdt_probe_empty(int blocks, int threads, hipStream_t s);
 extern "C" int mdt_probe_lds_poison(unsigned pattern, int blocks, hipStream_t s);
+extern "C" int mdt_probe_cu_ids(unsigned* out, int blocks, hipStream_t s);
 
 namespace mdt {
 
@@ -32,6 +33,12 @@ void probe_lds_poison(int64_t pattern, int64_t blocks) {
   TORCH_CHECK(blocks > 0 && blocks <= 65536, "probe_lds_poison: blocks");
   TORCH_CHECK(mdt_probe_lds_poison((unsigned)pattern, (int)blocks, c10::hip::getCurrentHIPStream().stream()) == 0,
               "probe_lds_poison");
+}
+
+void probe_cu_ids(at::Tensor out) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kInt32 && out.numel() >= 1, "out: cuda int32[blocks]");
+  TORCH_CHECK(mdt_probe_cu_ids(reinterpret_cast<unsigned*>(out.data_ptr<int32_t>()), (int)out.numel(),
+                               c10::hip::getCurrentHIPStream().stream()) == 0, "probe_cu_ids");
 }
 
 }  // namespace mdt
