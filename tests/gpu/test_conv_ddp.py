@@ -174,8 +174,9 @@ def test_conv_bucket_launches_interleave_with_backward(nccl_world, native_ext, i
         assert len(jm) == 2 and jm[0] < first < jm[1], log  # decoder wgrads | decoder bucket | encoder wgrads
 
 
-@pytest.mark.parametrize("image,f28", [(28, True), (28, False), (128, False)])
-def test_conv_step_graph_issues_real_collectives(nccl_world, native_ext, image, f28):
+@pytest.mark.parametrize("image,f28,pair", [(28, True, True), (28, True, False), (28, False, False),
+                                             (128, False, False)])
+def test_conv_step_graph_issues_real_collectives(nccl_world, native_ext, image, f28, pair):
     """A one-rank group's all-reduce is an identity, so the reducer skips it
     unless told otherwise. Here it runs with PreMulSum scale 2 (a real
     ncclAllReduce on every bucket, captured into the replayed step graphs)
@@ -192,6 +193,7 @@ def test_conv_step_graph_issues_real_collectives(nccl_world, native_ext, image, 
     for mode, overlap in (("single", None), ("scaled", True), ("scaled", False)):
         tr = _trainer(image, B, dev, True)
         tr.ddp_overlap = overlap
+        tr.f28_pair = pair  # the paired headline kernel under a real collective too
         if image == 28:
             tr.f28 = f28
         if mode == "scaled":
