@@ -46,8 +46,9 @@ def main():
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--model", default="conv28", choices=["conv28", "conv128"],
-                    help="conv128: the layer-by-layer 128x128 step at B=64 (config #5 model)")
+    ap.add_argument("--model", default="conv28", choices=["conv28", "conv128", "mlp"],
+                    help="conv128: the layer-by-layer 128x128 step at B=64 (config #5 model); "
+                         "mlp: the reference's MLP-VAE step at B=128 (fc4 bucket | rest)")
     ap.add_argument("--bucket-mb", type=float, default=None, help="RCCL bucket cap (default: decoder | encoder)")
     a = ap.parse_args()
     from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
@@ -59,6 +60,8 @@ def main():
     dev = torch.device("cuda", 0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     pg = dist.group.WORLD
+    if a.model == "mlp":
+        return mlp_variants(a, pg, dev)
     img = 28 if a.model == "conv28" else 128
     B, nb = (128, 16) if img == 28 else (64, 8)
     X = torch.rand(nb * B, img * img, generator=torch.Generator().manual_seed(3)).to(dev)
@@ -140,6 +143,46 @@ def main():
     out["xgmi_overlap_job_spans"] = lines
     for l in lines:
         print(f"  launch {l['launch']}  {l['job']:28s} {l['blocks']:5d} WGs  {l['start_us']:7.2f} .. {l['end_us']:7.2f} us")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+    dist.destroy_process_group()
+
+
+def mlp_variants(a, pg, dev):
+    """MLP-VAE step with its two buckets (fc4 | rest): side-stream overlap vs
+    everything inline on the compute stream, for RCCL and the p2p one-shot
+    kernel (scale 2 + grad_scale 0.5 force the collective on one rank)."""
+    from multidisttorch_amd.models.mlp_trainer import MlpVaeTrainer
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+
+    B, nb = 128, 16
+    X = torch.rand(nb * B, 784, generator=torch.Generator().manual_seed(3)).to(dev)
+    idx = torch.arange(nb * B, device=dev, dtype=torch.int32)
+    out = {"model": "mlp", "batch": B}
+    for name, kind, ov in (("none", None, None), ("rccl_overlap", "rccl", True), ("rccl_inline", "rccl", False),
+                           ("xgmi_overlap", "xgmi", True), ("xgmi_inline", "xgmi", False)):
+        tr = MlpVaeTrainer(batch_size=B, device=dev, seed=4, lr=1e-3, use_graphs=True, graph_steps=a.steps)
+        if kind is not None:
+            tr.attach_reducer(make_arena_reducer(pg, tr.grads, tr.bucket_bounds(None), kind=kind, scale=2.0))
+            tr.set_hparams(grad_scale=0.5)
+            tr.ddp_overlap = ov
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, nb)
+        tr.prepare([B])
+        tr.strict_graphs = True
+        tr.train_steps(a.steps)
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            tr.train_steps(a.steps)
+            torch.cuda.synchronize()
+            best = min(best, (time.perf_counter() - t0) / a.steps)
+        out[name] = round(best * 1e6, 2)
+        print(f"{name:14s} {out[name]:8.2f} us/step  ratio {out[name] / out['none']:.3f}", flush=True)
+        del tr
+    out["ratio"] = {k: round(v / out["none"], 3) for k, v in out.items() if isinstance(v, float)}
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)

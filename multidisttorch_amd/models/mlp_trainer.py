@@ -22,6 +22,7 @@ arithmetic, so a run is reproducible across them up to fp32 rounding.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -61,6 +62,13 @@ class MlpVaeTrainer:
         self.graph_steps = max(1, int(graph_steps))
         self._graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
         self.reducer = None
+        # DDP structure (MDT_DDP_OVERLAP, as ConvVaeTrainer): True = the fc4
+        # bucket goes out on the reducer's stream between backward parts;
+        # False = one stream, the whole backward then every bucket inline;
+        # None (auto) = overlap only when the fc4 bucket's transfer over one
+        # xGMI link outweighs the measured cost of the split (overlap_pays)
+        ov = os.getenv("MDT_DDP_OVERLAP", "auto")
+        self.ddp_overlap = None if ov == "auto" else ov != "0"
         self._data = None
         if backend == "hip":
             C = native.require()
@@ -195,11 +203,29 @@ class MlpVaeTrainer:
     def refresh_weights(self):
         """Params are the compute weights here (fp32 views): nothing to re-derive."""
 
+    # measured cost (us per step) of splitting the MLP backward around a
+    # side-stream bucket launch, per reducer family (profiles/r4_ddp_fused)
+    SPLIT_COST_US = {"rccl": 31.0, "p2p": 31.0}
+
+    def _overlap(self) -> bool:
+        red = self.reducer
+        if red is None or red.num_buckets() != 2:
+            return False
+        if self.ddp_overlap is not None:
+            return bool(self.ddp_overlap)
+        from ..parallel.ddp import overlap_pays
+
+        fam = "rccl" if type(red).__name__.startswith("Rccl") else "p2p"
+        return overlap_pays(4 * (self.numel - self.split), self.SPLIT_COST_US[fam])
+
     def _step_hip(self, M: int):
         X, idx = self._data[0], self._data[1]
         e = self.engine
         e.forward(X, idx, M, True, False, self.rng_stream, False)
-        if self.reducer is not None and self.reducer.num_buckets() == 2:
+        early = self._overlap()
+        if self.reducer is not None and hasattr(self.reducer, "set_inline"):
+            self.reducer.set_inline(not early)
+        if early:
             e.backward(X, idx, M, 1, False)
             self.reducer.launch(1)          # fc4 bucket: overlaps B2/B3
             e.backward(X, idx, M, 2, False)
@@ -207,9 +233,10 @@ class MlpVaeTrainer:
             self.reducer.launch(0)
             self.reducer.wait_all()
             e.adam()
-        elif self.reducer is not None:      # single bucket after the whole backward
+        elif self.reducer is not None:      # every bucket after the whole backward
             e.backward(X, idx, M, 0, False)
-            self.reducer.launch_all()
+            for k in reversed(range(self.reducer.num_buckets())):
+                self.reducer.launch(k)
             self.reducer.wait_all()
             e.adam()
         else:
