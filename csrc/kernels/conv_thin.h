@@ -196,6 +196,94 @@ __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* 
   }
 }
 
+// Forward-only form of thin_conv_body (no output mask, no column sums) for
+// stride 2: two horizontally adjacent output pixels per thread. The VALU
+// body issues 16 taps x CO / 4 wave-uniform ds_read_b128 weight reads per
+// pixel, and an LDS broadcast costs as much LDS time as 64 distinct
+// addresses, so it runs LDS-bound (enc1 forward at 128x128, B = 64: 16.9 us,
+// profiles/r3_pmc_end); here each weight read feeds both pixels and the two
+// patches share their middle columns (4 x 6 input loads instead of 2 x 16).
+// Per pixel the arithmetic is the body's own (bias, then one fmaf per tap in
+// tap order), so the output is bitwise the same. Host: thin_conv2_ok.
+template <int CO, int K, typename TIN>
+__device__ __forceinline__ void thin_conv2_body(const ThinConvArgs& ta, uint8_t* lds, int bid) {
+  constexpr int TAPS = K * K, S = 2, XW = K + S;
+  const ConvDesc& d = ta.d;
+  const TIN* X = reinterpret_cast<const TIN*>(ta.X);
+  float* wl = reinterpret_cast<float*>(lds);
+  const int M2 = (d.N * d.OH * d.OW) >> 1;
+  const int m2 = bid * blockDim.x + threadIdx.x;
+  const bool live = m2 < M2;
+  const int m = 2 * (live ? m2 : 0);  // first of the pair; OW even: both in one row
+  const int n = m / (d.OH * d.OW);
+  const int rem = m - n * d.OH * d.OW;
+  const int oy = rem / d.OW, ox = rem - oy * d.OW;
+  const int iy0 = oy * S - d.P, ix0 = ox * S - d.P;
+  const int* rows = ta.idx ? ta.idx + (size_t)ta.st->cursor * ta.B : nullptr;
+  const TIN* img = X + (size_t)(rows ? rows[n] : n) * d.H * d.W;
+  if (ta.xb) {
+    const int p4 = (d.H * d.W) >> 2;
+    const long long tot = (long long)d.N * p4;
+    for (long long e = (long long)bid * blockDim.x + threadIdx.x; e < tot; e += (long long)ta.nblk * blockDim.x) {
+      const int i = (int)(e / p4), c = (int)(e - (long long)i * p4);
+      reinterpret_cast<float4*>(ta.xb + (size_t)i * d.H * d.W)[c] =
+          reinterpret_cast<const float4*>(X + (size_t)(rows ? rows[i] : i) * d.H * d.W)[c];
+    }
+  }
+  if (ta.hp && bid == 0 && threadIdx.x == 0) {
+    TrainState* st = ta.st;
+    st->step = st->step + 1;
+    st->b1pow *= ta.hp->beta1_d;
+    st->b2pow *= ta.hp->beta2_d;
+  }
+  float xin[K][XW];
+#pragma unroll
+  for (int ty = 0; ty < K; ++ty)
+#pragma unroll
+    for (int tx = 0; tx < XW; ++tx) {
+      const int iy = iy0 + ty, ix = ix0 + tx;
+      const bool ok = live && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+      const float x = ld1(img + (ok ? iy * d.W + ix : 0));
+      xin[ty][tx] = ok ? x : 0.f;
+    }
+  float acc0[CO], acc1[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) acc0[c] = acc1[c] = ta.bias ? ta.bias[c] : 0.f;
+  for (int e = threadIdx.x; e < TAPS * CO; e += blockDim.x) {
+    const int c = e / TAPS, t = e - c * TAPS;
+    wl[t * CO + c] = ta.Wf[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t) {
+    const float x0 = xin[t / K][t % K], x1 = xin[t / K][t % K + S];
+#pragma unroll
+    for (int c4 = 0; c4 < CO / 4; ++c4) {
+      const float4 w = *reinterpret_cast<const float4*>(wl + t * CO + 4 * c4);
+      acc0[4 * c4 + 0] = fmaf(x0, w.x, acc0[4 * c4 + 0]);
+      acc1[4 * c4 + 0] = fmaf(x1, w.x, acc1[4 * c4 + 0]);
+      acc0[4 * c4 + 1] = fmaf(x0, w.y, acc0[4 * c4 + 1]);
+      acc1[4 * c4 + 1] = fmaf(x1, w.y, acc1[4 * c4 + 1]);
+      acc0[4 * c4 + 2] = fmaf(x0, w.z, acc0[4 * c4 + 2]);
+      acc1[4 * c4 + 2] = fmaf(x1, w.z, acc1[4 * c4 + 2]);
+      acc0[4 * c4 + 3] = fmaf(x0, w.w, acc0[4 * c4 + 3]);
+      acc1[4 * c4 + 3] = fmaf(x1, w.w, acc1[4 * c4 + 3]);
+    }
+  }
+  if (!live) return;
+#pragma unroll
+  for (int c8 = 0; c8 < CO / 8; ++c8) {
+    bf16x8 o0, o1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o0[j] = (__bf16)(ta.relu ? fmaxf(acc0[8 * c8 + j], 0.f) : acc0[8 * c8 + j]);
+      o1[j] = (__bf16)(ta.relu ? fmaxf(acc1[8 * c8 + j], 0.f) : acc1[8 * c8 + j]);
+    }
+    *reinterpret_cast<bf16x8*>(ta.y16 + (size_t)m * CO + 8 * c8) = o0;
+    *reinterpret_cast<bf16x8*>(ta.y16 + (size_t)(m + 1) * CO + 8 * c8) = o1;
+  }
+}
+
 // Transposed conv with one output channel, conv view (input C = 1 is the
 // convT output, CO = convT input channels): y[n, iy, ix] = bias +
 // sum over the class taps (ty, tx) and co of G[n, oy, ox, co] * W[co][ky][kx].
