@@ -87,7 +87,12 @@ def main(argv=None):
     ap.add_argument("--model", default="mlp", choices=["mlp", "conv28", "conv128"])
     ap.add_argument("--max-steps", type=int, default=None, help="cap the timed steps per epoch")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="conv models: autocast bf16 or fp32")
+    ap.add_argument("--no-miopen", action="store_true",
+                    help="torch.backends.cudnn.enabled = False: torch's own conv kernels instead of MIOpen "
+                         "(the 28x28 bf16 autocast run aborts inside a MIOpen backward kernel on this stack)")
     a = ap.parse_args(argv)
+    if a.no_miopen:
+        torch.backends.cudnn.enabled = False
 
     from multidisttorch_amd.runtime import setup_ddp
     from multidisttorch_amd.parallel.groups import setup_ddp_groups
@@ -183,7 +188,7 @@ def main(argv=None):
     total = samples * K  # samples counted once per trial
     if rank == 0:
         print(json.dumps({"what": "reference-equivalent torch eager (DDP + DataLoader + .item())",
-                          "model": a.model, "amp": str(amp),
+                          "model": a.model, "amp": str(amp), "miopen": not a.no_miopen,
                           "device": str(dev), "trials": K, "world": world, "epochs": a.epochs,
                           "full_epoch": a.full_epoch, "samples_per_trial": samples, "wall_s": round(dt, 4),
                           "aggregate_samples_per_s": round(total / dt, 1),
