@@ -59,3 +59,29 @@ def test_runner_fails_a_trial_on_reported_corruption():
     with pytest.raises(TrialCorrupted, match="exchange timed out"):
         _check_health(Fake())
     _check_health(object())  # trainers without the check pass
+
+
+def test_mlp_trainer_overlap_resolution(monkeypatch):
+    """MLP trainer: auto keeps both buckets inline (the 1.26 MB fc4 bucket
+    moves in ~8 us over one link, less than a side-stream split costs); an
+    explicit MDT_DDP_OVERLAP wins; one bucket never splits."""
+    from multidisttorch_amd.models.mlp_trainer import MlpVaeTrainer
+
+    class FakeReducer:
+        def __init__(self, n):
+            self.n = n
+
+        def num_buckets(self):
+            return self.n
+
+    monkeypatch.delenv("MDT_DDP_OVERLAP", raising=False)
+    tr = MlpVaeTrainer(batch_size=8, backend="torch", seed=0)
+    assert tr.ddp_overlap is None and tr._overlap() is False  # no reducer
+    tr.reducer = FakeReducer(2)
+    assert tr._overlap() is False
+    tr.ddp_overlap = True
+    assert tr._overlap() is True
+    tr.reducer = FakeReducer(1)
+    assert tr._overlap() is False
+    monkeypatch.setenv("MDT_DDP_OVERLAP", "1")
+    assert MlpVaeTrainer(batch_size=8, backend="torch", seed=0).ddp_overlap is True
