@@ -49,7 +49,7 @@ struct ThinConvArgs {
   int B;
   float* xb;
   int nblk;
-  int mfma;            // 1: thin_conv_mfma_body (host: thin_conv_mfma_ok)
+  int mfma;            // 1: thin_conv_mfma_body (host: thin_conv_mfma_ok), 2: thin_conv2_body (thin_conv_form)
 };
 
 // Geometry of the MFMA form of thin_conv (the 128x128 model's enc1 and its
@@ -91,14 +91,36 @@ __host__ inline int thin_conv_mfma_ok(const ConvDesc& d, int x_is_f32) {
 template <int CO, int K>
 constexpr int thin_conv_lds_bytes() { return (K * K * CO + 256 * (CO + 1)) * 4; }
 
+// Two-pixel forward form (thin_conv2_body below): stride 2, even output rows,
+// no output mask or column sums, VALU body selected. MDT_THIN_PX2=0 disables.
+// Body selector for ThinConvArgs::mfma; the grid then covers M / 2 threads.
+__host__ inline int thin_conv_form(const ConvDesc& d, int x_is_f32, bool omask, bool colsum) {
+  const int mfma = thin_conv_mfma_ok(d, x_is_f32);
+  static const bool px2_on = [] {
+    const char* e = getenv("MDT_THIN_PX2");
+    return !(e && e[0] == '0');
+  }();
+  if (!mfma && px2_on && !omask && !colsum && d.S == 2 && d.OW % 2 == 0) return 2;
+  return mfma;
+}
+
 template <typename TIN>
 __device__ void thin_conv_mfma_body(const ThinConvArgs& ta, uint8_t* lds, int bid);
+
+template <int CO, int K, typename TIN>
+__device__ __forceinline__ void thin_conv2_body(const ThinConvArgs& ta, uint8_t* lds, int bid);
 
 template <int CO, int K, typename TIN>
 __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* lds, int bid) {
   if constexpr (CO == 32 && K == 4) {
     if (ta.mfma == 1) {
       thin_conv_mfma_body<TIN>(ta, lds, bid);
+      return;
+    }
+  }
+  if constexpr (K == 4) {
+    if (ta.mfma == 2) {
+      thin_conv2_body<CO, K, TIN>(ta, lds, bid);
       return;
     }
   }
@@ -204,7 +226,7 @@ __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* 
 // profiles/r3_pmc_end); here each weight read feeds both pixels and the two
 // patches share their middle columns (4 x 6 input loads instead of 2 x 16).
 // Per pixel the arithmetic is the body's own (bias, then one fmaf per tap in
-// tap order), so the output is bitwise the same. Host: thin_conv2_ok.
+// tap order), so the output is bitwise the same. Host: thin_conv_form.
 template <int CO, int K, typename TIN>
 __device__ __forceinline__ void thin_conv2_body(const ThinConvArgs& ta, uint8_t* lds, int bid) {
   constexpr int TAPS = K * K, S = 2, XW = K + S;

@@ -26,12 +26,6 @@ __global__ void __launch_bounds__(256) thin_conv_k(ThinConvArgs ta) {
   thin_conv_body<CO, K, TIN>(ta, lds, blockIdx.x);
 }
 
-template <int CO, int K, typename TIN>
-__global__ void __launch_bounds__(256) thin_conv2_k(ThinConvArgs ta) {
-  __shared__ __attribute__((aligned(16))) float lds[K * K * CO];
-  thin_conv2_body<CO, K, TIN>(ta, reinterpret_cast<uint8_t*>(lds), blockIdx.x);
-}
-
 template <int CO, int WS>
 __global__ void __launch_bounds__(256) thin_tconv_patch_k(ThinTconvArgs ta) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[thin_tconv_patch_lds_bytes<CO, WS>()];
@@ -58,16 +52,6 @@ static inline int cdiv_t(long long a, long long b) { return (int)((a + b - 1) / 
 
 extern "C" {
 
-// Two-pixel forward form (thin_conv2_body): stride 2, even output rows, no
-// output mask or column sums, VALU body selected. MDT_THIN_PX2=0 disables.
-static bool thin_conv2_ok(const ConvDesc& d, const void* omask, const float* colsum, int mfma) {
-  static const bool on = [] {
-    const char* e = getenv("MDT_THIN_PX2");
-    return !(e && e[0] == '0');
-  }();
-  return on && !mfma && !omask && !colsum && d.S == 2 && d.OW % 2 == 0;
-}
-
 // conv with a single input channel; x_is_f32 selects f32 / bf16 input.
 int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, const float* bias, int relu, void* y16,
                   const void* omask, float* colsum, const int* idx, void* st, const void* hp, int B, float* xb,
@@ -75,19 +59,14 @@ int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, cons
   if (d.C != 1 || d.KH != 4 || d.KW != 4) return 1;
   if ((idx || xb || hp) && (!st || !x_is_f32 || (d.H * d.W) % 4)) return 1;
   const long long M = (long long)d.N * d.OH * d.OW;
-  const int mfma = thin_conv_mfma_ok(d, x_is_f32);
-  const bool px2 = thin_conv2_ok(d, omask, colsum, mfma);
-  dim3 grid(cdiv_t(px2 ? M / 2 : M, 256)), blk(256);
+  const int mfma = thin_conv_form(d, x_is_f32, omask != nullptr, colsum != nullptr);
+  dim3 grid(cdiv_t(mfma == 2 ? M / 2 : M, 256)), blk(256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
                         colsum, idx, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), B, xb,
                         (int)grid.x, mfma};
 #define THIN(CO_)                                                                     \
   {                                                                                   \
-    if (px2 && x_is_f32)                                                              \
-      hipLaunchKernelGGL((thin_conv2_k<CO_, 4, float>), grid, blk, 0, s, ta);         \
-    else if (px2)                                                                     \
-      hipLaunchKernelGGL((thin_conv2_k<CO_, 4, __bf16>), grid, blk, 0, s, ta);        \
-    else if (x_is_f32)                                                                \
+    if (x_is_f32)                                                                     \
       hipLaunchKernelGGL((thin_conv_k<CO_, 4, float>), grid, blk, 0, s, ta);          \
     else                                                                              \
       hipLaunchKernelGGL((thin_conv_k<CO_, 4, __bf16>), grid, blk, 0, s, ta);         \

@@ -204,8 +204,10 @@ class MlpVaeTrainer:
         """Params are the compute weights here (fp32 views): nothing to re-derive."""
 
     # measured cost (us per step) of splitting the MLP backward around a
-    # side-stream bucket launch, per reducer family (profiles/r4_ddp_fused)
-    SPLIT_COST_US = {"rccl": 31.0, "p2p": 31.0}
+    # side-stream bucket launch, per reducer family: overlap minus inline with
+    # forced one-rank collectives, 77.5 - 56.9 (RCCL) and 81.9 - 68.0 (p2p
+    # kernel) on a 49.0 us step (profiles/r4_ddp_fused/ddp_structure_mlp.json)
+    SPLIT_COST_US = {"rccl": 20.5, "p2p": 14.0}
 
     def _overlap(self) -> bool:
         red = self.reducer
