@@ -1,0 +1,89 @@
+"""Diagnostic: the eager reducer-free SOLO 28x28 step (f28_pair = False) gave
+three distinct results in three fresh runs once (bench/diag_fused_eager.py)
+while graph replays and the paired form stayed bitwise. Which launch reads
+state it did not write? Poisons every CU's LDS (quiet NaN / a large finite
+pattern) right before ONE of the step's three launches (f28_step_k,
+jobs_multi_k, grad_finalize_k) and counts distinct results per variant
+against the graph-replayed result, with and without a concurrent GEMM
+stream perturbing dispatch.
+
+    python bench/diag_solo_lds.py [--runs 4]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class PoisonC:
+    """Proxy of the extension module that poisons LDS before one launch kind."""
+
+    def __init__(self, C, which, pattern):
+        self._C, self._which, self._pattern = C, which, pattern
+
+    def __getattr__(self, name):
+        f = getattr(self._C, name)
+        if name == self._which:
+            def wrapped(*a, **k):
+                self._C.probe_lds_poison(self._pattern, 2048)
+                return f(*a, **k)
+            return wrapped
+        return f
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--runs", type=int, default=4)
+    ap.add_argument("--pair", type=int, default=0)
+    a = ap.parse_args()
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    dev = torch.device("cuda", 0)
+    nb, steps = 4, 8
+    X = torch.rand(nb * 128, 784, generator=torch.Generator().manual_seed(3)).to(dev)
+    idx = torch.arange(nb * 128, device=dev, dtype=torch.int32)
+
+    def run(graphs, which=None, pattern=0, noisy=False):
+        tr = ConvVaeTrainer(batch_size=128, image=28, z=32, device=dev, backend="hip", seed=4, lr=2e-3,
+                            use_graphs=graphs, graph_steps=4)
+        tr.f28_pair = bool(a.pair)
+        if which:
+            tr.C = PoisonC(tr.C, which, pattern)
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, nb)
+        side = torch.cuda.Stream()
+        junk = torch.rand(2048, 2048, device=dev)
+        for _ in range(steps):
+            if noisy:
+                with torch.cuda.stream(side):
+                    for _ in range(3):
+                        junk = junk @ junk
+                        junk = junk / junk.norm()
+            tr.train_steps(1)
+        torch.cuda.synchronize()
+        return tr.loss_history()[:steps].tolist(), tr.params.clone()
+
+    ref = run(True)
+    out = {}
+    variants = [("plain", None, 0), ("poison_f28_nan", "f28_step", 0x7FC00000),
+                ("poison_jobs_nan", "launch_jobs_multi", 0x7FC00000),
+                ("poison_finalize_nan", "grad_finalize", 0x7FC00000),
+                ("poison_jobs_big", "launch_jobs_multi", 0x4B000000),
+                ("poison_finalize_big", "grad_finalize", 0x4B000000)]
+    for noisy in (False, True):
+        for name, which, pat in variants:
+            res = [run(False, which, pat, noisy) for _ in range(a.runs)]
+            same = [h == ref[0] and torch.equal(p, ref[1]) for h, p in res]
+            finite = [bool(torch.isfinite(p).all().item()) for _, p in res]
+            key = f"{name}{'_noisy' if noisy else ''}"
+            out[key] = {"equal_to_graph": same, "finite": finite}
+            print(key, json.dumps(out[key]), flush=True)
+    print(json.dumps({k: sum(v["equal_to_graph"]) for k, v in out.items()}))
+
+
+if __name__ == "__main__":
+    main()

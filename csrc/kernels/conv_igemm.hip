@@ -147,12 +147,15 @@ bool plan_fwd(int mode, const ConvDesc& d, bool allow_split, FwdPlan* p, bool al
     return e ? atoi(e) : 16;
   }();
   // ... and, at any depth, while the grid would stay under
-  // MDT_CONV_BN_SPLIT_TINY = 64 blocks: the 28x28 decoder Linear and encoder
-  // head backward-data GEMMs (M = 128 rows, 50 blocks of 64x128) spread over
-  // twice the CUs (0.1199 -> 0.1152 ms/step, profiles/r1_defer/bn_tiny)
+  // MDT_CONV_BN_SPLIT_TINY = 512 blocks: the shallow Linear GEMMs (the 28x28
+  // decoder Linear / head backward-data, M = 128: 50 blocks of 64x128; the
+  // 128x128 model's dec_fc forward and head backward-data, M = 64, K <= 128:
+  // 128 blocks) spread over more CUs. 64 -> 512 measured conv128 B=64
+  // 0.3727-0.374 -> 0.3644-0.3645 ms/step, 1024 0.3767 (profiles/r4_tiles);
+  // 28x28 layer path: profiles/r1_defer/bn_tiny
   static const int bn_split_tiny = [] {
     const char* e = getenv("MDT_CONV_BN_SPLIT_TINY");
-    return e ? atoi(e) : 64;
+    return e ? atoi(e) : 512;
   }();
   auto grid64 = [&] { return (long long)q.classes * cdiv(q.M, 64) * cdiv(q.Ncols, q.BN); };
   while (q.BN > 32 && !q.thin &&

@@ -460,11 +460,10 @@ int mdt_job_thin_conv(JobBlob* j, const void* X, int x_is_f32, const float* Wf, 
   memset(j, 0, sizeof(*j));
   const bool ok = d.CO == 16 || d.CO == 32 || d.CO == 64;
   j->kind = ok ? kJobThinConv + d.CO + (x_is_f32 ? 100 : 0) : 0;
-  const int form = thin_conv_form(d, x_is_f32, omask != nullptr, colsum != nullptr);
-  j->nblk = cdivj((long long)d.N * d.OH * d.OW / (form == 2 ? 2 : 1), 256);
+  j->nblk = cdivj((long long)d.N * d.OH * d.OW, 256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
                         colsum, idx, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), B, xb,
-                        j->nblk, form};
+                        j->nblk, thin_conv_mfma_ok(d, x_is_f32)};
   put_args(j, ta);
   return 0;
 }

@@ -49,7 +49,7 @@ struct ThinConvArgs {
   int B;
   float* xb;
   int nblk;
-  int mfma;            // 1: thin_conv_mfma_body (host: thin_conv_mfma_ok), 2: thin_conv2_body (thin_conv_form)
+  int mfma;            // 1: thin_conv_mfma_body (host: thin_conv_mfma_ok)
 };
 
 // Geometry of the MFMA form of thin_conv (the 128x128 model's enc1 and its
@@ -91,36 +91,14 @@ __host__ inline int thin_conv_mfma_ok(const ConvDesc& d, int x_is_f32) {
 template <int CO, int K>
 constexpr int thin_conv_lds_bytes() { return (K * K * CO + 256 * (CO + 1)) * 4; }
 
-// Two-pixel forward form (thin_conv2_body below): stride 2, even output rows,
-// no output mask or column sums, VALU body selected. MDT_THIN_PX2=0 disables.
-// Body selector for ThinConvArgs::mfma; the grid then covers M / 2 threads.
-__host__ inline int thin_conv_form(const ConvDesc& d, int x_is_f32, bool omask, bool colsum) {
-  const int mfma = thin_conv_mfma_ok(d, x_is_f32);
-  static const bool px2_on = [] {
-    const char* e = getenv("MDT_THIN_PX2");
-    return !(e && e[0] == '0');
-  }();
-  if (!mfma && px2_on && !omask && !colsum && d.S == 2 && d.OW % 2 == 0) return 2;
-  return mfma;
-}
-
 template <typename TIN>
 __device__ void thin_conv_mfma_body(const ThinConvArgs& ta, uint8_t* lds, int bid);
-
-template <int CO, int K, typename TIN>
-__device__ __forceinline__ void thin_conv2_body(const ThinConvArgs& ta, uint8_t* lds, int bid);
 
 template <int CO, int K, typename TIN>
 __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* lds, int bid) {
   if constexpr (CO == 32 && K == 4) {
     if (ta.mfma == 1) {
       thin_conv_mfma_body<TIN>(ta, lds, bid);
-      return;
-    }
-  }
-  if constexpr (K == 4) {
-    if (ta.mfma == 2) {
-      thin_conv2_body<CO, K, TIN>(ta, lds, bid);
       return;
     }
   }
@@ -215,94 +193,6 @@ __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* 
       for (int c = 0; c < CO; ++c) acc[c] = 0.f;
     }
     block_colsum<CO>(acc, red, ta.colsum + (size_t)bid * CO);
-  }
-}
-
-// Forward-only form of thin_conv_body (no output mask, no column sums) for
-// stride 2: two horizontally adjacent output pixels per thread. The VALU
-// body issues 16 taps x CO / 4 wave-uniform ds_read_b128 weight reads per
-// pixel, and an LDS broadcast costs as much LDS time as 64 distinct
-// addresses, so it runs LDS-bound (enc1 forward at 128x128, B = 64: 16.9 us,
-// profiles/r3_pmc_end); here each weight read feeds both pixels and the two
-// patches share their middle columns (4 x 6 input loads instead of 2 x 16).
-// Per pixel the arithmetic is the body's own (bias, then one fmaf per tap in
-// tap order), so the output is bitwise the same. Host: thin_conv_form.
-template <int CO, int K, typename TIN>
-__device__ __forceinline__ void thin_conv2_body(const ThinConvArgs& ta, uint8_t* lds, int bid) {
-  constexpr int TAPS = K * K, S = 2, XW = K + S;
-  const ConvDesc& d = ta.d;
-  const TIN* X = reinterpret_cast<const TIN*>(ta.X);
-  float* wl = reinterpret_cast<float*>(lds);
-  const int M2 = (d.N * d.OH * d.OW) >> 1;
-  const int m2 = bid * blockDim.x + threadIdx.x;
-  const bool live = m2 < M2;
-  const int m = 2 * (live ? m2 : 0);  // first of the pair; OW even: both in one row
-  const int n = m / (d.OH * d.OW);
-  const int rem = m - n * d.OH * d.OW;
-  const int oy = rem / d.OW, ox = rem - oy * d.OW;
-  const int iy0 = oy * S - d.P, ix0 = ox * S - d.P;
-  const int* rows = ta.idx ? ta.idx + (size_t)ta.st->cursor * ta.B : nullptr;
-  const TIN* img = X + (size_t)(rows ? rows[n] : n) * d.H * d.W;
-  if (ta.xb) {
-    const int p4 = (d.H * d.W) >> 2;
-    const long long tot = (long long)d.N * p4;
-    for (long long e = (long long)bid * blockDim.x + threadIdx.x; e < tot; e += (long long)ta.nblk * blockDim.x) {
-      const int i = (int)(e / p4), c = (int)(e - (long long)i * p4);
-      reinterpret_cast<float4*>(ta.xb + (size_t)i * d.H * d.W)[c] =
-          reinterpret_cast<const float4*>(X + (size_t)(rows ? rows[i] : i) * d.H * d.W)[c];
-    }
-  }
-  if (ta.hp && bid == 0 && threadIdx.x == 0) {
-    TrainState* st = ta.st;
-    st->step = st->step + 1;
-    st->b1pow *= ta.hp->beta1_d;
-    st->b2pow *= ta.hp->beta2_d;
-  }
-  float xin[K][XW];
-#pragma unroll
-  for (int ty = 0; ty < K; ++ty)
-#pragma unroll
-    for (int tx = 0; tx < XW; ++tx) {
-      const int iy = iy0 + ty, ix = ix0 + tx;
-      const bool ok = live && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-      const float x = ld1(img + (ok ? iy * d.W + ix : 0));
-      xin[ty][tx] = ok ? x : 0.f;
-    }
-  float acc0[CO], acc1[CO];
-#pragma unroll
-  for (int c = 0; c < CO; ++c) acc0[c] = acc1[c] = ta.bias ? ta.bias[c] : 0.f;
-  for (int e = threadIdx.x; e < TAPS * CO; e += blockDim.x) {
-    const int c = e / TAPS, t = e - c * TAPS;
-    wl[t * CO + c] = ta.Wf[e];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int t = 0; t < TAPS; ++t) {
-    const float x0 = xin[t / K][t % K], x1 = xin[t / K][t % K + S];
-#pragma unroll
-    for (int c4 = 0; c4 < CO / 4; ++c4) {
-      const float4 w = *reinterpret_cast<const float4*>(wl + t * CO + 4 * c4);
-      acc0[4 * c4 + 0] = fmaf(x0, w.x, acc0[4 * c4 + 0]);
-      acc1[4 * c4 + 0] = fmaf(x1, w.x, acc1[4 * c4 + 0]);
-      acc0[4 * c4 + 1] = fmaf(x0, w.y, acc0[4 * c4 + 1]);
-      acc1[4 * c4 + 1] = fmaf(x1, w.y, acc1[4 * c4 + 1]);
-      acc0[4 * c4 + 2] = fmaf(x0, w.z, acc0[4 * c4 + 2]);
-      acc1[4 * c4 + 2] = fmaf(x1, w.z, acc1[4 * c4 + 2]);
-      acc0[4 * c4 + 3] = fmaf(x0, w.w, acc0[4 * c4 + 3]);
-      acc1[4 * c4 + 3] = fmaf(x1, w.w, acc1[4 * c4 + 3]);
-    }
-  }
-  if (!live) return;
-#pragma unroll
-  for (int c8 = 0; c8 < CO / 8; ++c8) {
-    bf16x8 o0, o1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      o0[j] = (__bf16)(ta.relu ? fmaxf(acc0[8 * c8 + j], 0.f) : acc0[8 * c8 + j]);
-      o1[j] = (__bf16)(ta.relu ? fmaxf(acc1[8 * c8 + j], 0.f) : acc1[8 * c8 + j]);
-    }
-    *reinterpret_cast<bf16x8*>(ta.y16 + (size_t)m * CO + 8 * c8) = o0;
-    *reinterpret_cast<bf16x8*>(ta.y16 + (size_t)(m + 1) * CO + 8 * c8) = o1;
   }
 }
 

@@ -59,11 +59,10 @@ int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, ConvDesc d, cons
   if (d.C != 1 || d.KH != 4 || d.KW != 4) return 1;
   if ((idx || xb || hp) && (!st || !x_is_f32 || (d.H * d.W) % 4)) return 1;
   const long long M = (long long)d.N * d.OH * d.OW;
-  const int mfma = thin_conv_form(d, x_is_f32, omask != nullptr, colsum != nullptr);
-  dim3 grid(cdiv_t(mfma == 2 ? M / 2 : M, 256)), blk(256);
+  dim3 grid(cdiv_t(M, 256)), blk(256);
   const ThinConvArgs ta{X, Wf, d, bias, relu, reinterpret_cast<__bf16*>(y16), reinterpret_cast<const __bf16*>(omask),
                         colsum, idx, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp), B, xb,
-                        (int)grid.x, mfma};
+                        (int)grid.x, thin_conv_mfma_ok(d, x_is_f32)};
 #define THIN(CO_)                                                                     \
   {                                                                                   \
     if (x_is_f32)                                                                     \

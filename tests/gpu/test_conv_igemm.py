@@ -226,28 +226,6 @@ def test_thin_conv_matches_conv2d(f32_in, H, native_ext):
     assert not bool(bad.any())
 
 
-@pytest.mark.parametrize("H", [28, 128])
-def test_thin_conv_two_pixel_form_is_bitwise(H, native_ext):
-    """The forward call without column sums runs thin_conv2_body (two output
-    pixels per thread, shared weight reads); with column sums the one-pixel
-    body runs. Same per-pixel fmaf sequence: outputs bitwise equal."""
-    C = native_ext
-    N, CO = (5, 32) if H == 28 else (3, 32)
-    torch.manual_seed(5)
-    x = torch.rand(N, H, H, 1, device=DEV)
-    w = torch.randn(CO, 4, 4, 1, device=DEV) / 4
-    b = torch.randn(CO, device=DEV)
-    d = conv_desc(N, H, H, 1, CO, 4, 2, 1)
-    M = N * (H // 2) ** 2
-    y1 = torch.zeros(M * CO, device=DEV, dtype=torch.bfloat16)
-    y2 = torch.full((M * CO,), float("nan"), device=DEV, dtype=torch.bfloat16)
-    cs = torch.zeros(C.thin_blocks(False, d) * CO, device=DEV)
-    C.thin_conv(x, w.flatten(), d, b, True, y1, None, cs)
-    C.thin_conv(x, w.flatten(), d, b, True, y2)
-    torch.cuda.synchronize()
-    assert torch.equal(y1, y2)
-
-
 def test_thin_tconv_fused_bce(native_ext):
     """Last decoder layer (32 -> 1 transposed conv) fused with logit BCE."""
     C = native_ext
