@@ -57,6 +57,20 @@ def _run(tr, X, idx, nb, steps):
     return tr.params.clone(), tr.loss_history()[:steps].copy()
 
 
+def _explain(make_ref, nb, steps, X, idx, p1, h1, p0, h0, layer_ranges):
+    """On a mismatch: which side moves (the reference re-run twice) and in
+    which layers the parameters differ -- printed for the log."""
+    if torch.equal(p1, p0) and (h1 == h0).all():
+        return
+    reruns = [_run(make_ref(), X, idx, nb, steps) for _ in range(2)]
+    same_ref = [bool(torch.equal(p, p0)) for p, _ in reruns]
+    same_fused = [bool(torch.equal(p, p1)) for p, _ in reruns]
+    diff = {l.name: float((p1[b:e] - p0[b:e]).abs().max()) for l, b, e in layer_ranges}
+    first = int(np.argmax(h1 != h0)) if (h1 != h0).any() else -1
+    print(f"MISMATCH first differing loss step {first}; reference re-runs equal to the first reference "
+          f"{same_ref}, equal to the fused run {same_fused}; per-layer max |dp| {diff}", flush=True)
+
+
 @pytest.mark.parametrize("graphs", [False, True])
 @pytest.mark.parametrize("pair", [True, False])
 @pytest.mark.parametrize("overlap", [True, False])
@@ -73,6 +87,7 @@ def test_fused_reducer_one_rank_is_bitwise_reducer_free(native_ext, graphs, pair
     assert int(tr.f28_err.item()) == 0
     assert red.launched_count() == 0  # no stream-side collectives: everything ran as jobs
     assert np.isfinite(h0).all() and tr.read_state()["step"] == steps
+    _explain(lambda: _trainer(dev, graphs, pair, overlap), nb, steps, X, idx, p1, h1, p0, h0, tr.layer_ranges())
     np.testing.assert_array_equal(h1, h0)
     assert torch.equal(p1, p0), (p1 - p0).abs().max().item()
 
@@ -90,6 +105,7 @@ def test_fused_reducer_scaled_reduce_runs_on_every_unit(native_ext, overlap):
     tr.attach_reducer(_fused_reducer(tr, scale=2.0))
     tr.set_hparams(grad_scale=0.5)
     p1, h1 = _run(tr, X, idx, nb, steps)
+    _explain(lambda: _trainer(dev, True, overlap=overlap), nb, steps, X, idx, p1, h1, p0, h0, tr.layer_ranges())
     np.testing.assert_array_equal(h1, h0)
     assert torch.equal(p1, p0), (p1 - p0).abs().max().item()
 
