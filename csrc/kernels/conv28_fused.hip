@@ -7,6 +7,8 @@
 //               resident in time runs the solo body), or grid M solo
 //
 // Bodies: conv28_fused.h (solo), conv28_pair.h (pairs).
+#include <stdlib.h>
+
 #include "conv28_pair.h"
 
 namespace mdt {
@@ -24,6 +26,7 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
 
 __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, PairCtl pc) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[StepLayout::LDS];
+  if (pc.acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (!pc.pair) {
     const int n = blockIdx.x;
     fwd_body<StepLayout>(fa, lds, n);
@@ -196,6 +199,11 @@ int mdt_f28_step(const long long* pf, const long long* pb, const long long* pp, 
   pc.M = M;
   pc.pair = pair ? 1 : 0;
   pc.delay_us = delay_us;
+  static const int acq = [] {
+    const char* e = getenv("MDT_F28_ACQ");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  pc.acquire = acq;
   if (pair) {
     if (!pp || !pp[0] || !pp[1] || !pp[2]) return 2;
     pc.xg = P<unsigned long long>(pp, 0);

@@ -53,6 +53,7 @@ struct PairCtl {
   int delay_us;            // tests: > 0 workgroups >= M wait this long before their ticket (forces solo);
                            //        < 0 sample 0's role-1 half stalls -delay_us after pairing (forces a
                            //        sweep timeout of its partner: `err` bit 0)
+  int acquire;             // diagnostic (MDT_F28_ACQ=1): agent-scope acquire fence at kernel entry
 };
 
 // granule offsets inside one (sample, role) slab

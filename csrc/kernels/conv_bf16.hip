@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // Conv-VAE step kernels around the implicit-GEMM layers (conv_igemm.hip):
 // batch gather, reparameterisation (+KLD) and its backward, logit-form BCE
 // (+dlogits, +bias-gradient partials), loss ring update, and the optimizer
@@ -151,10 +152,14 @@ __global__ void __launch_bounds__(256) adam_cast_k(float* P, const float* G, flo
   }
 }
 
+template <bool FENCE>
 __global__ void __launch_bounds__(kFinalizeThreads) grad_finalize_k(FinalizeArgs fa) {
   __shared__ float red[kFinalizeThreads];
   __shared__ AdamC cs;
   grad_finalize_body(fa, red, &cs, blockIdx.x);
+  // diagnostic (MDT_FIN_FENCE=1): an explicit agent-scope release of the
+  // parameter / bf16 stores before the kernel-end release
+  if constexpr (FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
 __global__ void __launch_bounds__(256) wtrans_k(WtransArgs wa) {
@@ -247,7 +252,14 @@ int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, const
   const FinalizeArgs fa{P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16), reinterpret_cast<const GradSeg*>(segs),
                         reinterpret_cast<const GradUnit*>(units), reinterpret_cast<const TrainState*>(st),
                         reinterpret_cast<const HParams*>(hp), do_adam};
-  hipLaunchKernelGGL(grad_finalize_k, dim3(nunits), dim3(kFinalizeThreads), 0, s, fa);
+  static const bool fence = [] {
+    const char* e = getenv("MDT_FIN_FENCE");
+    return e && e[0] == '1';
+  }();
+  if (fence)
+    hipLaunchKernelGGL(grad_finalize_k<true>, dim3(nunits), dim3(kFinalizeThreads), 0, s, fa);
+  else
+    hipLaunchKernelGGL(grad_finalize_k<false>, dim3(nunits), dim3(kFinalizeThreads), 0, s, fa);
   return (int)hipGetLastError();
 }
 
