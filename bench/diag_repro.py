@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--skip1", action="store_true")
     ap.add_argument("--skip2", action="store_true")
     ap.add_argument("--gc", action="store_true", help="gc.collect() after each replayed test")
+    ap.add_argument("--parts", default="rfRF", help="r/f: test 1 reference / fused run, R/F: test 2's")
+    ap.add_argument("--sync-steps", action="store_true", help="a): device sync after every step")
     a = ap.parse_args()
     from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
 
@@ -48,25 +50,39 @@ def main():
         torch.cuda.synchronize()
         return tr.params.clone(), tr.loss_history()[:steps].copy()
 
-    def replay_test(graphs, pair, overlap):
+    def replay_test(graphs, pair, overlap, do_ref, do_fused):
         X, idx = data()
-        p0, h0 = run(trainer(graphs, pair, overlap), X, idx)
-        tr = trainer(graphs, pair, overlap)
-        red = tr.C.XgmiP2PReducer(0, 1, tr.grads, tr.default_bucket_bounds(), True, 0.0, 64, 20.0, -1, True)
-        tr.attach_reducer(red)
-        p1, h1 = run(tr, X, idx)
-        print(f"replayed test graphs={graphs} pair={pair}: equal={bool(torch.equal(p0, p1))}", flush=True)
+        if do_ref:
+            run(trainer(graphs, pair, overlap), X, idx)
+        if do_fused:
+            tr = trainer(graphs, pair, overlap)
+            red = tr.C.XgmiP2PReducer(0, 1, tr.grads, tr.default_bucket_bounds(), True, 0.0, 64, 20.0, -1, True)
+            tr.attach_reducer(red)
+            run(tr, X, idx)
+        print(f"replayed test graphs={graphs} pair={pair} ref={do_ref} fused={do_fused}", flush=True)
 
     if not a.skip1:
-        replay_test(False, True, True)
+        replay_test(False, True, True, "r" in a.parts, "f" in a.parts)
         if a.gc:
             gc.collect()
     if not a.skip2:
-        replay_test(True, True, True)
+        replay_test(True, True, True, "R" in a.parts, "F" in a.parts)
         if a.gc:
             gc.collect()
     X, idx = data()
-    res = [run(trainer(False, False, True), X, idx) for _ in range(3)]
+
+    def run_a():
+        tr = trainer(False, False, True)
+        if not a.sync_steps:
+            return run(tr, X, idx)
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, nb)
+        for _ in range(steps):
+            tr.train_steps(1)
+            torch.cuda.synchronize()
+        return tr.params.clone(), tr.loss_history()[:steps].copy()
+
+    res = [run_a() for _ in range(3)]
     eq = [bool(torch.equal(p, res[0][0])) for p, _ in res[1:]]
     print("a) reference re-runs equal to the first:", eq, flush=True)
 
