@@ -47,17 +47,30 @@ def main():
                   "w16t": tr.w16t, "state": tr.state.train_state})
         return b
 
-    def one_step_snapshot():
-        tr, _ = trainer()
-        tr.train_steps(1)
-        torch.cuda.synchronize()
-        snap = {k: v.clone() for k, v in bufs(tr).items()}
-        addrs = {k: (v.data_ptr(), v.numel() * v.element_size()) for k, v in bufs(tr).items()}
-        return snap, addrs
+    STEPS = 8
 
-    clean, _ = one_step_snapshot()
-    clean2, _ = one_step_snapshot()
-    print("clean vs clean:", [k for k in clean if not torch.equal(clean[k], clean2[k])], flush=True)
+    def snapshots():
+        """Per-step buffer snapshots of one fresh reducer-free solo trainer
+        (device copies only: no host sync between the steps)."""
+        tr, _ = trainer()
+        out = []
+        for _ in range(STEPS):
+            tr.train_steps(1)
+            out.append({k: v.clone() for k, v in bufs(tr).items()})
+        torch.cuda.synchronize()
+        addrs = {k: (v.data_ptr(), v.numel() * v.element_size()) for k, v in bufs(tr).items()}
+        return out, addrs
+
+    def first_diff(a, b):
+        for s in range(STEPS):
+            d = [k for k in a[s] if not torch.equal(a[s][k], b[s][k])]
+            if d:
+                return s, d
+        return None, []
+
+    clean, _ = snapshots()
+    clean2, _ = snapshots()
+    print("clean vs clean:", first_diff(clean, clean2), flush=True)
 
     tr, red = trainer(graphs=True, pair=True, fused=True)
     tr.train_steps(8)
@@ -67,11 +80,12 @@ def main():
     del tr, red
     gc.collect()
 
-    for r in range(3):
-        snap, addrs = one_step_snapshot()
-        diff = [k for k in clean if not torch.equal(clean[k], snap[k])]
+    for r in range(4):
+        snap, addrs = snapshots()
+        s, diff = first_diff(clean, snap)
         inside = [k for k, (a, n) in addrs.items() if a < base + nbytes and a + n > base]
-        print(json.dumps({"run": r, "differ_after_step0": diff, "buffers_in_freed_uc_range": inside}), flush=True)
+        print(json.dumps({"run": r, "first_differing_step": s, "differ": diff, "buffers_in_freed_uc_range": inside}),
+              flush=True)
 
 
 if __name__ == "__main__":
