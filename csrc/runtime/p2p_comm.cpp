@@ -32,11 +32,49 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "kernels/p2p_allreduce.h"
 #include "runtime/stream_buckets.h"
 
 namespace mdt {
+
+// Process-lifetime pool of the uncached regions. A freed region is kept for
+// the next reducer of the same device and size instead of going back to the
+// runtime: otherwise its address range -- still mapped uncached -- was handed
+// out again to torch's caching allocator, and later trainers' activations and
+// partial slabs landed in it (bench/diag_uc_reuse.py); the reducer-free 28x28
+// step then stopped being run-to-run bitwise in the processes where that
+// happened (profiles/r4_determinism). Regions are reused only at exactly the
+// requested size; production keeps one reducer per trial for the whole run.
+class UncachedPool {
+ public:
+  static void* take(int dev, size_t bytes) {
+    std::lock_guard<std::mutex> g(mu());
+    auto& m = free_list();
+    auto it = m.find({dev, bytes});
+    if (it == m.end()) return nullptr;
+    void* p = it->second;
+    m.erase(it);
+    return p;
+  }
+  static void give(int dev, size_t bytes, void* p) {
+    std::lock_guard<std::mutex> g(mu());
+    free_list().emplace(std::make_pair(dev, bytes), p);
+  }
+
+ private:
+  static std::mutex& mu() {
+    static std::mutex m;
+    return m;
+  }
+  static std::multimap<std::pair<int, size_t>, void*>& free_list() {
+    static auto* m = new std::multimap<std::pair<int, size_t>, void*>();  // never destroyed: outlives every reducer
+    return *m;
+  }
+};
 
 class XgmiP2PReducer : public StreamBuckets {
  public:
@@ -82,7 +120,8 @@ class XgmiP2PReducer : public StreamBuckets {
       bytes_ = fep_byte_ + al(2LL * n * 4);
     }
     DeviceGuard dg(device_);
-    MDT_HIP_CHECK(hipExtMallocWithFlags(&base_, (size_t)bytes_, hipDeviceMallocUncached));
+    base_ = UncachedPool::take(device_, (size_t)bytes_);
+    if (!base_) MDT_HIP_CHECK(hipExtMallocWithFlags(&base_, (size_t)bytes_, hipDeviceMallocUncached));
     MDT_HIP_CHECK(hipMemset((char*)base_ + flags_byte_, 0, (size_t)(bytes_ - flags_byte_)));
     MDT_HIP_CHECK(hipDeviceSynchronize());
     for (int p = 0; p < kP2PMaxRanks; ++p) peer_base_[p] = nullptr;
@@ -95,7 +134,7 @@ class XgmiP2PReducer : public StreamBuckets {
     if (ctx_) (void)hipFree(ctx_);
     for (int p = 0; p < s_; ++p)
       if (p != me_ && peer_base_[p] && opened_[p]) (void)hipIpcCloseMemHandle(peer_base_[p]);
-    if (base_) (void)hipFree(base_);
+    if (base_) UncachedPool::give(device_, (size_t)bytes_, base_);
   }
 
   // 64-byte hipIpcMemHandle_t of this rank's region (uint8 CPU tensor)
