@@ -146,10 +146,10 @@ def test_autotune_comm_times_rccl_and_p2p(nccl_world, native_ext, tmp_path):
     make = lambda: MlpVaeTrainer(batch_size=128, device=dev, backend="hip", seed=3, use_graphs=True, graph_steps=4)
     bounds, kind, timings = autotune_comm(make, nccl_world, X, idx, candidates=(None, 0), steps=4, warmup=2,
                                           key="gpu-test", cache=str(tmp_path / "b.json"))
-    assert kind in ("rccl", "p2p1")
-    assert any(k.startswith("p2p1:") for k in timings) and any(k.startswith("rccl:") for k in timings)
+    assert kind in ("rccl", "p2p1", "xgmi")
+    assert all(any(k.startswith(c + ":") for k in timings) for c in ("rccl", "p2p1", "xgmi"))
     hist = []
-    for k in ("rccl", "p2p"):
+    for k in ("rccl", "p2p", "xgmi"):
         tr = make()
         tr.attach_reducer(make_arena_reducer(nccl_world, tr.grads, bounds, kind=k))
         tr.bind_train_data(X, idx)
@@ -158,3 +158,4 @@ def test_autotune_comm_times_rccl_and_p2p(nccl_world, native_ext, tmp_path):
         torch.cuda.synchronize()
         hist.append(tr.loss_history()[:8].copy())
     np.testing.assert_array_equal(hist[0], hist[1])
+    np.testing.assert_array_equal(hist[0], hist[2])
