@@ -178,14 +178,34 @@ __device__ __forceinline__ void thin_conv_body(const ThinConvArgs& ta, uint8_t* 
       for (int j = 0; j < 8; ++j) acc[8 * c8 + j] = (float)mk[j] > 0.f ? acc[8 * c8 + j] : 0.f;
     }
   }
-  if (live) {
+  {
+    // The block's 256 output rows are one contiguous NHWC range: staged in
+    // LDS (the colsum transpose area, free until block_colsum) and written as
+    // consecutive 16-B chunks, so a wave store covers 1 KB of whole lines.
+    // Stored straight from registers, lane l's 16-B chunk c sat 2 CO bytes
+    // from lane l + 1's: each store instruction touched 64 separate pieces of
+    // 4 KB and the enc1 forward (16.6 us, 20.5 MB written at 1.4 TB/s,
+    // profiles/r4_pmc_conv128) was bound by it. Slots are XOR-swizzled by the
+    // pixel so neither side of the hand-off piles onto one bank group.
+    constexpr int NCH = CO / 8;
+    bf16x8* stage = reinterpret_cast<bf16x8*>(red);
+    const int t = threadIdx.x;
 #pragma unroll
-    for (int c8 = 0; c8 < CO / 8; ++c8) {
+    for (int c8 = 0; c8 < NCH; ++c8) {
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (__bf16)acc[8 * c8 + j];
-      *reinterpret_cast<bf16x8*>(ta.y16 + (size_t)m * CO + 8 * c8) = o;
+      stage[t * NCH + (c8 ^ (t & (NCH - 1)))] = o;
     }
+    __syncthreads();
+    const long long m0 = (long long)bid * blockDim.x;
+    const int npx = (int)(M - m0 < (long long)blockDim.x ? M - m0 : (long long)blockDim.x);
+    bf16x8* dst = reinterpret_cast<bf16x8*>(ta.y16 + (size_t)m0 * CO);
+    for (int i = t; i < npx * NCH; i += blockDim.x) {
+      const int px = i / NCH, c = i - px * NCH;
+      dst[i] = stage[px * NCH + (c ^ (px & (NCH - 1)))];
+    }
+    if (ta.colsum) __syncthreads();  // block_colsum reuses the staging area
   }
   if (ta.colsum) {
     if (!live) {
