@@ -462,10 +462,10 @@ struct WtransArgs {
   const TrUnit* units;
 };
 
-constexpr int kWtransLds = 64 * 66 * 2;
+constexpr int kWtransPitch = 72;                 // 16-B form: row pitch in bf16 (16-B aligned rows)
+constexpr int kWtransLds = 64 * kWtransPitch * 2;  // >= the scalar form's 64 x 66
 
 __device__ __forceinline__ void wtrans_body(const WtransArgs& wa, uint8_t* lds, int bid) {
-  unsigned short (*tile)[66] = reinterpret_cast<unsigned short (*)[66]>(lds);
   const TrUnit u = wa.units[bid];
   const GradSeg sg = wa.segs[u.seg];
   const int k = sg.k, s = sg.s, CI = sg.ci, CO = sg.co, T = k / s;
@@ -473,6 +473,35 @@ __device__ __forceinline__ void wtrans_body(const WtransArgs& wa, uint8_t* lds, 
   const int a = ky % s, ty = ky / s, b = kx % s, tx = kx / s;
   const unsigned short* src = reinterpret_cast<const unsigned short*>(wa.w16) + sg.off;
   unsigned short* dst = reinterpret_cast<unsigned short*>(wa.w16t) + sg.toff;
+  if (CI % 8 == 0 && CO % 8 == 0 && sg.off % 8 == 0 && sg.toff % 8 == 0) {
+    // 16-B form: 8 channels per global access on both sides (the 2-B form
+    // below issued 32 global instructions per thread; 13.4 us for the
+    // 128x128 model's 3 M weights, profiles/r4_pmc_conv128). Chunk q of tile
+    // row r sits at slot q ^ (r >> 3), so the column reads of the transposed
+    // side spread over 8 bank groups.
+    typedef unsigned short us8 __attribute__((ext_vector_type(8)));
+    unsigned short (*tile)[kWtransPitch] = reinterpret_cast<unsigned short (*)[kWtransPitch]>(lds);
+    for (int ch = threadIdx.x; ch < 64 * 8; ch += blockDim.x) {
+      const int r = ch >> 3, q = ch & 7;  // tile row = co, chunk = 8 ci
+      const int co = u.co0 + r, ci = u.ci0 + 8 * q;
+      if (co < CO && ci < CI)
+        *reinterpret_cast<us8*>(&tile[r][8 * (q ^ (r >> 3))]) =
+            *reinterpret_cast<const us8*>(src + ((long long)(co * k + ky) * k + kx) * CI + ci);
+    }
+    __syncthreads();
+    for (int ch = threadIdx.x; ch < 64 * 8; ch += blockDim.x) {
+      const int r = ch >> 3, q = ch & 7;  // output row = ci, chunk = 8 co
+      const int ci = u.ci0 + r, co = u.co0 + 8 * q;
+      if (co < CO && ci < CI) {
+        us8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = tile[8 * q + j][8 * ((r >> 3) ^ q) + (r & 7)];
+        *reinterpret_cast<us8*>(dst + ((((long long)(a * s + b) * CI + ci) * T + ty) * T + tx) * CO + co) = v;
+      }
+    }
+    return;
+  }
+  unsigned short (*tile)[66] = reinterpret_cast<unsigned short (*)[66]>(lds);
   for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
     const int r = idx >> 6, c = idx & 63;
     const int co = u.co0 + r, ci = u.ci0 + c;

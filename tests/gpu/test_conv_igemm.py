@@ -251,3 +251,26 @@ def test_thin_tconv_fused_bce(native_ext):
     assert abs(float(part.sum()) - float(bce)) / float(bce) < 1e-4
     assert _rel(dlog.float().view(N, -1), p - x) < 1e-2
     assert abs(float(gpart.sum()) - float((p - x).sum())) < 1e-2 * float((p - x).abs().sum())
+
+
+@pytest.mark.parametrize("image", [28, 128])
+def test_weight_transposes_match_parity_transpose(image, native_ext):
+    """w16t (the transposed bf16 weight copies the backward-data GEMMs read)
+    equals ops.conv_layout.parity_transpose of every layer's bf16 weights:
+    the 16-B form of wtrans_body for channel counts divisible by 8, the 2-B
+    form for the single-channel layers."""
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer, _w_shape
+    from multidisttorch_amd.ops.conv_layout import parity_transpose
+
+    tr = ConvVaeTrainer(batch_size=8, image=image, z=32 if image == 28 else 64, device=DEV, backend="hip", seed=1)
+    tr.params.copy_(torch.randn(tr.params.shape, generator=torch.Generator().manual_seed(7)).to(DEV))
+    tr._cast_weights()
+    torch.cuda.synchronize()
+    checked = 0
+    for l in tr.spec:
+        w = tr._w(l).view(*_w_shape(l))
+        got = tr._wt(l)
+        ref = parity_transpose(w, l.s)
+        assert torch.equal(got, ref), l.name
+        checked += 1
+    assert checked == len(tr.spec)
