@@ -324,9 +324,6 @@ __device__ __forceinline__ f32x4 slab_sum4(const float* p, long long n, int nspl
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
   f32x4 a0 = z, a1 = z, a2 = z, a3 = z;
   int s = 0;
-  // unrolled: the loads of several groups of four are in flight together
-  // (each accumulator still adds its slabs in order: bitwise unchanged)
-#pragma unroll 4
   for (; s + 3 < nsplit; s += 4) {
     a0 += *reinterpret_cast<const f32x4*>(p + (long long)s * n);
     a1 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 1) * n);
@@ -340,7 +337,6 @@ __device__ __forceinline__ f32x4 slab_sum4(const float* p, long long n, int nspl
 __device__ __forceinline__ float slab_sum1(const float* p, long long n, int nsplit) {
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int s = 0;
-#pragma unroll 4
   for (; s + 3 < nsplit; s += 4) {
     a0 += p[(long long)s * n];
     a1 += p[(long long)(s + 1) * n];
@@ -354,7 +350,6 @@ __device__ __forceinline__ float slab_sum1(const float* p, long long n, int nspl
 __device__ __forceinline__ float slab_partial(const float* p, long long n, int nsplit, int rl, int rp) {
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int s = rl;
-#pragma unroll 4
   for (; s + 3 * rp < nsplit; s += 4 * rp) {
     a0 += p[(long long)s * n];
     a1 += p[(long long)(s + rp) * n];
@@ -379,13 +374,6 @@ __device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const 
   const long long o = sg.off + e0;
   const long long n = sg.numel;
   if (left >= 4) {
-    // Adam state first: its loads share the round trip of the slab loads
-    f32x4 p, m, v;
-    if (a.do_adam) {
-      p = *reinterpret_cast<const f32x4*>(a.P + o);
-      m = *reinterpret_cast<const f32x4*>(a.Mo + o);
-      v = *reinterpret_cast<const f32x4*>(a.Vo + o);
-    }
     f32x4 g;
     if (sg.slab) {
       g = slab_sum4(sg.slab + e0, n, sg.nsplit);
@@ -394,6 +382,9 @@ __device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const 
       g = *reinterpret_cast<const f32x4*>(a.G + o);
     }
     if (a.do_adam) {
+      f32x4 p = *reinterpret_cast<const f32x4*>(a.P + o);
+      f32x4 m = *reinterpret_cast<const f32x4*>(a.Mo + o);
+      f32x4 v = *reinterpret_cast<const f32x4*>(a.Vo + o);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float pj = p[j], mj = m[j], vj = v[j];
