@@ -413,7 +413,7 @@ __device__ __forceinline__ void fwd_p01(const FwdArgs& a, uint8_t* lds, int n, A
     // XCD's L2 now, through LDS-DMA loads into a scratch LDS zone (nothing
     // reads it). The builtin (not asm) keeps them in the compiler's vmcnt
     // accounting, so no wait above includes them.
-    {
+    if (a.pf_slices > 0) {
       constexpr int kWh = kFlat * 64 * 2, kWd = kFlat * 32 * 2;
       const int nsl = a.pf_slices, kSlice = (kWh + kWd) / nsl;
       const int r = (int)(blockIdx.x >> 3) % nsl;
