@@ -165,3 +165,37 @@ def test_p2p_multiprocess_ipc(s, kind):
         assert r["bitwise_one_shot"], r
         assert r["same"], r
         assert max(r["errs"] + r["gerrs"]) < 1e-5, r
+
+
+def test_uncached_region_is_pooled_not_freed(native_ext):
+    """A freed reducer's uncached region goes to the process pool (its
+    address range is never handed to torch's caching allocator, see
+    profiles/r4_determinism) and the next reducer of the same size gets it
+    back with its flags / epochs zeroed, so it all-reduces correctly."""
+    import gc
+
+    C = native_ext
+    dev = torch.device("cuda", 0)
+    n, bounds = 5000, [0, 2000, 5000]
+    f = torch.zeros(n, device=dev)
+    red = C.XgmiP2PReducer(0, 1, f, bounds, True, 2.0, 64, 5.0, -1, True)
+    base, nbytes = red.local_base(), red.region_bytes()
+    f.fill_(1.0)
+    red.launch_all()
+    red.wait_all()
+    torch.cuda.synchronize()
+    assert torch.equal(f, torch.full_like(f, 2.0)) and int(red.status()) == 0
+    del red
+    gc.collect()
+    # allocations after the free never land in the pooled region
+    junk = [torch.empty(1 << 18, device=dev) for _ in range(64)]
+    for t in junk:
+        a = t.data_ptr()
+        assert not (a < base + nbytes and a + t.numel() * 4 > base)
+    red2 = C.XgmiP2PReducer(0, 1, f, bounds, True, 2.0, 64, 5.0, -1, True)
+    assert red2.local_base() == base
+    f.fill_(3.0)
+    red2.launch_all()
+    red2.wait_all()
+    torch.cuda.synchronize()
+    assert torch.equal(f, torch.full_like(f, 6.0)) and int(red2.status()) == 0
