@@ -32,6 +32,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstring>
+#include <iterator>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -54,8 +55,9 @@ class UncachedPool {
   static void* take(int dev, size_t bytes) {
     std::lock_guard<std::mutex> g(mu());
     auto& m = free_list();
-    auto it = m.find({dev, bytes});
-    if (it == m.end()) return nullptr;
+    auto range = m.equal_range({dev, bytes});
+    if (range.first == range.second) return nullptr;
+    auto it = std::prev(range.second);  // the most recently freed region of that size
     void* p = it->second;
     m.erase(it);
     return p;
