@@ -211,11 +211,11 @@ int mdt_f28_step(const long long* pf, const long long* pb, const long long* pp, 
     pc.err = P<unsigned>(pp, 2);
     fa.pf_slices = 32;
   }
-  static const int pf = [] {  // A/B: MDT_F28_PF = L2-prefetch slices per XCD (0 = no prefetch)
+  static const int pf_env = [] {  // A/B: MDT_F28_PF = L2-prefetch slices per XCD (0 = no prefetch)
     const char* e = getenv("MDT_F28_PF");
     return e ? atoi(e) : -1;
   }();
-  if (pf >= 0) fa.pf_slices = pf;
+  if (pf_env >= 0) fa.pf_slices = pf_env;
   hipLaunchKernelGGL(f28::f28_step_k, dim3(pair ? 2 * M : M), dim3(f28::kThreads), 0, s, fa, ba, pc);
   return (int)hipGetLastError();
 }
