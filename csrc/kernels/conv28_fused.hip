@@ -209,7 +209,10 @@ int mdt_f28_step(const long long* pf, const long long* pb, const long long* pp, 
     pc.xg = P<unsigned long long>(pp, 0);
     pc.pairw = P<int>(pp, 1);
     pc.err = P<unsigned>(pp, 2);
-    fa.pf_slices = 32;
+    // no P0 L2 prefetch in the paired form: measured 0.0636-0.0639 vs
+    // 0.0638-0.0644 ms/step on the driver command with 32 slices, 200/20
+    // 0.0608-0.0613 vs 0.0616-0.0622 (profiles/r4_end, gpurun_out r4af/r4ag)
+    fa.pf_slices = 0;
   }
   static const int pf_env = [] {  // A/B: MDT_F28_PF = L2-prefetch slices per XCD (0 = no prefetch)
     const char* e = getenv("MDT_F28_PF");
