@@ -234,8 +234,11 @@ class ConvVaeTrainer:
         # neutral at 28x28 with the transposes in the tail (the tail shrinks,
         # the hosting launches grow by as much) and 0.7 % slower at 128x128
         # (profiles/r1_tail); with the transposes deferred (below) 1 % faster
-        # at 28x28 (0.1208 -> 0.1196 ms, profiles/r1_defer): on up to 64x64
-        self.spread_fin = os.getenv("MDT_CONV_SPREAD_FIN", "1" if image <= 64 else "0") == "1"
+        # at 28x28 (0.1208 -> 0.1196 ms, profiles/r1_defer). Round 4 (16-B
+        # transposes, 64x32 shallow-Linear tiles) re-measured 128x128 B=64:
+        # 0.3572-0.3585 spread vs 0.3595-0.3608 ms tail (profiles/r4_tiles):
+        # on at every size now
+        self.spread_fin = os.getenv("MDT_CONV_SPREAD_FIN", "1") == "1"
         # two-launch tail without the transposes (MDT_CONV_DEFER_WT=1|2, no
         # ticket, no fences): the tail's second launch is the first layer's
         # finalize alone, and the transposed weight copies ride in the next
