@@ -135,6 +135,8 @@ def main(argv=None):
             if base and c.get("value"):
                 c["efficiency"] = round(c["value"] / (c["n_gpus"] * base), 4)
         results["scaling"] = curve
+    if os.path.dirname(a.out):
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(results, f, indent=1)
     print("wrote", a.out)
