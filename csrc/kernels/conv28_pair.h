@@ -96,9 +96,6 @@ using g32i = __attribute__((address_space(1))) int;
 // the stamps, results bitwise run to run (tests/gpu/test_conv28_fused.py,
 // bench/diag_determinism.py). MDT_HIP_EXTRA_FLAGS=-DMDT_F28_NEAR_WG=0 builds
 // the agent-scope form.
-#ifndef MDT_F28_DEFER_A2  // 1: P2's global copy of enc2's output written from LDS after P3's loads issue
-#define MDT_F28_DEFER_A2 1
-#endif
 #ifndef MDT_F28_NEAR_WG  // 0: agent scope on the near path too (A/B build, profiles/r4_near_scope)
 #define MDT_F28_NEAR_WG 1
 #endif
@@ -380,9 +377,7 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
                  [&](int, int col) { return Bias[kB2 + col]; }, [&](int p, int col, float v, float bias) {
     const __bf16 o = (__bf16)fmaxf(v + bias, 0.f);
     A2s[p * 64 + col] = o;
-#if !MDT_F28_DEFER_A2
     if (train) a2p[p * 64 + col] = o;
-#endif
   });
   lds_barrier();
 
@@ -404,16 +399,6 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
     ld_rows(1, wr[1]);
     ld_rows(2, wr[2]);
     ld_rows(3, wr[3]);
-#if MDT_F28_DEFER_A2
-    // enc2's output rows for the weight-gradient launch leave here, as 16-B
-    // copies out of A2s issued AFTER P3's weight loads: vmcnt counts stores
-    // too, so stores issued before those loads (P2's per-element epilogue
-    // stores did) are waited for with them
-    if (train && tid < 8 * (p1 - p0)) {
-      const int e = 64 * p0 + 8 * tid;
-      *reinterpret_cast<bf16x8*>(a2p + e) = *reinterpret_cast<const bf16x8*>(A2s + e);
-    }
-#endif
     float d[8];
 #pragma unroll
     for (int c2 = 0; c2 < 4; ++c2)
