@@ -464,3 +464,32 @@ def test_f28_no_uninitialised_lds_reads(pair, native_ext):
     for h, p in res[1:]:
         np.testing.assert_array_equal(h, res[0][0])
         assert torch.equal(p, res[0][1])
+
+
+def test_f28_near_path_is_exercised_and_bitwise(native_ext):
+    """Same-XCD pairs hand off through workgroup-scope granule stores
+    (conv28_pair.h `near`, profiles/r4_near_scope): the phase stamps' slot 15
+    must show such pairs, and the paired result must still be bitwise the
+    solo one, which has no hand-offs at all."""
+    dev = torch.device("cuda")
+    X = torch.rand(4 * 128, 784, generator=torch.Generator().manual_seed(6)).to(dev)
+    idx = torch.arange(4 * 128, device=dev, dtype=torch.int32)
+    res = {}
+    for pair in (True, False):
+        tr = _trainer(seed=5, use_graphs=False)
+        tr.f28_pair = pair
+        stamps = torch.zeros(2 * 128 * 16, dtype=torch.int64, device=dev)
+        tr.f28_stamps = (stamps, None)
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, 4)
+        near = 0
+        for _ in range(4):
+            tr.train_steps(1)
+            if pair:
+                s = stamps.view(256, 16)[:, 15].cpu()
+                near += int(((s >> 4) & 1).sum())
+        torch.cuda.synchronize()
+        res[pair] = (tr.loss_history()[:4].copy(), tr.params.clone(), near)
+    assert res[True][2] > 0, "no same-XCD pair took the near hand-off"
+    np.testing.assert_array_equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])
