@@ -24,25 +24,14 @@ __global__ void __launch_bounds__(kThreads) f28_bwd_k(BwdArgs a) {
   bwd_body<BwdLayout, false>(a, lds, blockIdx.x);
 }
 
-// The one-workgroup body after P0/P1 (solo launches and the paired launch's
-// solo fallback), kept OUT of line: inlined, its ~60 argument pointers
-// competed with the paired body for SGPRs and the whole kernel spilled 91
-// SGPRs into VGPR lanes (1 k v_readlane reloads); the paired body alone
-// spills 8.
-__device__ __attribute__((noinline)) void solo_tail(const FwdArgs& fa, const BwdArgs& ba, uint8_t* lds, int n) {
-  fwd_rest<StepLayout>(fa, lds, n);
-  lds_barrier();
-  bwd_body<StepLayout, true>(ba, lds, n);
-}
-
 __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, PairCtl pc) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[StepLayout::LDS];
   if (pc.acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (!pc.pair) {
     const int n = blockIdx.x;
-    fwd_p01<StepLayout>(fa, lds, n, [] {});
+    fwd_body<StepLayout>(fa, lds, n);
     lds_barrier();
-    solo_tail(fa, ba, lds, n);
+    bwd_body<StepLayout, true>(ba, lds, n);
     return;
   }
   // pairing (see conv28_pair.h): ticket at entry, the leader's solo claim
@@ -80,7 +69,9 @@ __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, P
   const int mode = __builtin_amdgcn_readfirstlane(*mode_w);
   if (mode == kModeExit) return;
   if (mode == kModeSolo) {
-    solo_tail(fa, ba, lds, n);
+    fwd_rest<StepLayout>(fa, lds, n);
+    lds_barrier();
+    bwd_body<StepLayout, true>(ba, lds, n);
     return;
   }
   if (pc.delay_us < 0 && mode == kModeRole1 && n == 0) {  // tests: a paired half that stalls (sweep timeout)
