@@ -69,20 +69,9 @@ __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, P
   const int mode = __builtin_amdgcn_readfirstlane(*mode_w);
   if (mode == kModeExit) return;
   if (mode == kModeSolo) {
-    // The fallback re-reads its arguments from the kernarg segment through a
-    // pointer the compiler cannot see through, so the ~60 pointers of
-    // FwdArgs/BwdArgs are not kept live in SGPRs across the paired body
-    // (which takes them from the LDS table): inline use spilled 91 SGPRs
-    // into VGPR lanes for the whole kernel.
-    const __attribute__((address_space(4))) uint8_t* kp =
-        (const __attribute__((address_space(4))) uint8_t*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(kp));
-    constexpr size_t kBa = (sizeof(FwdArgs) + alignof(BwdArgs) - 1) / alignof(BwdArgs) * alignof(BwdArgs);
-    const FwdArgs fa2 = *reinterpret_cast<const __attribute__((address_space(4))) FwdArgs*>(kp);
-    const BwdArgs ba2 = *reinterpret_cast<const __attribute__((address_space(4))) BwdArgs*>(kp + kBa);
-    fwd_rest<StepLayout>(fa2, lds, n);
+    fwd_rest<StepLayout>(fa, lds, n);
     lds_barrier();
-    bwd_body<StepLayout, true>(ba2, lds, n);
+    bwd_body<StepLayout, true>(ba, lds, n);
     return;
   }
   if (pc.delay_us < 0 && mode == kModeRole1 && n == 0) {  // tests: a paired half that stalls (sweep timeout)
