@@ -161,7 +161,8 @@ def main(argv=None):
                 dist.broadcast(trainer.params, src=dist.get_global_rank(pg, 0), group=pg)
                 trainer.refresh_weights()
                 mb = None if a.bucket_mb in (None, "") else float(a.bucket_mb)
-                trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, trainer.bucket_bounds(mb)))
+                trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, trainer.bucket_bounds(mb),
+                                                          comm_jobs=getattr(trainer, "comm_jobs", False)))
             # reference sampler replicas W // group size (vae-hpo.py:146); packing: one shard per trial
             idx = shard_indices(len(train), (world // n_per) * T, tid)
             trainer.bind_train_data(train.data, idx)

@@ -33,24 +33,33 @@
 // to finalize + scale + Adam: the same step structure with nothing to move,
 // which is how its cost is measured on a one-GPU box.
 //
-// Memory: the receive region, flags and epochs live in ONE uncached device
+// Memory: the receive region and flags live in ONE uncached device
 // allocation per rank (hipDeviceMallocUncached; exported with hipIpc by
 // XgmiP2PReducer, csrc/runtime/p2p_comm.cpp), indexed by ARENA OFFSET, so any
 // unit decomposition works without re-sizing the shared region:
 //   recv  [2 parity][s src][numel] f32      flags [s src][numel] u32
-//   epochs: push [numel] u32, reduce [numel] u32 (only the entry at a unit's
-//           first element is used; local, never read by peers)
-// Epochs advance once per step and unit (device counters, so graph replays and
-// the capture-time eager step stay consistent); parity double-buffers the
-// receive slots: a peer can run at most one step ahead (its next push of a
-// unit needs this rank's next push of the same unit, which follows this rank's
-// reduce of it on the same stream).
+//   (a flag is stored at its unit's first element only)
+// Epoch: ONE per step for every unit, e = TrainState.step + ep_base. Every job
+// of a step runs after the launch that advanced `step` (f28: the loss/step job
+// of the first job launch; layer path: the forward's first launch), so all
+// units of a step -- whatever the batch size M made of the unit
+// decomposition -- agree on e and on the receive parity e & 1 (the per-unit
+// epochs of round 4 gave full and tail steps different parities for the same
+// elements). Parity double-buffers the receive slots: a peer can
+// run at most one step ahead (its step k+2 push needs its step k+1 reduce,
+// which needs this rank's step k+1 pushes, which follow this rank's step k
+// reduce on the same stream). A flag only ever grows while `step` grows;
+// ``rebase_epochs`` keeps e increasing when the host moves `step` backwards.
 // Publication: every storing wave waits for its stores (s_waitcnt vmcnt(0)
 // after the release fence, MI355X_MICROARCH.md "Compiler hazard"), then a
 // workgroup barrier, then one lane per peer does a system-scope release store
 // of the flag; the consumer polls with system-scope acquire loads, then a
 // barrier. A wait longer than `timeout_ticks` sets `status` (1 + 1000000 +
-// unit offset, never 0) and leaves the unit's parameters unchanged: a lost peer never hangs the GPU.
+// unit offset, never 0) and leaves the unit's parameters unchanged: a lost peer
+// never hangs the GPU. Once `status` is set, or the host raised the abort word
+// (host-mapped, XgmiP2PReducer.abort(): the runner's _abort on a lost peer),
+// a wait gives up at its first unsuccessful poll, so the steps still queued
+// behind a failure drain in microseconds each instead of one timeout each.
 #pragma once
 #include "conv_small.h"
 #include "p2p_allreduce.h"
@@ -81,7 +90,7 @@ __device__ __forceinline__ void comm_unit_body(const CommJobArgs& a, uint8_t* ld
   const long long o0 = sg.off + u.start;  // the unit's first arena element: its flag / epoch slot
   const int S = cx->s, me = cx->me;
   if (threadIdx.x == 0) {
-    *s_ep = (push ? cx->ep_push[o0] : cx->ep_red[o0]) + 1u;
+    *s_ep = (unsigned)(fa.st->step + cx->ep_base);
     *s_ok = 1;
   }
   __syncthreads();
@@ -162,9 +171,17 @@ __device__ __forceinline__ void comm_unit_body(const CommJobArgs& a, uint8_t* ld
         const bool mine = t < S && t != me;
         const unsigned* f = cx->peer_flags[me] + (long long)(mine ? t : 0) * rs + o0;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (true) {
+        for (unsigned it = 0;; ++it) {
           const bool ready = !mine || (int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) >= 0;
           if (__all(ready)) break;
+          // a failure already recorded (this or an earlier step) or a host abort: give up now
+          if ((it & 63u) == 0 && p2p_wait_abandoned(cx->status, cx->abort_flag, t)) {
+            if (t == 0) {
+              atomicCAS(cx->status, 0, kCommAborted);
+              *s_ok = 0;
+            }
+            break;
+          }
           if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > cx->timeout_ticks) {
             if (t == 0) {
               atomicCAS(cx->status, 0, (int)(1 + 1000000 + (o0 < 2000000000LL ? o0 : 2000000000LL)));
@@ -234,10 +251,6 @@ __device__ __forceinline__ void comm_unit_body(const CommJobArgs& a, uint8_t* ld
         }
       }
     }
-  }
-  if (threadIdx.x == 0) {
-    if (push) cx->ep_push[o0] = e;
-    if (reduce) cx->ep_red[o0] = e;
   }
 }
 

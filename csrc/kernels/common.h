@@ -76,4 +76,20 @@ __device__ __forceinline__ float normal_from_bits(uint32_t a, uint32_t b) {
   return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
 }
 
+// Slow path of the xGMI all-reduce waits (p2p_allreduce.hip, comm_jobs.h),
+// called by every lane of the polling wave after an unsuccessful poll: true
+// (wave-uniform) when a wait already failed (`status` != 0, this or an earlier
+// step) or the host raised the abort word (host-mapped, may be null). The
+// caller records the abort in `status` (so later waits stop at the cheaper
+// device-memory read); here lane 0 only reads, at system scope (the words are
+// written by other workgroups / the host).
+__device__ __forceinline__ bool p2p_wait_abandoned(const int* status, const int* abort_flag, int lane) {
+  int bad = 0;
+  if (lane == 0) {
+    bad = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    if (!bad && abort_flag) bad = __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  }
+  return __any(bad);
+}
+
 }  // namespace mdt

@@ -26,6 +26,7 @@ struct P2PArgs {
   int two_shot;                         // 1: reduce-scatter by chunk owner + all-gather
   float scale;                          // 1/s for averaging
   long long timeout_ticks;              // s_memrealtime ticks (100 MHz)
+  const int* abort_flag;                // host-mapped word the host sets to abandon every wait (may be null)
 };
 
 // Device descriptor of the all-reduce JOBS (comm_jobs.h) over a gradient
@@ -33,16 +34,18 @@ struct P2PArgs {
 struct CommCtx {
   float* peer_recv[kP2PMaxRanks];      // every rank's receive region (device VA in this process)
   unsigned* peer_flags[kP2PMaxRanks];  // every rank's flag array
-  unsigned* ep_push;                   // [numel] local epochs of the push phase
-  unsigned* ep_red;                    // [numel] local epochs of the reduce phase
-  int* status;                         // 0 ok; else 1 + 1000000 + arena offset of a unit whose wait timed out
+  int* status;                         // 0 ok; else 1 + 1000000 + arena offset of a unit whose wait timed out,
+                                       // or kCommAborted once a wait saw the host's abort word
+  const int* abort_flag;               // host-mapped word: nonzero = abandon every wait (runner's _abort)
   long long numel;                     // gradient arena elements (receive stride)
+  long long ep_base;                   // epoch of a step = TrainState.step + ep_base (rebase_epochs)
   int me, s;
   float scale;                         // 1/s (averaging) or a test pre-multiplier
   long long timeout_ticks;             // s_memrealtime ticks (100 MHz)
 };
 
 enum : int { kCommPush = 1, kCommReduce = 2, kCommPushReduce = 3 };
+constexpr int kCommAborted = 999999;  // status after an abort (distinct from 1 + bucket / 1000001 + offset)
 
 }  // namespace mdt
 

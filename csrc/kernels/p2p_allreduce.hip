@@ -31,7 +31,9 @@
 // Receive slabs and flags are uncached (hipDeviceMallocUncached) so polled
 // flags and freshly pushed data never come from a stale cache line.
 // A wait that exceeds `timeout_ticks` records the bucket in `status` and the
-// block exits: a lost peer never hangs the GPU.
+// block exits: a lost peer never hangs the GPU. Once `status` is set (or the
+// host raised the abort word) later waits give up at their first unsuccessful
+// poll, so the launches queued behind a failure drain at once.
 #include "common.h"
 #include "p2p_allreduce.h"
 
@@ -77,18 +79,22 @@ __device__ __forceinline__ bool p2p_wait(const P2PArgs& a, int phase, unsigned e
     const bool mine = p < a.s && p != a.me;
     const unsigned* f = a.my_flags + a.flag_off + ((long long)phase * a.s + p) * G + blockIdx.x;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    bool timed_out = false;
-    while (true) {
+    int fail = 0;  // 1: timed out, 2: abandoned (earlier failure or host abort)
+    for (unsigned it = 0;; ++it) {
       const bool ready = !mine || (int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) >= 0;
       if (__all(ready)) break;
+      if ((it & 63u) == 0 && p2p_wait_abandoned(a.status, a.abort_flag, p)) {
+        fail = 2;
+        break;
+      }
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
-        timed_out = true;
+        fail = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (timed_out && p == 0) {
-      atomicCAS(a.status, 0, 1 + a.bucket);
+    if (fail && p == 0) {
+      atomicCAS(a.status, 0, fail == 1 ? 1 + a.bucket : kCommAborted);
       *s_ok = 0;
     }
   }

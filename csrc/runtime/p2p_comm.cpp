@@ -25,15 +25,17 @@
 // `connect_local` maps peers that live in the same process (single-GPU tests
 // run s "ranks" on one device, each with its own stream).
 // With `fused` the region also holds the receive slots / flags / epochs of the
-// all-reduce JOBS (csrc/kernels/comm_jobs.h): models that issue their own
+// all-reduce JOBS (csrc/kernels/comm_jobs.h; one epoch per step, read from the
+// trainer's step counter): models that issue their own
 // backward launches put the push and the reduce+Adam of the gradient arena
 // into those launches instead of calling launch()/wait() (one stream, no
 // events); `comm_ctx()` is the device descriptor those jobs take.
 #include <hip/hip_runtime_api.h>
 
+#include <cstddef>
 #include <cstring>
 #include <iterator>
-#include <map>
+#include <list>
 #include <mutex>
 #include <utility>
 
@@ -43,38 +45,71 @@
 namespace mdt {
 
 // Process-lifetime pool of the uncached regions. A freed region is kept for
-// the next reducer of the same device and size instead of going back to the
-// runtime: otherwise its address range -- still mapped uncached -- was handed
-// out again to torch's caching allocator, and later trainers' activations and
-// partial slabs landed in it (bench/diag_uc_reuse.py); the reducer-free 28x28
-// step then stopped being run-to-run bitwise in the processes where that
-// happened (profiles/r4_determinism). Regions are reused only at exactly the
-// requested size; production keeps one reducer per trial for the whole run.
+// the next reducer of the same device and size class instead of going back to
+// the runtime: otherwise its address range -- still mapped uncached -- was
+// handed out again to torch's caching allocator, and later trainers'
+// activations and partial slabs landed in it (bench/diag_uc_reuse.py); the
+// reducer-free 28x28 step then stopped being run-to-run bitwise in the
+// processes where that happened (profiles/r4_determinism; the mechanism is
+// still open). Sizes are rounded up to a power of two (>= 1 MiB) so reducers
+// with different bucket layouts share regions, and at most kMaxFree regions
+// per device stay parked: beyond that the oldest one is freed after a device
+// sync (autotune's throw-away reducers no longer pin one region per layout).
 class UncachedPool {
  public:
+  static constexpr int kMaxFree = 4;
+  static size_t size_class(size_t bytes) {
+    size_t c = (size_t)1 << 20;
+    while (c < bytes) c <<= 1;
+    return c;
+  }
   static void* take(int dev, size_t bytes) {
     std::lock_guard<std::mutex> g(mu());
-    auto& m = free_list();
-    auto range = m.equal_range({dev, bytes});
-    if (range.first == range.second) return nullptr;
-    auto it = std::prev(range.second);  // the most recently freed region of that size
-    void* p = it->second;
-    m.erase(it);
-    return p;
+    auto& l = free_list();
+    for (auto it = l.rbegin(); it != l.rend(); ++it) {  // the most recently freed region of that class
+      if (it->dev == dev && it->bytes == bytes) {
+        void* p = it->p;
+        l.erase(std::next(it).base());
+        return p;
+      }
+    }
+    return nullptr;
   }
   static void give(int dev, size_t bytes, void* p) {
     std::lock_guard<std::mutex> g(mu());
-    free_list().emplace(std::make_pair(dev, bytes), p);
+    auto& l = free_list();
+    l.push_back({dev, bytes, p});
+    int n = 0;
+    for (const auto& r : l) n += r.dev == dev;
+    if (n <= kMaxFree) return;
+    for (auto it = l.begin(); it != l.end(); ++it) {
+      if (it->dev != dev) continue;
+      (void)hipDeviceSynchronize();  // no kernel of this device still touches it
+      (void)hipFree(it->p);
+      l.erase(it);
+      return;
+    }
+  }
+  static int64_t parked(int dev) {
+    std::lock_guard<std::mutex> g(mu());
+    int64_t n = 0;
+    for (const auto& r : free_list()) n += r.dev == dev;
+    return n;
   }
 
  private:
+  struct Region {
+    int dev;
+    size_t bytes;
+    void* p;
+  };
   static std::mutex& mu() {
     static std::mutex m;
     return m;
   }
-  static std::multimap<std::pair<int, size_t>, void*>& free_list() {
-    static auto* m = new std::multimap<std::pair<int, size_t>, void*>();  // never destroyed: outlives every reducer
-    return *m;
+  static std::list<Region>& free_list() {
+    static auto* l = new std::list<Region>();  // never destroyed: outlives every reducer
+    return *l;
   }
 };
 
@@ -114,17 +149,21 @@ class XgmiP2PReducer : public StreamBuckets {
     ep_byte_ = flags_byte_ + al(foff * 4);
     status_byte_ = ep_byte_ + al(eoff * 4);
     bytes_ = status_byte_ + 256;
-    if (fused_) {  // comm_jobs.h: recv [2][s][numel] f32 | flags [s][numel] u32 | epochs [2][numel] u32
+    if (fused_) {  // comm_jobs.h: recv [2][s][numel] f32 | flags [s][numel] u32 (one epoch per step: none stored)
       const long long n = flat_.numel();
       frecv_byte_ = bytes_;
       fflags_byte_ = frecv_byte_ + al(2LL * s_ * n * 4);
-      fep_byte_ = fflags_byte_ + al((long long)s_ * n * 4);
-      bytes_ = fep_byte_ + al(2LL * n * 4);
+      bytes_ = fflags_byte_ + al((long long)s_ * n * 4);
     }
+    alloc_bytes_ = (long long)UncachedPool::size_class((size_t)bytes_);
     DeviceGuard dg(device_);
-    base_ = UncachedPool::take(device_, (size_t)bytes_);
-    if (!base_) MDT_HIP_CHECK(hipExtMallocWithFlags(&base_, (size_t)bytes_, hipDeviceMallocUncached));
+    base_ = UncachedPool::take(device_, (size_t)alloc_bytes_);
+    if (!base_) MDT_HIP_CHECK(hipExtMallocWithFlags(&base_, (size_t)alloc_bytes_, hipDeviceMallocUncached));
     MDT_HIP_CHECK(hipMemset((char*)base_ + flags_byte_, 0, (size_t)(bytes_ - flags_byte_)));
+    // the host's abort word (abort()): pinned, mapped into the device address space, read uncached by the waits
+    MDT_HIP_CHECK(hipHostMalloc((void**)&abort_host_, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    *abort_host_ = 0;
+    MDT_HIP_CHECK(hipHostGetDevicePointer((void**)&abort_dev_, abort_host_, 0));
     MDT_HIP_CHECK(hipDeviceSynchronize());
     for (int p = 0; p < kP2PMaxRanks; ++p) peer_base_[p] = nullptr;
     peer_base_[me_] = base_;
@@ -136,7 +175,8 @@ class XgmiP2PReducer : public StreamBuckets {
     if (ctx_) (void)hipFree(ctx_);
     for (int p = 0; p < s_; ++p)
       if (p != me_ && peer_base_[p] && opened_[p]) (void)hipIpcCloseMemHandle(peer_base_[p]);
-    if (base_) UncachedPool::give(device_, (size_t)bytes_, base_);
+    if (base_) UncachedPool::give(device_, (size_t)alloc_bytes_, base_);
+    if (abort_host_) (void)hipHostFree(abort_host_);
   }
 
   // 64-byte hipIpcMemHandle_t of this rank's region (uint8 CPU tensor)
@@ -183,6 +223,31 @@ class XgmiP2PReducer : public StreamBuckets {
   double scale() const { return scale_; }
   bool fused() const { return fused_; }
 
+  // Abandon every wait of this reducer, now and later (the runner's _abort
+  // after a peer was lost): the host-mapped word is visible to kernels that
+  // are already spinning, so the queued steps drain at once (status() then
+  // reports kCommAborted unless a timeout was recorded first). No sync.
+  void abort() { __atomic_store_n(abort_host_, 1, __ATOMIC_SEQ_CST); }
+  bool aborted() const { return __atomic_load_n(abort_host_, __ATOMIC_SEQ_CST) != 0; }
+
+  // The fused jobs' epoch of a step is TrainState.step + ep_base. Call when the
+  // host moves the trainer's step counter from `old_step` back to `new_step`
+  // (every member of the group the same way, at a point where no step is in
+  // flight): the epochs keep increasing, so no stale peer flag looks current.
+  void rebase_epochs(int64_t old_step, int64_t new_step) {
+    if (new_step >= old_step) return;
+    ep_base_ += (old_step - new_step) + 2;
+    if (ctx_) {
+      DeviceGuard dg(device_);
+      MDT_HIP_CHECK(hipDeviceSynchronize());
+      MDT_HIP_CHECK(hipMemcpy((char*)ctx_ + offsetof(CommCtx, ep_base), &ep_base_, sizeof(ep_base_),
+                              hipMemcpyHostToDevice));
+    }
+  }
+  int64_t epoch_base() const { return ep_base_; }
+  static int64_t pooled_regions(int64_t dev) { return UncachedPool::parked((int)dev); }
+  int64_t alloc_bytes() const { return alloc_bytes_; }
+
   // Device address of the CommCtx the fused all-reduce jobs take (built once,
   // after connect; a one-rank group needs no connect).
   int64_t comm_ctx() {
@@ -195,9 +260,9 @@ class XgmiP2PReducer : public StreamBuckets {
         c.peer_recv[p] = p < s_ ? (float*)((char*)peer_base_[p] + frecv_byte_) : nullptr;
         c.peer_flags[p] = p < s_ ? (unsigned*)((char*)peer_base_[p] + fflags_byte_) : nullptr;
       }
-      c.ep_push = (unsigned*)((char*)base_ + fep_byte_);
-      c.ep_red = c.ep_push + flat_.numel();
       c.status = (int*)((char*)base_ + status_byte_);
+      c.abort_flag = abort_dev_;
+      c.ep_base = ep_base_;
       c.numel = flat_.numel();
       c.me = me_;
       c.s = s_;
@@ -233,6 +298,7 @@ class XgmiP2PReducer : public StreamBuckets {
     a.two_shot = two_[b];
     a.scale = scale_;
     a.timeout_ticks = timeout_ticks_;
+    a.abort_flag = abort_dev_;
     if (s_ == 1 && scale_ == 1.0f) return;
     const int rc = mdt_p2p_allreduce(&a, grid_[b], s);
     TORCH_CHECK(rc == 0, "p2p all-reduce launch failed: ", rc);
@@ -242,7 +308,10 @@ class XgmiP2PReducer : public StreamBuckets {
   int me_, s_;
   bool fused_ = false;
   void* ctx_ = nullptr;
-  long long frecv_byte_ = 0, fflags_byte_ = 0, fep_byte_ = 0;
+  long long frecv_byte_ = 0, fflags_byte_ = 0, alloc_bytes_ = 0;
+  int64_t ep_base_ = 0;
+  int* abort_host_ = nullptr;
+  int* abort_dev_ = nullptr;
   float scale_ = 1.0f;
   long long timeout_ticks_ = 0;
   void* base_ = nullptr;
@@ -271,7 +340,13 @@ void bind_p2p(pybind11::module& m) {
                .def("comm_ctx", &XgmiP2PReducer::comm_ctx)
                .def("scale", &XgmiP2PReducer::scale)
                .def("grids", &XgmiP2PReducer::grids)
-               .def("two_shot", &XgmiP2PReducer::two_shot);
+               .def("two_shot", &XgmiP2PReducer::two_shot)
+               .def("abort", &XgmiP2PReducer::abort)
+               .def("aborted", &XgmiP2PReducer::aborted)
+               .def("rebase_epochs", &XgmiP2PReducer::rebase_epochs)
+               .def("epoch_base", &XgmiP2PReducer::epoch_base)
+               .def("alloc_bytes", &XgmiP2PReducer::alloc_bytes)
+               .def_static("pooled_regions", &XgmiP2PReducer::pooled_regions);
   def_bucket_api(c);
 }
 

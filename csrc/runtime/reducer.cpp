@@ -14,8 +14,8 @@ BucketReducer::BucketReducer(c10::intrusive_ptr<c10d::ProcessGroup> pg, at::Tens
   for (size_t i = 1; i < bounds_.size(); ++i)
     TORCH_CHECK(bounds_[i] > bounds_[i - 1], "bucket bounds must be increasing");
   world_ = pg_->getSize();
-  // RCCL/NCCL implement AVG natively (pre-mul-sum); gloo does not.
-  use_avg_op_ = average_ && flat_.is_cuda();
+  // RCCL/NCCL implement AVG natively (pre-mul-sum); gloo does not (also not on GPU tensors).
+  use_avg_op_ = average_ && flat_.is_cuda() && pg_->getBackendName() != "gloo";
   work_.resize(bounds_.size() - 1);
 }
 

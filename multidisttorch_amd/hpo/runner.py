@@ -180,13 +180,41 @@ def _launch_epoch(trainer, epoch: int, n_shard: int, opts: RunOptions, fault_at:
     return step0, early
 
 
-def _abort(group, device):
+def _abort(group, device, trainer=None):
+    """Give up on the group's data plane: the trainer's xGMI reducer (its
+    in-kernel waits see the host-mapped abort word, so the steps still queued
+    drain at once instead of one MDT_P2P_TIMEOUT_S each) and the group's RCCL
+    communicator (its kernels observe the abort flag and exit)."""
+    red = getattr(trainer, "reducer", None)
+    if red is not None and hasattr(red, "abort"):
+        red.abort()
     try:
         be = group._get_backend(device)
         if hasattr(be, "abort"):
             be.abort()
     except Exception:  # noqa: BLE001 - best effort, we are failing anyway
         pass
+
+
+def _drain(events, limit_s: float):
+    """After an abort: wait (bounded) until the queued steps have left the
+    stream, so the process can sync, checkpoint or exit. Seconds taken, or
+    None if the stream is still busy after ``limit_s``."""
+    t = time.monotonic()
+    while events and not events[-1].query():
+        if time.monotonic() - t > limit_s:
+            return None
+        time.sleep(0.001)
+    return time.monotonic() - t
+
+
+def _fail_epoch(trainer, group, device, events, msg):
+    _abort(group, device, trainer)
+    limit = float(os.getenv("MDT_ABORT_DRAIN_S", "30"))
+    d = _drain(events, limit)
+    trainer.drain_s = d
+    tail = f"stream drained in {d:.2f} s" if d is not None else f"stream still busy after {limit:.0f} s"
+    raise TrialTimeout(f"{msg} ({tail})")
 
 
 def _wait_epoch(trainer, group, device, events, watch=None):
@@ -198,8 +226,9 @@ def _wait_epoch(trainer, group, device, events, watch=None):
     trial's ``TrialWatch`` and check the peers (a published failure or a
     silent peer ends the wait within ~0.5 s / ``MDT_HEARTBEAT_S``); and if no
     chunk of steps completes for ``MDT_GROUP_TIMEOUT_S`` the epoch is stuck.
-    Either way abort the group's communicator (RCCL kernels observe the abort
-    flag and exit) and fail the trial."""
+    Either way abort the group's data plane (``_abort``: the xGMI reducer's
+    waits and the RCCL communicator give up), let the queued steps drain
+    (bounded by ``MDT_ABORT_DRAIN_S``) and fail the trial."""
     if device.type != "cuda" or group is None or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
     ev = torch.cuda.Event()
@@ -218,8 +247,7 @@ def _wait_epoch(trainer, group, device, events, watch=None):
             break
         now = time.monotonic()
         if now - last_progress > stall:
-            _abort(group, device)
-            raise TrialTimeout(f"no step of the epoch completed for {stall:.0f} s (peer lost?)")
+            _fail_epoch(trainer, group, device, events, f"no step of the epoch completed for {stall:.0f} s (peer lost?)")
         if watch is not None and now >= next_beat:
             next_beat = now + 0.5
             try:
@@ -228,8 +256,7 @@ def _wait_epoch(trainer, group, device, events, watch=None):
             except Exception as e:  # noqa: BLE001 - the store (on world rank 0) is unreachable
                 msg = f"control store unreachable: {type(e).__name__}: {e}"
             if msg:
-                _abort(group, device)
-                raise TrialTimeout(msg)
+                _fail_epoch(trainer, group, device, events, msg)
         time.sleep(0.0005)
     red = getattr(trainer, "reducer", None)
     if red is not None and hasattr(red, "status") and int(red.status()) != 0:
@@ -324,7 +351,8 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
                    process_group=group)
         else:
             bounds, kind = trainer.bucket_bounds(opts.bucket_mb), None
-        trainer.attach_reducer(make_arena_reducer(group, trainer.grads, bounds, kind=kind))
+        trainer.attach_reducer(make_arena_reducer(group, trainer.grads, bounds, kind=kind,
+                                                  comm_jobs=getattr(trainer, "comm_jobs", False)))
     start_epoch = 1
     if opts.ckpt_dir and opts.resume:
         # only group rank 0 writes checkpoints, so only it reads one; the

@@ -360,8 +360,18 @@ class ConvVaeTrainer:
     def step_count(self):
         return int(self.read_state()["step"])
 
+    @property
+    def comm_jobs(self) -> bool:
+        """The step can host the fused all-reduce jobs (comm_jobs.h): the
+        default intra-node reducer for this trainer is then kind "xgmi"."""
+        return self.backend == "hip" and self.fuse_jobs
+
     def set_step(self, step):
         if self.backend == "hip":
+            red = self.reducer
+            if red is not None and hasattr(red, "rebase_epochs"):
+                # the fused jobs' epoch is step + base: keep it increasing
+                red.rebase_epochs(self.step_count, int(step))
             self.state.set_step(False, int(step))
         else:
             self._st["step"] = int(step)
@@ -411,6 +421,12 @@ class ConvVaeTrainer:
         (csrc/kernels/comm_jobs.h): no second stream, no events."""
         self.reducer = reducer
         self._graphs.clear()
+        from ..parallel.ddp import graph_capturable
+
+        # a host-blocking (c10d/gloo) reducer cannot live inside a step graph: eager steps
+        if not hasattr(self, "_graphs_wanted"):
+            self._graphs_wanted = self.use_graphs
+        self.use_graphs = self._graphs_wanted and graph_capturable(reducer)
         self._plans28.clear()
         self._comm_packs = {}
         self._comm_tables = {}

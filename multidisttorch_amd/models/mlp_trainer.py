@@ -191,6 +191,12 @@ class MlpVaeTrainer:
         first, overlapping the rest of the backward) or [0, numel]."""
         self.reducer = reducer
         self._graphs.clear()
+        from ..parallel.ddp import graph_capturable
+
+        # a host-blocking (c10d/gloo) reducer cannot live inside a step graph: eager steps
+        if not hasattr(self, "_graphs_wanted"):
+            self._graphs_wanted = self.use_graphs
+        self.use_graphs = self._graphs_wanted and graph_capturable(reducer)
 
     def bucket_bounds(self, bucket_mb=None):
         """The fused step finishes gradients in two groups (fc4 after B1, the

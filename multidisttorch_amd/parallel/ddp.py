@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import math
 import os
+import sys
 from typing import Dict, Iterable, List, Optional, Sequence
 
 import torch
@@ -34,7 +35,7 @@ from ..ops import native
 
 __all__ = ["XgmiModel", "plan_buckets", "make_arena_reducer", "PyBucketReducer", "ArenaDDP",
            "broadcast_params", "rccl_comm_ptr", "reducer_kind", "make_p2p_reducer", "P2P_KINDS",
-           "two_shot_min_bytes", "group_on_one_node", "overlap_pays"]
+           "two_shot_min_bytes", "group_on_one_node", "overlap_pays", "graph_capturable"]
 
 
 class XgmiModel:
@@ -195,32 +196,36 @@ def group_on_one_node(pg) -> bool:
     return len(set(hosts)) == 1
 
 
-def reducer_kind(pg, flat: torch.Tensor) -> str:
+def reducer_kind(pg, flat: torch.Tensor, comm_jobs: bool = True) -> str:
     """'xgmi' (hipIpc push over xGMI fused into the step's launches where the
     model supports it, a one-shot push kernel otherwise), 'rccl' (direct RCCL
     on torch's communicator), 'p2p' (one-shot, two-shot for big buckets of
     groups >= 3), 'p2p1' (one-shot only), 'p2p2' (two-shot only), 'c10d'
     (native reducer over the ProcessGroup) or 'python'. MDT_REDUCER overrides.
 
-    Default on GPU: 'xgmi' for a multi-rank group whose members share a node
-    (every intra-node group on an 8x MI355X node: one-GPU structure cost 1.04x
-    of the reducer-free 28x28 step against 1.12x for RCCL on the compute
-    stream and 1.62x for RCCL on its own stream, profiles/r4_ddp_fused), RCCL
-    for a group that spans nodes; collective (all members call it)."""
+    Default on GPU, for a multi-rank group whose members share a node (every
+    intra-node group on an 8x MI355X node): 'xgmi' when the trainer puts the
+    all-reduce into its own launches (``comm_jobs``: ConvVaeTrainer; one-GPU
+    structure cost 1.04x of the reducer-free 28x28 step against 1.12x for
+    RCCL on the compute stream, profiles/r4_ddp_fused), 'rccl' when it does not
+    (the MLP trainer: RCCL inline 1.16x against 1.39x for the standalone push
+    kernel, profiles/r4_ddp_fused/ddp_structure_mlp.json). RCCL for a group
+    that spans nodes. Collective (all members call it)."""
     forced = os.getenv("MDT_REDUCER", "")
     if forced:
         return forced
     if not native.available():
         return "python"
     if flat.is_cuda and dist.get_backend(pg) == "nccl":
-        if dist.get_world_size(pg) > 1 and group_on_one_node(pg):
+        if comm_jobs and dist.get_world_size(pg) > 1 and group_on_one_node(pg):
             return "xgmi"
         return "rccl"
     return "c10d"
 
 
 def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: bool = True,
-                       prefer_native: bool = True, kind: Optional[str] = None, scale: float = 0.0):
+                       prefer_native: bool = True, kind: Optional[str] = None, scale: float = 0.0,
+                       comm_jobs: bool = True):
     """Bucket reducer over a flat gradient arena ([begin, end) buckets).
 
     On MI355X trial groups (RCCL) this is the direct-RCCL reducer of
@@ -230,23 +235,39 @@ def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: b
     ``scale`` (RCCL only) replaces the 1/s pre-multiplier; any scale other
     than 1 issues the collective even on a one-rank group (tests use it to
     put real ``ncclAllReduce`` kernels into a one-GPU step graph).
+    ``comm_jobs``: the trainer can host the fused all-reduce jobs (see
+    ``reducer_kind``). A peer-to-peer kind whose hipIpc mapping fails on any
+    member (e.g. GPU visibility restricted per rank) falls back, on every
+    member together, to RCCL (nccl groups) or the c10d reducer.
     """
     if pg is None:
         pg = dist.distributed_c10d._get_default_group()
-    kind = kind or (reducer_kind(pg, flat) if prefer_native else "python")
+    kind = kind or (reducer_kind(pg, flat, comm_jobs) if prefer_native else "python")
     b = [int(x) for x in bounds]
+    if kind in ("xgmi",) or kind in P2P_KINDS:
+        red = (make_p2p_reducer(pg, flat, b, average, two_shot="never", fused=True, scale=scale)
+               if kind == "xgmi" else make_p2p_reducer(pg, flat, b, average, two_shot=P2P_KINDS[kind]))
+        if red is not None:
+            return red
+        kind = "rccl" if dist.get_backend(pg) == "nccl" else "c10d"
+        print(f"[mdt] peer mapping over xGMI failed in a group of {dist.get_world_size(pg)}: "
+              f"falling back to the {kind} reducer", file=sys.stderr, flush=True)
     if kind == "rccl":
         size = dist.get_world_size(pg)
         return native.require().RcclBucketReducer(rccl_comm_ptr(pg, flat.device), size, flat, b, average, scale)
-    if kind == "xgmi":
-        return make_p2p_reducer(pg, flat, b, average, two_shot="never", fused=True, scale=scale)
-    if kind in P2P_KINDS:
-        return make_p2p_reducer(pg, flat, b, average, two_shot=P2P_KINDS[kind])
     if kind == "c10d" and native.available():
         return native.require().BucketReducer(pg, flat, b, average)
     if flat.is_cuda:
         native.require()  # on GPU the native reducer is mandatory: fail loudly
     return PyBucketReducer(pg, flat, bounds, average)
+
+
+def graph_capturable(reducer) -> bool:
+    """Whether a reducer's collectives can be captured into a replayed step
+    graph: the RCCL and xGMI reducers issue device work only; the c10d/gloo
+    reducers block on host-side work objects (a gloo world on GPU tensors,
+    e.g. the IPC-failure fallback of a one-GPU rehearsal)."""
+    return reducer is None or type(reducer).__name__ not in ("BucketReducer", "PyBucketReducer")
 
 
 def overlap_pays(first_bucket_bytes: int, split_cost_us: float, link_gbps: float = 153.0) -> bool:
@@ -289,7 +310,9 @@ def make_p2p_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: boo
     (reduce-scatter to chunk owners + all-gather, 2/s of the bucket per link;
     ``two_shot``: "auto" | "never" | "always", see ``two_shot_min_bytes``).
     All ranks of the group must share one node. Selected with
-    ``MDT_REDUCER=p2p`` (or ``kind="p2p"/"p2p1"/"p2p2"``).
+    ``MDT_REDUCER=p2p`` (or ``kind="p2p"/"p2p1"/"p2p2"``). Returns None on
+    every member when any member could not map a peer's region (the caller
+    falls back to another reducer).
     ``fused`` (kind "xgmi") also allocates the receive slots of the all-reduce
     JOBS (csrc/kernels/comm_jobs.h) that models with their own backward
     launches (ConvVaeTrainer) put into those launches: one stream, no events;
@@ -304,13 +327,29 @@ def make_p2p_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: boo
     red = C.XgmiP2PReducer(r, s, flat, [int(x) for x in bounds], average, float(scale), max_blocks, timeout_s,
                            two_shot_min_bytes(two_shot, s), fused)
     if s > 1:
-        h = red.ipc_handle()
-        if dist.get_backend(pg) == "nccl":
+        ok = 1
+        try:
+            h = red.ipc_handle()
+        except RuntimeError:
+            ok, h = 0, torch.zeros(64, dtype=torch.uint8)
+        on_dev = dist.get_backend(pg) == "nccl"
+        if on_dev:
             h = h.to(flat.device)
         hs = [torch.empty_like(h) for _ in range(s)]
         dist.all_gather(hs, h, group=pg)
         # every peer zeroed its region (the ctor syncs the device) before publishing its handle
-        red.connect([x.cpu() for x in hs])
+        if ok:
+            try:
+                if os.getenv("MDT_TEST_IPC_FAIL_RANK", "") == str(r):
+                    raise RuntimeError("injected hipIpcOpenMemHandle failure (MDT_TEST_IPC_FAIL_RANK)")
+                red.connect([x.cpu() for x in hs])
+            except RuntimeError as e:
+                ok = 0
+                print(f"[mdt] group rank {r}: cannot map a peer's memory: {e}", file=sys.stderr, flush=True)
+        flag = torch.tensor([ok], dtype=torch.int32, device=flat.device if on_dev else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=pg)
+        if int(flag.item()) == 0:
+            return None
     return red
 
 
@@ -370,7 +409,7 @@ class ArenaDDP(nn.Module):
         if self.world > 1:
             if broadcast:
                 broadcast_params([p.data for p in params] + list(module.buffers()), process_group)
-            self.reducer = make_arena_reducer(process_group, self.grad_arena, bounds, average)
+            self.reducer = make_arena_reducer(process_group, self.grad_arena, bounds, average, comm_jobs=False)
             self.reducer.set_param_map(pb)
             self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i))
                            for i, p in enumerate(params)]

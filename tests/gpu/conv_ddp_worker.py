@@ -10,7 +10,14 @@ bitwise identical. Phase 2 (independent eps per replica, rng_stream = group
 rank, as the reference's unseeded replicas): replicas still bitwise identical
 after every step, while their per-replica losses differ.
 
-argv: image graphs(0|1) bucket_mb [reducer kind]  -> prints RESULT json
+argv: image graphs(0|1) bucket_mb [reducer kind] [mode] [tail]  -> prints RESULT json
+  mode "split" (default for xgmi at 28x28 before round 5): push and reduce in
+  separate eager launches with a host barrier between them; "prod": the
+  production schedule exactly (graphs as given, the in-kernel wait, no split
+  tail, no host barrier; run with MDT_CU_SPLIT=1 so ranks sharing the GPU
+  never starve each other). tail > 0: every epoch ends with a partial batch of
+  that many samples (full and tail steps alternate: different finalize-unit
+  decompositions of the same arena).
 """
 import json
 import os
@@ -27,6 +34,8 @@ def main():
     image, graphs = int(sys.argv[1]), sys.argv[2] == "1"
     bucket_mb = None if sys.argv[3] == "none" else float(sys.argv[3])
     kind = sys.argv[4] if len(sys.argv) > 4 else "p2p"
+    mode = sys.argv[5] if len(sys.argv) > 5 else ("split" if kind == "xgmi" and image == 28 else "prod")
+    tail = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     from multidisttorch_amd.runtime.env import apply_cu_split
 
     apply_cu_split()  # MDT_CU_SPLIT=1: disjoint CU shares per rank (before HIP initialises)
@@ -42,9 +51,16 @@ def main():
     z = 32 if image == 28 else 64
     nb = 4
     D = image * image
-    X = torch.rand(nb * B, D, generator=torch.Generator().manual_seed(11)).to(dev)
-    idx = torch.arange(nb * B, device=dev, dtype=torch.int32)
-    steps = 8
+    n = nb * B + tail
+    X = torch.rand(n, D, generator=torch.Generator().manual_seed(11)).to(dev)
+    idx = torch.arange(n, device=dev, dtype=torch.int32)
+    per_epoch = nb + (1 if tail else 0)
+    steps = 2 * per_epoch
+
+    def epoch(tr):
+        tr.train_steps(nb)
+        if tail:
+            tr.train_steps(1, M=tail)
 
     def make(stream):
         return ConvVaeTrainer(batch_size=B, image=image, z=z, device=dev, backend="hip", seed=7, lr=2e-3,
@@ -62,28 +78,30 @@ def main():
         tr.refresh_weights()
         red = make_arena_reducer(dist.group.WORLD, tr.grads, tr.bucket_bounds(bucket_mb), kind=kind)
         tr.attach_reducer(red)
-        if kind == "xgmi" and image == 28:
-            # ranks share one GPU: a reduce spinning on a peer's push could hold the CUs that
-            # peer needs, so push and reduce go in separate launches with a host barrier between
-            # (eager steps; on a node every rank owns its GPU and the reduce waits in-kernel)
+        if kind == "xgmi" and image == 28 and mode == "split":
+            # push and reduce in separate launches with a host barrier between
+            # (eager steps): the pre-CU-split rehearsal form, kept as a variant
             tr.comm_split_tail = True
             tr.comm_phase_hook = lambda: (torch.cuda.synchronize(), dist.barrier())
+        assert mode == "split" or not tr.comm_split_tail
         tr.bind_train_data(X, idx)
-        tr.set_cursor(0, nb)
+        tr.set_cursor(0, per_epoch)
         same_each = []
         for _ in range(2):
-            tr.train_steps(steps // 2)
+            epoch(tr)
             torch.cuda.synchronize()
             same_each.append(gather_same(tr.params.cpu()))
         hist = tr.loss_history()[:steps].astype(np.float64)
-        res[phase] = dict(same=same_each, status=int(red.status()), nb=int(red.num_buckets()),
+        res[phase] = dict(reducer=type(red).__name__, same=same_each, split=bool(tr.comm_split_tail), pair=bool(getattr(tr, "f28_pair", False)),
+                          cu_mask=os.environ.get("HSA_CU_MASK"), status=int(red.status()) if hasattr(red, "status") else 0, nb=int(red.num_buckets()),
                           launched=int(red.launched_count()), loss=hist.tolist(),
                           finite=bool(torch.isfinite(tr.params).all().item()))
         if phase == "same_eps" and r == 0:
             ref = make(0)
             ref.bind_train_data(X, idx)
-            ref.set_cursor(0, nb)
-            ref.train_steps(steps)
+            ref.set_cursor(0, per_epoch)
+            epoch(ref)
+            epoch(ref)
             torch.cuda.synchronize()
             d = (tr.params - ref.params).abs().max().item()
             scale = ref.params.abs().max().item()

@@ -240,21 +240,34 @@ def test_prepare_locks_graphs_for_timed_steps(native_ext, model):
         tr.train_steps(1, M=64)
 
 
-@pytest.mark.parametrize("s,image,graphs,mb,kind", [(2, 28, 1, "none", "p2p"), (4, 28, 1, "0.25", "p2p"),
-                                                    (2, 128, 1, "2", "p2p"), (4, 128, 0, "none", "p2p"),
-                                                    (2, 28, 1, "none", "p2p2"), (4, 128, 1, "2", "p2p2"),
-                                                    (2, 28, 0, "none", "xgmi"), (4, 28, 0, "none", "xgmi")])
-def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb, kind):
+@pytest.mark.parametrize("s,image,graphs,mb,kind,mode,tail", [
+    (2, 28, 1, "none", "p2p", "prod", 0), (4, 28, 1, "0.25", "p2p", "prod", 0),
+    (2, 128, 1, "2", "p2p", "prod", 0), (4, 128, 0, "none", "p2p", "prod", 0),
+    (2, 28, 1, "none", "p2p2", "prod", 0), (4, 128, 1, "2", "p2p2", "prod", 0),
+    (2, 28, 0, "none", "xgmi", "split", 0), (4, 28, 0, "none", "xgmi", "split", 0),
+    # the shipped default exactly: fused jobs with the in-kernel wait, graphs on,
+    # paired kernel on, no split tail, no host barrier; CU-split ranks
+    (2, 28, 1, "none", "xgmi", "cu", 0), (4, 28, 1, "none", "xgmi", "cu", 0),
+    (2, 128, 1, "none", "xgmi", "cu", 0), (4, 128, 1, "none", "xgmi", "cu", 0),
+    # full and tail batches alternate (different finalize-unit decompositions)
+    (2, 28, 1, "none", "xgmi", "cu", 40), (2, 128, 1, "none", "xgmi", "cu", 8)])
+def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb, kind, mode, tail):
     from multidisttorch_amd.launch import launch
 
-    # several processes share the GPU: the fused 28x28 step keeps one workgroup
-    # per sample (a paired sample whose partner is not resident falls back to
-    # the solo form, whose f32 summation order differs at rounding level). The
-    # fused all-reduce jobs ("xgmi") run eagerly with push and reduce in
-    # separate launches and a host barrier between them (conv_ddp_worker.py).
-    env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2", "MDT_F28_PAIR": "0"}
-    rc, outs = launch([sys.executable, os.path.join(HERE, "conv_ddp_worker.py"), str(image), str(graphs), mb, kind], s,
-                      emulate="torchrun", timeout=150, extra_env=env, capture=True)
+    # several processes share the GPU. "prod"/"split": the fused 28x28 step keeps
+    # one workgroup per sample (MDT_F28_PAIR=0), and the "split" xgmi form runs
+    # push and reduce in separate eager launches with a host barrier between
+    # them. "cu": production defaults (pair on, graphs, in-kernel wait) with every
+    # rank confined to its own CU share (MDT_CU_SPLIT=1, runtime/env.py), so a
+    # rank's spinning reduce never holds the CUs its peers need.
+    env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2"}
+    if mode == "cu":
+        env["MDT_CU_SPLIT"] = "1"
+    else:
+        env["MDT_F28_PAIR"] = "0"
+    wmode = "prod" if mode == "cu" else mode
+    rc, outs = launch([sys.executable, os.path.join(HERE, "conv_ddp_worker.py"), str(image), str(graphs), mb, kind,
+                       wmode, str(tail)], s, emulate="torchrun", timeout=150, extra_env=env, capture=True)
     text = "\n".join(o or "" for o in outs)
     assert rc == 0, text[-4000:]
     res = [json.loads(l[7:]) for l in text.splitlines() if l.startswith("RESULT ")]
@@ -263,6 +276,10 @@ def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb, kind):
         for ph in ("same_eps", "indep_eps"):
             assert r[ph]["status"] == 0 and r[ph]["finite"], (ph, r)
             assert all(r[ph]["same"]), (ph, r)  # replicas bitwise identical at every check
+            assert r[ph]["split"] == (mode == "split"), (ph, r)
+            if mode == "cu":
+                assert r[ph]["cu_mask"], (ph, r)  # the rank really ran on its CU share
+                assert r[ph]["pair"] == (image == 28), (ph, r)
     r0 = [r for r in res if r["rank"] == 0][0]
     sg = r0["single"]
     assert sg["max_param_diff"] <= 1e-5 * max(1.0, sg["param_scale"]), sg
@@ -270,3 +287,24 @@ def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb, kind):
     # independent eps: per-replica losses differ (different samples of z)
     losses = [tuple(r["indep_eps"]["loss"]) for r in res]
     assert len(set(losses)) == s
+
+
+def test_xgmi_falls_back_when_a_peer_cannot_be_mapped():
+    """hipIpcOpenMemHandle failing on one member (e.g. GPU visibility
+    restricted per rank; injected with MDT_TEST_IPC_FAIL_RANK) makes EVERY
+    member fall back together (here: gloo world -> the c10d reducer), and the
+    trial still trains data-parallel with bitwise-equal replicas."""
+    from multidisttorch_amd.launch import launch
+
+    env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2", "MDT_CU_SPLIT": "1", "MDT_TEST_IPC_FAIL_RANK": "1"}
+    rc, outs = launch([sys.executable, os.path.join(HERE, "conv_ddp_worker.py"), "28", "1", "none", "xgmi", "prod",
+                       "0"], 2, emulate="torchrun", timeout=150, extra_env=env, capture=True)
+    text = "\n".join(o or "" for o in outs)
+    assert rc == 0, text[-4000:]
+    res = [json.loads(l[7:]) for l in text.splitlines() if l.startswith("RESULT ")]
+    assert len(res) == 2, text[-4000:]
+    for r in res:
+        for ph in ("same_eps", "indep_eps"):
+            assert r[ph]["reducer"] == "BucketReducer", r
+            assert all(r[ph]["same"]) and r[ph]["finite"], (ph, r)
+    assert "falling back to the c10d reducer" in text

@@ -194,3 +194,36 @@ def test_fused_reducer_layer_path_bitwise(native_ext, image):
         np.testing.assert_array_equal(out[1][0], out[0][0])
         assert torch.equal(out[1][1], out[0][1]), (out[1][1] - out[0][1]).abs().max().item()
         assert torch.equal(out[1][2], out[0][2])  # transposed copies of the updated weights
+
+
+def test_fused_reducer_epoch_rebase_and_abort_word(native_ext):
+    """Host-side controls of the fused reducer: moving the trainer's step
+    counter backwards rebases the jobs' epoch (step + base stays increasing);
+    the abort word is visible to the host and a one-rank step (no waits) still
+    runs bitwise after it; the uncached regions are pooled per size class."""
+    dev = torch.device("cuda", 0)
+    nb = 4
+    X, idx = _data(nb, 128, dev)
+    tr = _trainer(dev, False)
+    red = _fused_reducer(tr)
+    tr.attach_reducer(red)
+    tr.bind_train_data(X, idx)
+    tr.set_cursor(0, nb)
+    tr.train_steps(3)
+    torch.cuda.synchronize()
+    assert red.epoch_base() == 0
+    tr.set_step(10)  # forward (resume): no rebase needed
+    assert red.epoch_base() == 0
+    tr.set_step(2)  # backwards: base grows past the epochs already used
+    assert red.epoch_base() == (10 - 2) + 2
+    tr.train_steps(2)
+    torch.cuda.synchronize()
+    assert int(red.status()) == 0 and tr.read_state()["step"] == 4
+    assert not red.aborted()
+    red.abort()
+    assert red.aborted()
+    tr.train_steps(1)  # s = 1: nothing to wait for, the step is unaffected
+    torch.cuda.synchronize()
+    assert int(red.status()) == 0
+    sz = red.alloc_bytes()
+    assert sz >= red.region_bytes() and sz & (sz - 1) == 0  # power-of-two size class

@@ -85,3 +85,65 @@ def test_mlp_trainer_overlap_resolution(monkeypatch):
     assert tr._overlap() is False
     monkeypatch.setenv("MDT_DDP_OVERLAP", "1")
     assert MlpVaeTrainer(batch_size=8, backend="torch", seed=0).ddp_overlap is True
+
+
+def test_default_reducer_follows_trainer_capability(monkeypatch):
+    """Intra-node multi-rank RCCL groups: the fused xGMI jobs for trainers that
+    host them (conv), RCCL inline for the MLP trainer (1.16x vs 1.39x for the
+    standalone push kernel, profiles/r4_ddp_fused/ddp_structure_mlp.json)."""
+    from multidisttorch_amd.parallel import ddp
+
+    class FlatCuda:
+        is_cuda = True
+
+    monkeypatch.delenv("MDT_REDUCER", raising=False)
+    monkeypatch.setattr(ddp.native, "available", lambda: True)
+    monkeypatch.setattr(ddp.dist, "get_backend", lambda pg=None: "nccl")
+    monkeypatch.setattr(ddp.dist, "get_world_size", lambda pg=None: 2)
+    monkeypatch.setattr(ddp, "group_on_one_node", lambda pg: True)
+    assert ddp.reducer_kind(object(), FlatCuda()) == "xgmi"
+    assert ddp.reducer_kind(object(), FlatCuda(), comm_jobs=True) == "xgmi"
+    assert ddp.reducer_kind(object(), FlatCuda(), comm_jobs=False) == "rccl"
+    monkeypatch.setattr(ddp, "group_on_one_node", lambda pg: False)
+    assert ddp.reducer_kind(object(), FlatCuda(), comm_jobs=True) == "rccl"
+
+
+def test_trainer_comm_job_capability():
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+    from multidisttorch_amd.models.mlp_trainer import MlpVaeTrainer
+
+    assert ConvVaeTrainer(batch_size=4, image=28, backend="torch", seed=0).comm_jobs is False  # no HIP launches
+    assert getattr(MlpVaeTrainer(batch_size=4, backend="torch", seed=0), "comm_jobs", False) is False
+
+
+def test_production_paths_never_split_the_comm_tail():
+    """The push/reduce split with a host barrier between them
+    (``comm_split_tail``) is a test-only rehearsal form: no production module,
+    the bench or the entry point may turn it on; the trainer defaults it off."""
+    import ast
+    import os
+
+    from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    files = [os.path.join(root, "bench.py"), os.path.join(root, "vae-hpo.py")]
+    for d, _, fs in os.walk(os.path.join(root, "multidisttorch_amd")):
+        files += [os.path.join(d, f) for f in fs if f.endswith(".py")]
+    offenders = []
+    for path in files:
+        tree = ast.parse(open(path).read())
+        for node in ast.walk(tree):
+            targets = node.targets if isinstance(node, ast.Assign) else (
+                [node.target] if isinstance(node, (ast.AugAssign, ast.AnnAssign)) else [])
+            for t in targets:
+                if isinstance(t, ast.Attribute) and t.attr in ("comm_split_tail", "comm_phase_hook"):
+                    v = node.value
+                    if not (isinstance(v, ast.Constant) and v.value in (False, None)):
+                        offenders.append(f"{path}:{node.lineno}")
+            if isinstance(node, ast.Call) and getattr(node.func, "id", "") == "setattr":
+                a = node.args
+                if len(a) >= 2 and isinstance(a[1], ast.Constant) and a[1].value == "comm_split_tail":
+                    offenders.append(f"{path}:{node.lineno}")
+    assert not offenders, offenders
+    tr = ConvVaeTrainer(batch_size=4, image=28, backend="torch", seed=0)
+    assert tr.comm_split_tail is False and tr.comm_phase_hook is None

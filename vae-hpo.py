@@ -78,6 +78,9 @@ def parse_args(argv=None):
 
 def main(argv=None):
     args = parse_args(argv)
+    from multidisttorch_amd.runtime.env import apply_cu_split
+
+    apply_cu_split()  # one-GPU multi-rank rehearsals only (MDT_CU_SPLIT=1), before HIP initialises
     if args.debug_sync:  # must precede any HIP initialisation
         os.environ["AMD_SERIALIZE_KERNEL"] = "3"
         os.environ["AMD_SERIALIZE_COPY"] = "3"
