@@ -74,6 +74,53 @@ struct CommJobArgs {
 
 constexpr int kCommLds = kFinalizeThreads * 4 + 64 + 16;
 
+// Publication of a unit's stores to every peer: each storing wave waits for
+// its stores (release fence + vmcnt(0)), a workgroup barrier, then lane p
+// stores `val` into peer p's flag of (this rank, unit) at system scope.
+__device__ __forceinline__ void comm_publish(const CommCtx* cx, long long o0, unsigned val, int t) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t < cx->s && t != cx->me)
+    __hip_atomic_store(cx->peer_flags[t] + (long long)cx->me * cx->numel + o0, val, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Wait until every peer's flag of the unit reaches `target` (bounded; gives up
+// at once after a recorded failure or a host abort: *s_ok = 0), then barrier +
+// acquire. Lane p of wave 0 polls peer p's flag in local memory.
+__device__ __forceinline__ void comm_wait(const CommCtx* cx, long long o0, unsigned target, int t, int* s_ok) {
+  if (t < 64 && *s_ok) {
+    const int me = cx->me;
+    const bool mine = t < cx->s && t != me;
+    const unsigned* f = cx->peer_flags[me] + (long long)(mine ? t : 0) * cx->numel + o0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned it = 0;; ++it) {
+      const bool ready =
+          !mine || (int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - target) >= 0;
+      if (__all(ready)) break;
+      // a failure already recorded (this or an earlier step) or a host abort: give up now
+      if ((it & 63u) == 0 && p2p_wait_abandoned(cx->status, cx->abort_flag, t)) {
+        if (t == 0) {
+          atomicCAS(cx->status, 0, kCommAborted);
+          *s_ok = 0;
+        }
+        break;
+      }
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > cx->timeout_ticks) {
+        if (t == 0) {
+          atomicCAS(cx->status, 0, (int)(1 + 1000000 + (o0 < 2000000000LL ? o0 : 2000000000LL)));
+          *s_ok = 0;
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
 __device__ __forceinline__ void comm_unit_body(const CommJobArgs& a, uint8_t* lds, int b) {
   float* red = reinterpret_cast<float*>(lds);
   AdamC* cs = reinterpret_cast<AdamC*>(lds + kFinalizeThreads * 4);
@@ -141,66 +188,38 @@ __device__ __forceinline__ void comm_unit_body(const CommJobArgs& a, uint8_t* ld
     }
   }
 
+  // two-shot (groups >= 3, CommCtx.two_shot): the unit is cut into S chunks of
+  // `chunk` elements (a multiple of 4 from the unit start, so a thread's elements
+  // never straddle two chunks); chunk q is owned by rank q
+  const bool two = cx->two_shot && S > 2;
+  const int chunk = two ? ((u.count + S - 1) / S + 3) / 4 * 4 : u.count;
+  const int owner = two ? (int)((o - o0) / chunk) : me;
+
   if (push) {
-    // own contribution into the local arena, then into every peer's slot [par][me]
+    // own contribution into the local arena, then into the receive slot [par][me]
+    // of every peer (one-shot) or of the chunk's owner only (two-shot)
     if (nel == 4) {
       const f32x4 s4 = {g[0], g[1], g[2], g[3]};
       *reinterpret_cast<f32x4*>(fa.G + o) = s4;
       for (int p = 0; p < S; ++p)
-        if (p != me) *reinterpret_cast<f32x4*>(cx->peer_recv[p] + ((long long)par * S + me) * rs + o) = s4;
+        if (p != me && (!two || p == owner))
+          *reinterpret_cast<f32x4*>(cx->peer_recv[p] + ((long long)par * S + me) * rs + o) = s4;
     } else {
       for (int j = 0; j < nel; ++j) {
         fa.G[o + j] = g[j];
         for (int p = 0; p < S; ++p)
-          if (p != me) cx->peer_recv[p][((long long)par * S + me) * rs + o + j] = g[j];
+          if (p != me && (!two || p == owner)) cx->peer_recv[p][((long long)par * S + me) * rs + o + j] = g[j];
       }
     }
-    if (S > 1) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t < S && t != me)
-        __hip_atomic_store(cx->peer_flags[t] + (long long)me * rs + o0, e, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (S > 1) comm_publish(cx, o0, 2u * e - 1u, t);
   }
 
   if (reduce) {
-    if (S > 1) {
-      if (t < 64) {
-        const bool mine = t < S && t != me;
-        const unsigned* f = cx->peer_flags[me] + (long long)(mine ? t : 0) * rs + o0;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        for (unsigned it = 0;; ++it) {
-          const bool ready = !mine || (int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) >= 0;
-          if (__all(ready)) break;
-          // a failure already recorded (this or an earlier step) or a host abort: give up now
-          if ((it & 63u) == 0 && p2p_wait_abandoned(cx->status, cx->abort_flag, t)) {
-            if (t == 0) {
-              atomicCAS(cx->status, 0, kCommAborted);
-              *s_ok = 0;
-            }
-            break;
-          }
-          if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > cx->timeout_ticks) {
-            if (t == 0) {
-              atomicCAS(cx->status, 0, (int)(1 + 1000000 + (o0 < 2000000000LL ? o0 : 2000000000LL)));
-              *s_ok = 0;
-            }
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    }
-    if (*s_ok && nel > 0) {
-      // rank-order sum: identical bits on every replica
-      float acc[4];
-      const float* my_recv = cx->peer_recv[me];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = 0.f;
+    if (S > 1) comm_wait(cx, o0, 2u * e - 1u, t, s_ok);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* my_recv = cx->peer_recv[me];
+    if (*s_ok && nel > 0 && owner == me) {
+      // rank-order sum: identical bits on every replica (and two-shot == one-shot)
       for (int p = 0; p < S; ++p) {
         if (p == me) {
 #pragma unroll
@@ -218,6 +237,38 @@ __device__ __forceinline__ void comm_unit_body(const CommJobArgs& a, uint8_t* ld
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] *= cx->scale;
+      if (two) {
+        // all-gather: the reduced chunk into every peer's slot [par][me] (its
+        // elements there are never a reduce-scatter target: those are the
+        // peer's own chunk)
+        for (int p = 0; p < S; ++p) {
+          if (p == me) continue;
+          float* dst = cx->peer_recv[p] + ((long long)par * S + me) * rs + o;
+          if (nel == 4) {
+            *reinterpret_cast<f32x4*>(dst) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+          } else {
+            for (int j = 0; j < nel; ++j) dst[j] = acc[j];
+          }
+        }
+      }
+    }
+    if (two) {
+      // a failed reduce-scatter wait publishes nothing: the peers then fail
+      // their own wait (status) instead of reading a chunk that never came
+      if (*s_ok) comm_publish(cx, o0, 2u * e, t);
+      comm_wait(cx, o0, 2u * e, t, s_ok);
+      if (*s_ok && nel > 0 && owner != me) {  // the owner's reduced, scaled chunk
+        const float* src = my_recv + ((long long)par * S + owner) * rs + o;
+        if (nel == 4) {
+          const f32x4 r4 = *reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = r4[j];
+        } else {
+          for (int j = 0; j < nel; ++j) acc[j] = src[j];
+        }
+      }
+    }
+    if (*s_ok && nel > 0) {
       if (!adam) {
         if (nel == 4) {
           const f32x4 s4 = {acc[0], acc[1], acc[2], acc[3]};

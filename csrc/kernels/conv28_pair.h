@@ -94,7 +94,7 @@ using g32i = __attribute__((address_space(1))) int;
 // command 0.0652-0.0653 vs 0.0640-0.0642 ms). Stress coverage: pairs run under
 // a concurrent GEMM stream and a packed second trial, near pairs counted from
 // the stamps, results bitwise run to run (tests/gpu/test_conv28_fused.py,
-// bench/diag_determinism.py). MDT_HIP_EXTRA_FLAGS=-DMDT_F28_NEAR_WG=0 builds
+// scripts/diag/diag_determinism.py). MDT_HIP_EXTRA_FLAGS=-DMDT_F28_NEAR_WG=0 builds
 // the agent-scope form.
 #ifndef MDT_F28_NEAR_WG  // 0: agent scope on the near path too (A/B build, profiles/r4_near_scope)
 #define MDT_F28_NEAR_WG 1
@@ -397,8 +397,16 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) wr[0][i] = wh0[i];
     ld_rows(1, wr[1]);
+#ifdef MDT_F28_HALFW_EXP  // timing experiment only (wrong results): half the P3 / Q5 weight bytes
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      wr[2][i] = wr[0][i];
+      wr[3][i] = wr[1][i];
+    }
+#else
     ld_rows(2, wr[2]);
     ld_rows(3, wr[3]);
+#endif
     float d[8];
 #pragma unroll
     for (int c2 = 0; c2 < 4; ++c2)
@@ -783,8 +791,13 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = 0.f;
     bf16x8 wh6[16];  // rows 16..31 of the group: with wh5, all 32 in flight at once
+#ifdef MDT_F28_HALFW_EXP
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wh6[i] = wh5[i];
+#else
 #pragma unroll
     for (int i = 0; i < 16; ++i) wh6[i] = wh_ld(16 + i);
+#endif
     w2r.load(TB(kTW2));  // enc2 tap images: in flight during Q5
 #pragma unroll
     for (int i = 0; i < 32; ++i) {

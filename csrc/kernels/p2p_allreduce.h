@@ -40,6 +40,7 @@ struct CommCtx {
   long long numel;                     // gradient arena elements (receive stride)
   long long ep_base;                   // epoch of a step = TrainState.step + ep_base (rebase_epochs)
   int me, s;
+  int two_shot;                        // 1 (groups >= 3): reduce-scatter to chunk owners + all-gather per unit
   float scale;                         // 1/s (averaging) or a test pre-multiplier
   long long timeout_ticks;             // s_memrealtime ticks (100 MHz)
 };

@@ -48,7 +48,7 @@ namespace mdt {
 // the next reducer of the same device and size class instead of going back to
 // the runtime: otherwise its address range -- still mapped uncached -- was
 // handed out again to torch's caching allocator, and later trainers'
-// activations and partial slabs landed in it (bench/diag_uc_reuse.py); the
+// activations and partial slabs landed in it (scripts/diag/diag_uc_reuse.py); the
 // reducer-free 28x28 step then stopped being run-to-run bitwise in the
 // processes where that happened (profiles/r4_determinism; the mechanism is
 // still open). Sizes are rounded up to a power of two (>= 1 MiB) so reducers
@@ -151,6 +151,9 @@ class XgmiP2PReducer : public StreamBuckets {
     bytes_ = status_byte_ + 256;
     if (fused_) {  // comm_jobs.h: recv [2][s][numel] f32 | flags [s][numel] u32 (one epoch per step: none stored)
       const long long n = flat_.numel();
+      // the jobs' two-shot form (reduce-scatter to chunk owners + all-gather, 2/s of the arena per link)
+      // under the same rule as the buckets': groups >= 3 and an arena of at least two_shot_min_bytes
+      fused_two_ = s_ >= 3 && two_shot_min_bytes >= 0 && n * 4 >= two_shot_min_bytes;
       frecv_byte_ = bytes_;
       fflags_byte_ = frecv_byte_ + al(2LL * s_ * n * 4);
       bytes_ = fflags_byte_ + al((long long)s_ * n * 4);
@@ -222,6 +225,7 @@ class XgmiP2PReducer : public StreamBuckets {
   }
   double scale() const { return scale_; }
   bool fused() const { return fused_; }
+  bool fused_two_shot() const { return fused_two_; }
 
   // Abandon every wait of this reducer, now and later (the runner's _abort
   // after a peer was lost): the host-mapped word is visible to kernels that
@@ -266,6 +270,7 @@ class XgmiP2PReducer : public StreamBuckets {
       c.numel = flat_.numel();
       c.me = me_;
       c.s = s_;
+      c.two_shot = fused_two_ ? 1 : 0;
       c.scale = scale_;
       c.timeout_ticks = timeout_ticks_;
       MDT_HIP_CHECK(hipMalloc(&ctx_, sizeof(CommCtx)));
@@ -306,7 +311,7 @@ class XgmiP2PReducer : public StreamBuckets {
 
  private:
   int me_, s_;
-  bool fused_ = false;
+  bool fused_ = false, fused_two_ = false;
   void* ctx_ = nullptr;
   long long frecv_byte_ = 0, fflags_byte_ = 0, alloc_bytes_ = 0;
   int64_t ep_base_ = 0;
@@ -337,6 +342,7 @@ void bind_p2p(pybind11::module& m) {
                .def("connect_local", &XgmiP2PReducer::connect_local)
                .def("status", &XgmiP2PReducer::status)
                .def("fused", &XgmiP2PReducer::fused)
+               .def("fused_two_shot", &XgmiP2PReducer::fused_two_shot)
                .def("comm_ctx", &XgmiP2PReducer::comm_ctx)
                .def("scale", &XgmiP2PReducer::scale)
                .def("grids", &XgmiP2PReducer::grids)

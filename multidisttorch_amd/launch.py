@@ -45,7 +45,7 @@ def rank_env(rank: int, world: int, port: int, emulate: str = "torchrun",
     # CPU ranks share the host: split the intra-op threads instead of oversubscribing
     env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // max(1, world))))
     if emulate == "torchrun":
-        env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+        env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
     elif emulate == "slurm":
         env.update(SLURM_NPROCS=str(world), SLURM_PROCID=str(rank), SLURM_LOCALID=str(rank),
                    SLURM_NODELIST="localhost")

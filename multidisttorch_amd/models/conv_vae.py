@@ -1402,6 +1402,8 @@ class ConvVaeTrainer:
         g.replay()
 
     def _capture(self, S, M):
+        red = self.reducer
+        k0 = self.step_count if red is not None and hasattr(red, "rebase_epochs") else None
         snap = [t.clone() for t in (self.params, self.exp_avg, self.exp_avg_sq, self.state.train_state)]
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -1414,6 +1416,12 @@ class ConvVaeTrainer:
                 self._step_hip(M)
         for t, v in zip((self.params, self.exp_avg, self.exp_avg_sq, self.state.train_state), snap):
             t.copy_(v)
+        if k0 is not None:
+            # the warm-up step ran the fused all-reduce jobs at epoch k0 + 1 and
+            # published flags for it; the step counter now goes back to k0, so
+            # the next real step must not reuse that epoch (every member
+            # captures at the same points: the rebase is the same everywhere)
+            red.rebase_epochs(k0 + 1, k0)
         self._cast_weights()
         native.upload_graph(g)
         return g

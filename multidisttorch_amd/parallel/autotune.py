@@ -80,8 +80,8 @@ def comm_kinds(pg, device: torch.device) -> List[Optional[str]]:
     if len(set(hosts)) != 1:
         return ["rccl"]
     # groups of 3+: the mixed "p2p" kind (two-shot only for buckets >= MDT_P2P_TWO_SHOT_MB)
-    # as well as all-one-shot and all-two-shot
-    return ["rccl", "p2p1", "xgmi"] + (["p2p", "p2p2"] if len(hosts) >= 3 else [])
+    # as well as all-one-shot and all-two-shot, and the fused jobs in both forms
+    return ["rccl", "p2p1", "xgmi1"] + (["p2p", "p2p2", "xgmi2"] if len(hosts) >= 3 else [])
 
 
 def autotune_buckets(make_trainer: Callable[[], object], pg, X: torch.Tensor, idx: torch.Tensor,

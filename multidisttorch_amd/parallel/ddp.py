@@ -35,7 +35,8 @@ from ..ops import native
 
 __all__ = ["XgmiModel", "plan_buckets", "make_arena_reducer", "PyBucketReducer", "ArenaDDP",
            "broadcast_params", "rccl_comm_ptr", "reducer_kind", "make_p2p_reducer", "P2P_KINDS",
-           "two_shot_min_bytes", "group_on_one_node", "overlap_pays", "graph_capturable"]
+           "two_shot_min_bytes", "group_on_one_node", "overlap_pays", "graph_capturable",
+           "XGMI_KINDS"]
 
 
 class XgmiModel:
@@ -244,9 +245,9 @@ def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: b
         pg = dist.distributed_c10d._get_default_group()
     kind = kind or (reducer_kind(pg, flat, comm_jobs) if prefer_native else "python")
     b = [int(x) for x in bounds]
-    if kind in ("xgmi",) or kind in P2P_KINDS:
-        red = (make_p2p_reducer(pg, flat, b, average, two_shot="never", fused=True, scale=scale)
-               if kind == "xgmi" else make_p2p_reducer(pg, flat, b, average, two_shot=P2P_KINDS[kind]))
+    if kind in XGMI_KINDS or kind in P2P_KINDS:
+        red = (make_p2p_reducer(pg, flat, b, average, two_shot=XGMI_KINDS[kind], fused=True, scale=scale)
+               if kind in XGMI_KINDS else make_p2p_reducer(pg, flat, b, average, two_shot=P2P_KINDS[kind]))
         if red is not None:
             return red
         kind = "rccl" if dist.get_backend(pg) == "nccl" else "c10d"
@@ -282,6 +283,10 @@ def overlap_pays(first_bucket_bytes: int, split_cost_us: float, link_gbps: float
 # reducer kind -> two-shot rule: "auto" (buckets >= MDT_P2P_TWO_SHOT_MB, default 4, in groups >= 3),
 # "never" (one-shot), "always"
 P2P_KINDS = {"p2p": "auto", "p2p1": "never", "p2p2": "always"}
+# fused all-reduce jobs (comm_jobs.h): "xgmi" one-shot or, in groups >= 3 with
+# an arena of at least MDT_P2P_TWO_SHOT_MB (default 4: the 12-18 MB 128x128
+# model, not the 1.5 MB 28x28 one), two-shot per unit; "xgmi1" / "xgmi2" force
+XGMI_KINDS = {"xgmi": "auto", "xgmi1": "never", "xgmi2": "always"}
 
 
 def two_shot_min_bytes(rule: str, group_size: int) -> int:

@@ -6,7 +6,7 @@ so every torch.empty allocation of the trainer starts with that garbage,
 and compares the trained result bitwise with a clean run, for the solo and
 paired forms, eager and graph-replayed.
 
-    python bench/diag_alloc_poison.py
+    python scripts/diag/diag_alloc_poison.py
 """
 import json
 import os
@@ -14,7 +14,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def poison_allocator(value):

@@ -11,7 +11,7 @@ baseline result of stage 0:
   4 a fused reducer constructed, never launched, kept alive
   5 gc.collect() + torch.cuda.empty_cache()
 
-    python bench/diag_context.py
+    python scripts/diag/diag_context.py
 """
 import gc
 import json
@@ -20,7 +20,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -5,7 +5,7 @@ stream of unrelated GEMMs beside it, and reports how many distinct results
 (loss history + parameters) came out, and -- for the paired launch -- how many
 samples fell back to the one-workgroup form in each step (stamp slot 15).
 
-    python bench/diag_determinism.py [--runs 6] [--json out.json]
+    python scripts/diag/diag_determinism.py [--runs 6] [--json out.json]
 """
 import argparse
 import json
@@ -14,7 +14,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

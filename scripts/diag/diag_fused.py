@@ -5,7 +5,7 @@ f28_skip_adam (finalize only), and of the fused kernel's backward outputs, for
 the paired and the solo step; plus the solo step with an extra LDS-dirtying
 launch before it (uninitialised-LDS check).
 
-    python bench/diag_fused.py
+    python scripts/diag/diag_fused.py
 """
 import json
 import os
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -5,7 +5,7 @@ reducer-free eager, reducer-free graphs, fused-reducer eager, fused-reducer
 graphs -- three times each (fresh trainers), and prints how many distinct
 results each way produced and which ways agree with each other.
 
-    python bench/diag_fused_eager.py
+    python scripts/diag/diag_fused_eager.py
 """
 import json
 import os
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -6,7 +6,7 @@ bias partial rows, loss partials, activations and their gradients) with NaN
 before every step of an eager reducer-free trial; a buffer whose stale
 contents leak into the result turns the parameters non-finite.
 
-    python bench/diag_garbage.py
+    python scripts/diag/diag_garbage.py
 """
 import json
 import os
@@ -14,7 +14,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -5,7 +5,7 @@ differs (in pipeline order) names the launch whose result moved.
 Context first (what test_fused_comm does before its failing cases): fused
 -reducer trainers built and run, kept alive.
 
-    python bench/diag_lockstep.py [--pairs 10] [--pair 0]
+    python scripts/diag/diag_lockstep.py [--pairs 10] [--pair 0]
 """
 import argparse
 import json
@@ -14,7 +14,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

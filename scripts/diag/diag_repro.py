@@ -6,7 +6,7 @@ outside pytest, then probed:
   b) two reference trainers in lockstep with a device sync after every step,
      every per-step buffer compared -- the first buffer that differs.
 
-    python bench/diag_repro.py [--skip1] [--skip2]
+    python scripts/diag/diag_repro.py [--skip1] [--skip2]
 """
 import argparse
 import gc
@@ -16,7 +16,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -1,5 +1,5 @@
 """Diagnostic: the eager reducer-free SOLO 28x28 step (f28_pair = False) gave
-three distinct results in three fresh runs once (bench/diag_fused_eager.py)
+three distinct results in three fresh runs once (scripts/diag/diag_fused_eager.py)
 while graph replays and the paired form stayed bitwise. Which launch reads
 state it did not write? Poisons every CU's LDS (quiet NaN / a large finite
 pattern) right before ONE of the step's three launches (f28_step_k,
@@ -7,7 +7,7 @@ jobs_multi_k, grad_finalize_k) and counts distinct results per variant
 against the graph-replayed result, with and without a concurrent GEMM
 stream perturbing dispatch.
 
-    python bench/diag_solo_lds.py [--runs 4]
+    python scripts/diag/diag_solo_lds.py [--runs 4]
 """
 import argparse
 import json
@@ -16,7 +16,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 class PoisonC:

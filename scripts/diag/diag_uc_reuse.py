@@ -3,7 +3,7 @@ and died, do later trainers' buffers land inside the address range of its
 freed uncached (hipDeviceMallocUncached) reducer region, and which per-step
 buffer of a reducer-free solo step first differs from a clean run?
 
-    python bench/diag_uc_reuse.py
+    python scripts/diag/diag_uc_reuse.py
 """
 import gc
 import json
@@ -12,7 +12,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -19,6 +19,7 @@ argv: image graphs(0|1) bucket_mb [reducer kind] [mode] [tail]  -> prints RESULT
   that many samples (full and tail steps alternate: different finalize-unit
   decompositions of the same arena).
 """
+import hashlib
 import json
 import os
 import sys
@@ -92,7 +93,9 @@ def main():
             torch.cuda.synchronize()
             same_each.append(gather_same(tr.params.cpu()))
         hist = tr.loss_history()[:steps].astype(np.float64)
-        res[phase] = dict(reducer=type(red).__name__, same=same_each, split=bool(tr.comm_split_tail), pair=bool(getattr(tr, "f28_pair", False)),
+        res[phase] = dict(reducer=type(red).__name__, same=same_each,
+                          phash=hashlib.sha1(tr.params.cpu().numpy().tobytes()).hexdigest(),
+                          two_shot=bool(red.fused_two_shot()) if hasattr(red, "fused_two_shot") else None, split=bool(tr.comm_split_tail), pair=bool(getattr(tr, "f28_pair", False)),
                           cu_mask=os.environ.get("HSA_CU_MASK"), status=int(red.status()) if hasattr(red, "status") else 0, nb=int(red.num_buckets()),
                           launched=int(red.launched_count()), loss=hist.tolist(),
                           finite=bool(torch.isfinite(tr.params).all().item()))

@@ -279,7 +279,8 @@ def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb, kind, mode, tail):
             assert r[ph]["split"] == (mode == "split"), (ph, r)
             if mode == "cu":
                 assert r[ph]["cu_mask"], (ph, r)  # the rank really ran on its CU share
-                assert r[ph]["pair"] == (image == 28), (ph, r)
+                if image == 28:
+                    assert r[ph]["pair"], (ph, r)  # the paired headline kernel, as shipped
     r0 = [r for r in res if r["rank"] == 0][0]
     sg = r0["single"]
     assert sg["max_param_diff"] <= 1e-5 * max(1.0, sg["param_scale"]), sg
@@ -308,3 +309,32 @@ def test_xgmi_falls_back_when_a_peer_cannot_be_mapped():
             assert r[ph]["reducer"] == "BucketReducer", r
             assert all(r[ph]["same"]) and r[ph]["finite"], (ph, r)
     assert "falling back to the c10d reducer" in text
+
+
+def _worker_results(s, image, kind, tail=0):
+    from multidisttorch_amd.launch import launch
+
+    env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2", "MDT_CU_SPLIT": "1"}
+    rc, outs = launch([sys.executable, os.path.join(HERE, "conv_ddp_worker.py"), str(image), "1", "none", kind, "prod",
+                       str(tail)], s, emulate="torchrun", timeout=150, extra_env=env, capture=True)
+    text = "\n".join(o or "" for o in outs)
+    assert rc == 0, text[-4000:]
+    res = [json.loads(l[7:]) for l in text.splitlines() if l.startswith("RESULT ")]
+    assert len(res) == s, text[-4000:]
+    return {r["rank"]: r for r in res}
+
+
+@pytest.mark.parametrize("image,tail", [(128, 0), (28, 40)])
+def test_fused_two_shot_is_bitwise_one_shot(image, tail):
+    """The fused jobs' two-shot form (reduce-scatter to chunk owners +
+    all-gather, 2/s of the arena per link; groups >= 3) sums every chunk in
+    rank order with the same scale as the one-shot form: four CU-split ranks
+    end bitwise where the one-shot run ends, full and tail batches alike."""
+    one = _worker_results(4, image, "xgmi1", tail)
+    two = _worker_results(4, image, "xgmi2", tail)
+    for r in range(4):
+        for ph in ("same_eps", "indep_eps"):
+            assert one[r][ph]["two_shot"] is False and two[r][ph]["two_shot"] is True
+            assert one[r][ph]["status"] == 0 and two[r][ph]["status"] == 0
+            assert all(two[r][ph]["same"]), (ph, two[r])
+            assert two[r][ph]["phash"] == one[r][ph]["phash"], (r, ph)
