@@ -323,11 +323,6 @@ const Combo kCombos[] = {
     COMBO3(IgT2, Wg0, JFinalize),
     COMBO3(IgT4, Wg0, JFinalize),
     COMBO3(IgT6, Wg0, JFinalize),
-    // 128x128: enc4's backward launch (parity-mode cfg 5) and the direct
-    // 32x32 <-> 16x16 launches host the finalize of the big layers too
-    COMBO3(IgT5, Wg0, JFinalize),
-    COMBO3(Wg0, JFinalize, DcJS2),
-    COMBO3(Wg0, JFinalize, DcJT2),
     // optimizer tail: first-layer weight gradient || finalize+Adam of every
     // other layer; then first-layer finalize || transposed weight copies
     COMBO2(WgT5f, JFinalize),
