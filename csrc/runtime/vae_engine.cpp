@@ -229,7 +229,10 @@ void MlpVaeEngine::forward(const at::Tensor& X, const at::Tensor& idx, int64_t M
   VaeArgs a;
   fill_args(&a, X, idx, M, train, eval, rng_stream, want_recon);
   const VaeGrid g = vae_grid(a);
-  last_f2_blocks_ = g.f2 * 8;  // per-wave partial slots
+  // KLD partial slots: F2 blocks of group 0 write 8 per batch row tile (NOT
+  // g.f2 * 8: the other groups write none, and with a tail batch those slots
+  // still hold the previous batch's partials -- round 4's eval loss summed them)
+  last_f2_blocks_ = (int)((M + 15) / 16) * 8;
   last_f3_blocks_ = g.f3 * 8;
   check_rc(mdt_vae_forward(&a, c10::hip::getCurrentHIPStream().stream()), "vae forward");
 }
