@@ -174,7 +174,9 @@ class XgmiP2PReducer : public StreamBuckets {
 
   ~XgmiP2PReducer() override {
     DeviceGuard dg(device_);
-    (void)hipStreamSynchronize(stream_);
+    // the fused jobs run on the trainer's stream, not stream_: no kernel of
+    // any stream may still read ctx_ / the abort word / the region below
+    (void)hipDeviceSynchronize();
     if (ctx_) (void)hipFree(ctx_);
     for (int p = 0; p < s_; ++p)
       if (p != me_ && peer_base_[p] && opened_[p]) (void)hipIpcCloseMemHandle(peer_base_[p]);
