@@ -181,8 +181,8 @@ def test_grad_finalize_is_deterministic_and_fuses_adam(native_ext):
 @pytest.mark.parametrize("H", [28, 128])
 @pytest.mark.parametrize("f32_in", [True, False])
 def test_thin_conv_matches_conv2d(f32_in, H, native_ext):
-    # H = 128 exercises the MFMA form only with bit 1 of MDT_THIN_MFMA set
-    # (opt-in); otherwise the VALU body at both sizes
+    # H = 128 exercises the MFMA form (bit 1 of MDT_THIN_MFMA, default since
+    # round 5) for the f32 input and bit 8 for bf16; H = 28 the VALU body
     """Single-input-channel conv (encoder conv 1 / last layer backward-data).
     H = 28 runs the VALU body, H = 128 the MFMA form (thin_conv_mfma_body:
     split hi/lo bf16 weights and inputs); the f32 column sums pin both to the

@@ -186,7 +186,10 @@ def test_conv_vae_grads_match_bf16_emulated_reference(image, M, native_ext):
     """Layer-path step (28x28 with MDT_CONV_F28=0; 128x128: direct kernels,
     im2col GEMMs, thin edge kernels, split-K head) against a float64 reference
     rounded to bf16 where the kernels store bf16: every gradient tensor within
-    2e-2 relative error (the plain-fp32 comparison above allows 0.12)."""
+    3e-2 relative error (the plain-fp32 comparison above allows 0.12). The
+    bound is the bf16 rounding-flip noise floor of this comparison, measured
+    over ten seeds for both enc1 forms (profiles/r5_thin_mfma: worst 0.0275
+    VALU, 0.0230 MFMA); round 4's 2e-2 held only at this seed."""
     from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
 
     dev = torch.device("cuda")
@@ -211,7 +214,7 @@ def test_conv_vae_grads_match_bf16_emulated_reference(image, M, native_ext):
     assert abs(kloss - loss) / abs(loss) < 1e-3, (kloss, loss)
     errs = {n: _rel(tr.named_grads()[n], gref[n]) for n in gref}
     print(f"{image}x{image} layer-path grad rel-err vs bf16-emulated f64:", {k: round(v, 5) for k, v in errs.items()})
-    bad = {n: e for n, e in errs.items() if not e < 2e-2}
+    bad = {n: e for n, e in errs.items() if not e < 3e-2}
     assert not bad, bad
 
 
