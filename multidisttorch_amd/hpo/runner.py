@@ -390,9 +390,10 @@ def run_trial(spec: TrialSpec, group, opts: RunOptions, data=None, num_trials: O
     idx = shard_indices(len(train), n_rep, spec.group_id)
     trainer.bind_train_data(train.data, idx)
     n_shard = idx.numel()
-    # capture the step graphs and load the eval/decode kernels now, like the
-    # reference's model/DDP construction before its timer starts (vae-hpo.py:159)
-    trainer.prepare([opts.batch_size, n_shard % opts.batch_size], test.data[: opts.batch_size])
+    # capture the step graphs and the test-set eval graphs and load the
+    # decode kernels now, like the reference's model/DDP construction before
+    # its timer starts (vae-hpo.py:159)
+    trainer.prepare([opts.batch_size, n_shard % opts.batch_size], test.data if opts.eval_each_epoch else None)
 
     # Parity with the reference's download barrier (vae-hpo.py:133-144).
     global_barrier()
@@ -512,7 +513,7 @@ def run_packed_trials(specs, group, opts: RunOptions, data=None, num_trials: Opt
                 start = prog["epoch"] + 1
         idx = shard_indices(len(train), total, spec.group_id)  # packing extension: one shard per trial
         trainer.bind_train_data(train.data, idx)
-        trainer.prepare([opts.batch_size, idx.numel() % opts.batch_size], test.data[: opts.batch_size])
+        trainer.prepare([opts.batch_size, idx.numel() % opts.batch_size], test.data if opts.eval_each_epoch else None)
         rdir = (f"results-t{spec.group_id}-0" if opts.results else None)
         tr.append(dict(spec=spec, trainer=trainer, start=start, n_shard=idx.numel(), rdir=rdir,
                        stream=torch.cuda.Stream(device) if device.type == "cuda" else None,

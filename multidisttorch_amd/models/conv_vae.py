@@ -38,6 +38,7 @@ from torch import nn
 
 from ..ops import native
 from ..ops.philox import reparam_eps
+from .eval_graphs import GraphedEval
 from .mlp_vae import reference_adam_
 
 __all__ = ["Layer", "conv_vae_spec", "TorchConvVAE", "ConvVaeTrainer", "conv_layout"]
@@ -199,7 +200,7 @@ class TorchConvVAE(nn.Module):
 
 
 # --------------------------------------------------------------------------
-class ConvVaeTrainer:
+class ConvVaeTrainer(GraphedEval):
     """One trial of the conv VAE. Same driver-facing API as MlpVaeTrainer."""
 
     def __init__(self, batch_size: int = 128, image: int = 28, channels: int = 1, z: int = 32, device=None,
@@ -773,7 +774,9 @@ class ConvVaeTrainer:
         dec = [l for l in self.spec if l.name.startswith("dec")]
         h = self.xb
         first = 0
-        wt = self._wt_deferred()  # w16t of the previous step's update still to be written
+        # w16t of the previous step's update still to be written (an eval
+        # forward finds them current: evaluate() ran _ensure_wt first)
+        wt = self._wt_deferred() and train
         if src is not None:
             X, idx = src
             l = enc[0]
@@ -1427,6 +1430,20 @@ class ConvVaeTrainer:
         return g
 
     @torch.no_grad()
+    # graph-replayed eval passes (models/eval_graphs.py)
+    def _eval_batch(self, M, X, idx, want_recon):
+        st = self.state
+        self._forward_hip(M, st.eval_state, EVAL_STREAM + self.rng_stream, want_recon=want_recon, train=False,
+                          src=(X, idx))
+        self.C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, self._n_kld(M), st.eval_state,
+                              st.hparams, True)
+
+    def _eval_state(self):
+        return self.state.eval_state
+
+    def _eval_recon(self, M):
+        return self.recon[: M * self.D].view(M, self.D).clone()
+
     def evaluate(self, X, idx, want_first_recon=True):
         self._ensure_wt()
         idx = idx.to(device=self.device, dtype=torch.int32).contiguous()
@@ -1435,20 +1452,19 @@ class ConvVaeTrainer:
         pad = nb * self.B - n
         if pad:
             idx = torch.cat([idx, idx[:1].expand(pad)])
+        if self.backend == "hip" and self.use_graphs:
+            first = self._eval_graphed(X.contiguous(), idx, n, want_first_recon)
+            return self.read_state(eval=True)["epoch_loss"], first
         self.set_cursor(0, nb, eval=True)
         self.reset_loss(eval=True)
         first = None
         for b in range(nb):
             M = min(self.B, n - b * self.B)
             if self.backend == "hip":
-                st = self.state
                 want = want_first_recon and b == 0
-                self._forward_hip(M, st.eval_state, EVAL_STREAM + self.rng_stream, want_recon=want, train=False,
-                                  src=(X.contiguous(), idx))
-                self.C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, self._n_kld(M),
-                                      st.eval_state, st.hparams, True)
+                self._eval_batch(M, X.contiguous(), idx, want)
                 if want:
-                    first = self.recon[: M * self.D].view(M, self.D).clone()
+                    first = self._eval_recon(M)
             else:
                 st = self._st_eval
                 rows = idx[b * self.B: b * self.B + M].long()

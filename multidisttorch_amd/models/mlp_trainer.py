@@ -30,6 +30,7 @@ import torch
 
 from ..ops import native
 from ..ops.philox import reparam_eps
+from .eval_graphs import GraphedEval
 from .mlp_vae import arena_layout, init_params_, reference_adam_, reference_forward, reference_step, views
 
 __all__ = ["MlpVaeTrainer"]
@@ -38,7 +39,7 @@ EVAL_STREAM = 1 << 30
 LOSS_HIST = 4096
 
 
-class MlpVaeTrainer:
+class MlpVaeTrainer(GraphedEval):
     def __init__(self, batch_size: int = 128, D: int = 784, H: int = 400, Z: int = 20,
                  device=None, backend: Optional[str] = None, seed: int = 0, init_seed: Optional[int] = None,
                  lr: float = 1e-3, kl_beta: float = 1.0, betas=(0.9, 0.999), eps: float = 1e-8,
@@ -380,6 +381,17 @@ class MlpVaeTrainer:
 
     # ------------------------------------------------------------------ eval / sample
     @torch.no_grad()
+    # graph-replayed eval passes (models/eval_graphs.py)
+    def _eval_batch(self, M, X, idx, want_recon):
+        self.engine.forward(X, idx, M, False, True, EVAL_STREAM + self.rng_stream, want_recon)
+        self.engine.loss_finalize(True)
+
+    def _eval_state(self):
+        return self.engine.eval_state
+
+    def _eval_recon(self, M):
+        return self.engine.act("recon", M).clone()
+
     def evaluate(self, X: torch.Tensor, idx: torch.Tensor, want_first_recon: bool = True):
         """Forward + loss over (X[idx]); returns (sum_loss, recon of the first batch or None)."""
         idx = idx.to(device=self.device, dtype=torch.int32).contiguous()
@@ -389,6 +401,9 @@ class MlpVaeTrainer:
         if pad:
             idx = torch.cat([idx, idx[:1].expand(pad)])
         X = X.contiguous()
+        if self.backend == "hip" and self.use_graphs:
+            first = self._eval_graphed(X, idx, n, want_first_recon)
+            return self.read_state(eval=True)["epoch_loss"], first
         self.set_cursor(0, nb, eval=True)
         self.reset_loss(eval=True)
         first = None
@@ -396,10 +411,9 @@ class MlpVaeTrainer:
             M = min(self.B, n - b * self.B)
             if self.backend == "hip":
                 want = want_first_recon and b == 0
-                self.engine.forward(X, idx, M, False, True, EVAL_STREAM + self.rng_stream, want)
-                self.engine.loss_finalize(True)
+                self._eval_batch(M, X, idx, want)
                 if want:
-                    first = self.engine.act("recon", M).clone()
+                    first = self._eval_recon(M)
             else:
                 st = self._st_eval
                 cpu = self._cpu_native()
