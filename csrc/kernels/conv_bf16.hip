@@ -101,9 +101,12 @@ __global__ void __launch_bounds__(256) bce_logits_k(const float* logits, const f
 }
 
 // Sum loss partials -> loss ring; advance step (optionally cursor).
-__global__ void __launch_bounds__(256) conv_loss_finalize_k(LossArgs la) {
+__global__ void __launch_bounds__(256) conv_loss_finalize_k(LossArgs la, int advance_step) {
   __shared__ float scratch[16];
-  loss_finalize_body(la, scratch);
+  if (advance_step)
+    loss_step_body(la, scratch);  // the fused 28x28 forward's eval batches (its forward reads the step first)
+  else
+    loss_finalize_body(la, scratch);
 }
 
 // step++ and the Adam beta^t running products (first launch of a step).
@@ -221,9 +224,10 @@ int mdt_bce_logits(const float* logits, const float* X, const int* rows, int B, 
 
 int mdt_conv_loss_finalize(const float* bce_part, int nb, const float* kld_part, int nk, void* st, const void* hp,
                            int advance_cursor, hipStream_t s) {
+  // advance_cursor: bit 0 = advance the batch cursor, bit 1 = also advance the step (loss_step_body)
   const LossArgs la{bce_part, nb, kld_part, nk, reinterpret_cast<TrainState*>(st), reinterpret_cast<const HParams*>(hp),
-                    advance_cursor};
-  hipLaunchKernelGGL(conv_loss_finalize_k, dim3(1), dim3(256), 0, s, la);
+                    advance_cursor & 1};
+  hipLaunchKernelGGL(conv_loss_finalize_k, dim3(1), dim3(256), 0, s, la, (advance_cursor >> 1) & 1);
   return (int)hipGetLastError();
 }
 

@@ -318,9 +318,9 @@ void loss_finalize2(const at::Tensor& bce_part, int64_t nb, const at::Tensor& kl
        "job_loss");
     return;
   }
-  TORCH_CHECK(!advance_step, "loss_finalize2: advance_step needs a job (jobs_multi)");
   rc(mdt_conv_loss_finalize(bce_part.data_ptr<float>(), (int)nb, kld_part.data_ptr<float>(), (int)nk,
-                            state.data_ptr(), hparams.data_ptr(), advance_cursor ? 1 : 0, cur()),
+                            state.data_ptr(), hparams.data_ptr(), (advance_cursor ? 1 : 0) | (advance_step ? 2 : 0),
+                            cur()),
      "loss_finalize");
 }
 

@@ -1118,9 +1118,7 @@ class ConvVaeTrainer(GraphedEval):
         L = {l.name: l for l in self.spec}
         X, idx = self._data[0], self._data[1]
         st = self.state
-        w = [self._wf32(L["enc1"]), self._b(L["enc1"]), self._w(L["enc2"]), self._b(L["enc2"]),
-             self._w(L["enc_head"]), self._b(L["enc_head"]), self._w(L["dec_fc"]), self._b(L["dec_fc"]),
-             self._w(L["dec1"]), self._b(L["dec1"]), self._wf32(L["dec2"]), self._b(L["dec2"])]
+        w = self._f28_weights()
         part = self.f28_part
         bce, kld, db4 = part.narrow(0, 0, B), part.narrow(0, B, B), part.narrow(0, 2 * B, B)
         bias = self.f28_bias
@@ -1433,10 +1431,36 @@ class ConvVaeTrainer(GraphedEval):
     # graph-replayed eval passes (models/eval_graphs.py)
     def _eval_batch(self, M, X, idx, want_recon):
         st = self.state
+        if self.f28:
+            # the fused 28x28 forward in eval mode (f28_fwd_k, one workgroup
+            # per sample, no activation stores): one launch instead of the
+            # layer path's dozen; its loss job advances the eval step exactly
+            # like the layer path's step_begin (same Philox keys, same ring slot)
+            bce, kld = self.f28_part.narrow(0, 0, self.B), self.f28_part.narrow(0, self.B, self.B)
+            self.C.f28_forward(self._eval_fwd28(X, idx, want_recon), self.B, M, EVAL_STREAM + self.rng_stream,
+                               False)
+            self.C.loss_finalize2(bce, M, kld, M, st.eval_state, st.hparams, True, advance_step=True)
+            return
         self._forward_hip(M, st.eval_state, EVAL_STREAM + self.rng_stream, want_recon=want_recon, train=False,
                           src=(X, idx))
         self.C.loss_finalize2(self.bce_part, self._n_bce(M), self.kld_part, self._n_kld(M), st.eval_state,
                               st.hparams, True)
+
+    def _f28_weights(self):
+        L = {l.name: l for l in self.spec}
+        return [self._wf32(L["enc1"]), self._b(L["enc1"]), self._w(L["enc2"]), self._b(L["enc2"]),
+                self._w(L["enc_head"]), self._b(L["enc_head"]), self._w(L["dec_fc"]), self._b(L["dec_fc"]),
+                self._w(L["dec1"]), self._b(L["dec1"]), self._wf32(L["dec2"]), self._b(L["dec2"])]
+
+    def _eval_fwd28(self, X, idx, want_recon):
+        """Pointer table of the fused forward over an eval set: the eval state,
+        no activation outputs (train = 0), the reconstruction when wanted."""
+        st = self.state
+        part = self.f28_part
+        bce, kld, db4 = part.narrow(0, 0, self.B), part.narrow(0, self.B, self.B), part.narrow(0, 2 * self.B, self.B)
+        return self._f28_weights() + [X, idx, st.eval_state, st.hparams, self.xb, None, None, self.mulv, self.eps,
+                                      self.z16, None, None, None, self.recon if want_recon else None, bce, kld, db4,
+                                      None]
 
     def _eval_state(self):
         return self.state.eval_state
