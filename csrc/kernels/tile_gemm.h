@@ -196,13 +196,31 @@ __device__ __forceinline__ float gemm_tiles(const AL& A, const BL& B, EPI& epi, 
   float rs = 0.f;
   wave_tiles<NT, NCW, ROWSUM>(A, B, ti * 16, tg * NT * 16, 16, kc0, kc1, acc, &rs);
   if constexpr (KSPLIT > 1) {
+    // split-K combine + epilogue spread over the tile's waves: wave ks sums
+    // (in wave order, the same additions as one wave summing all four) and
+    // finishes VPW of the lane's four rows, so no single wave carries the
+    // whole epilogue's load round trip and stores
     static_assert(NT == 1, "split-K reduction implemented for NT == 1");
+    constexpr int VPW = KSPLIT >= 4 ? 1 : 4 / KSPLIT;
     *reinterpret_cast<f32x4*>(lds + w * 256 + lane * 4) = acc[0];
     __syncthreads();
-    if (ks == 0) {
+    float contrib = 0.f;
+    if (live && ks < 4 / VPW) {
+      const float* base = lds + (w - ks) * 256 + lane * 4 + ks * VPW;
+      const int row0 = ti * 16 + 4 * (lane >> 4) + ks * VPW;
+      int rows[VPW];
+      float v[VPW];
 #pragma unroll
-      for (int s = 1; s < KSPLIT; ++s) acc[0] += *reinterpret_cast<const f32x4*>(lds + (w + s) * 256 + lane * 4);
+      for (int u = 0; u < VPW; ++u) {
+        float t = base[u];
+#pragma unroll
+        for (int s = 1; s < KSPLIT; ++s) t += base[s * 256 + u];
+        v[u] = t;
+        rows[u] = row0 + u;
+      }
+      contrib = epi.template run<VPW>(rows, tg * 16 + (lane & 15), v);
     }
+    return contrib;
   }
   float contrib = 0.f;
   if (live && ks == 0) {
@@ -289,20 +307,43 @@ __device__ __forceinline__ void gemm_tiles32(const AL& A, const BL& B, EPI& epi,
   float rs = 0.f;
   f32x16 acc = wave_tile32<NPW, ROWSUM>(A, B, ti * 32, tj * 32, kp0, kp1, &rs);
   if constexpr (KSPLIT > 1) {
+    // combine + epilogue spread over the tile's KSPLIT waves (see gemm_tiles):
+    // wave ks sums values [ks*VPW, +VPW) of the lane's 16 in wave order and
+    // runs their epilogue (a weight-gradient + Adam epilogue is 3 loads and
+    // 4 stores per value: one wave doing all 16 doubled the block's time)
+    static_assert(16 % KSPLIT == 0, "KSPLIT must divide the 16 values per lane");
+    constexpr int VPW = 16 / KSPLIT;
     float* mine = lds + w * 1024 + lane * 16;
 #pragma unroll
     for (int v = 0; v < 16; v += 4) *reinterpret_cast<f32x4*>(mine + v) = f32x4{acc[v], acc[v + 1], acc[v + 2], acc[v + 3]};
     if constexpr (ROWSUM) lds[WAVES * 1024 + w * 64 + lane] = rs;
     __syncthreads();
-    if (ks == 0) {
+    if (!live) return;
+    const float* base = lds + (w - ks) * 1024 + lane * 16 + ks * VPW;
+    const int col = tj * 32 + (lane & 31);
+    const int rb = ti * 32 + 4 * (lane >> 5);
+    int rows[VPW];
+    float vals[VPW];
 #pragma unroll
-      for (int s = 1; s < KSPLIT; ++s) {
-        const float* o = lds + (w + s) * 1024 + lane * 16;
+    for (int u = 0; u < VPW; ++u) {
+      float t = base[u];
 #pragma unroll
-        for (int v = 0; v < 16; ++v) acc[v] += o[v];
-        if constexpr (ROWSUM) rs += lds[WAVES * 1024 + (w + s) * 64 + lane];
+      for (int s = 1; s < KSPLIT; ++s) t += base[s * 1024 + u];
+      const int v = ks * VPW + u;
+      vals[u] = t;
+      rows[u] = rb + (v & 3) + 8 * (v >> 2);
+    }
+    epi.template run<VPW>(rows, col, vals);
+    if constexpr (ROWSUM) {
+      if (ks == 0 && tj == 0 && (lane >> 5) == 0) {
+#pragma unroll
+        for (int s = 1; s < KSPLIT; ++s) rs += lds[WAVES * 1024 + (w + s) * 64 + lane];
+        const int rr[1] = {ti * 32 + lane};
+        const float vv[1] = {rs};
+        epi.template run<1>(rr, -1, vv);
       }
     }
+    return;
   }
   if (live && ks == 0) {
     const int col = tj * 32 + (lane & 31);

@@ -8,12 +8,12 @@
 //   F2  [mu|lv] = h1 W2^T + b2 ; z = mu + eps*exp(lv/2) (Philox) ; KLD partial ;
 //       h3 = relu(z W3^T + b3) ; cursor++                     (16 rows / block)
 //   F3  logits = h3 W4^T + b4 ; dlogits = sigmoid - x ; BCE partial (logit form)
-//   B1  dh3 = (dlogits W4) . [h3>0]    ||  dW4 = dlogits^T h3, db4
+//   B1  dh3 = (dlogits W4) . [h3>0] (+ its dz split-K slab)
 //   B2  dz = dh3 W3 -> dmu, dlv (reparam + beta-KLD) ; dh1 = ([dmu|dlv] W2) . [h1>0]
-//                                      ||  dW3 = dh3^T z, db3  || loss reduction
+//       ||  dW3 = dh3^T z, db3  ||  dW4 = dlogits^T h3, db4  || loss reduction
 //   B3  dW2 = [dmu|dlv]^T h1, db2      ||  dW1 = dh1^T xb, db1
 //       with fuse_adam: Adam applied in those epilogues, + Adam streamed over
-//       the fc3/fc4 slice of the arena (gradients final since B1/B2). Without
+//       the fc3/fc4 slice of the arena (gradients final since B2). Without
 //       it (intra-group DDP), the bucketed all-reduce runs on the comm stream
 //       and adam.hip updates the whole arena afterwards.
 //
@@ -35,12 +35,20 @@ constexpr int kThreads = kWaves * 64;
 __device__ __forceinline__ int cdiv_d(int a, int b) { return (a + b - 1) / b; }
 
 // Phase timestamps for the profiling tool (obs/stamps.py); a null pointer
-// (production) costs one uniform branch.
+// (production) costs one uniform branch. Slot 7 holds where the wave ran:
+// (XCC id << 16) | HW_ID's CU/SH/SE bits (written with slot 0).
 #define STAMP(K, S)                                                                         \
   do {                                                                                      \
-    if (a.stamps && lane_id() == 0 && blockIdx.x < kStampBlocks)                            \
-      a.stamps[(((size_t)(K) * kStampBlocks + blockIdx.x) * 8 + wave_id()) * 8 + (S)] =     \
-          __builtin_amdgcn_s_memrealtime();                                                 \
+    if (a.stamps && lane_id() == 0 && blockIdx.x < kStampBlocks) {                          \
+      unsigned long long* sp_ = a.stamps + (((size_t)(K) * kStampBlocks + blockIdx.x) * 8 + wave_id()) * 8; \
+      sp_[S] = __builtin_amdgcn_s_memrealtime();                                            \
+      if ((S) == 0) {                                                                       \
+        unsigned hw_, xcc_;                                                                 \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                   \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc_));           \
+        sp_[7] = ((unsigned long long)xcc_ << 16) | (hw_ & 0xff00u);                        \
+      }                                                                                     \
+    }                                                                                       \
   } while (0)
 
 // ------------------------------------------------------------------- F1 ----
@@ -144,17 +152,19 @@ __global__ void __launch_bounds__(kThreads) vae_f1(VaeArgs a) {
     for (int rr = 0; rr < 4; ++rr)
       if (i0 + 4 * q + rr < a.M) a.h1[(size_t)(i0 + 4 * q + rr) * a.H + j] = h[rr];
   }
-  // blocks of tile column 0 materialise their 16 batch rows into xb for F3/B3
-  // (each wave re-reads the K slice it just loaded: L1/L2 hits, no barrier)
-  if (tj == 0) {
-    const int i = i0 + (lane & 15);
-    if (i < a.M) {
-      const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)rows[i] * a.D);
-      float4* dst = reinterpret_cast<float4*>(a.xb + (size_t)i * a.D);
-      for (int c = kc0; c < kc1; ++c) {
-        const int k4 = c * 4 + q;
-        if (k4 * 4 < a.D) dst[k4] = src[k4];
-      }
+  // the TH blocks of a row tile materialise its 16 batch rows into xb for
+  // F3/B3, each a 1/TH column slice (L2-hot lines: the block's waves just
+  // loaded every column of these rows), on the waves the slab step leaves idle.
+  // (Round 4 gave the whole copy to the tile-column-0 blocks: 2.4 us of tail.)
+  if (w >= geo.ntm) {
+    const int d4 = a.D >> 2;
+    const int q0 = (tj * d4) / geo.th, nq = ((tj + 1) * d4) / geo.th - q0;
+    for (int e = (w - geo.ntm) * 64 + lane; e < 16 * nq; e += (kWaves - geo.ntm) * 64) {
+      const int r = e / nq, k4 = q0 + (e - r * nq);
+      const int i = i0 + r;
+      if (i < a.M)
+        reinterpret_cast<float4*>(a.xb + (size_t)i * a.D)[k4] =
+            reinterpret_cast<const float4*>(a.X + (size_t)rows[i] * a.D)[k4];
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -396,11 +406,11 @@ __host__ __device__ inline int wgrad_blocks(int out_rows, int in_cols) {
 #define WGRAD(A, B, EPI, OUT, IN, BLK, LDS) \
   gemm_tiles32<kWaves, kWgTPB, kWgNPW, true>(A, B, EPI, a.M, cdiv_d(OUT, 32), cdiv_d(IN, 32), BLK, LDS)
 
-__global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a, int nblk_dh3) {
-  __shared__ __attribute__((aligned(16))) float lds[kWgLds];
+__global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[kWaves * 256];
   __shared__ __attribute__((aligned(16))) float ht[16][20];
   STAMP(3, 0);
-  if ((int)blockIdx.x < nblk_dh3) {
+  {
     // one 16x16 tile (ti, tj) of dh3 = (dlog W4) . [h3 > 0], K = D over 8 waves;
     // then waves 0..NTZ-1 emit the dz split-K slab dh3[:, tj] W3[tj, :].
     const SlabGeo geo(a.H, a.Z);
@@ -447,12 +457,6 @@ __global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a, int nblk_dh3) {
       for (int rr = 0; rr < 4; ++rr)
         if (i0 + 4 * q + rr < a.M) a.dh3[(size_t)(i0 + 4 * q + rr) * a.H + j] = d[rr];
     }
-  } else {
-    // dW4[D, H] = dlog^T h3 (k = batch), db4 = column sums of dlog
-    ATrans A{a.dlog, a.D, a.D, a.M};
-    BRowMajor Bh{a.h3, a.H, a.H, a.M};
-    EpiWGrad epi{a.gW4, a.gb4, a.H, a.D, a.H};
-    WGRAD(A, Bh, epi, a.D, a.H, blockIdx.x - nblk_dh3, lds);
   }
   STAMP(3, 1);
 }
@@ -462,13 +466,13 @@ __global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a, int nblk_dh3) {
 // sums in LDS), dmu/dlv (reparam + beta-KLD grads), then wave w computes dh1
 // tile g*8+w = ([dmu|dlv] W2) . [h1 > 0] with K = 2Z from LDS; group 0 stores
 // dmulv. Blocks [nrow, nrow + nw3): dW3 = dh3^T z, db3. Last block: loss.
-__global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3) {
+__global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3, int nw4) {
   __shared__ __attribute__((aligned(16))) float red[kWgLds];
   __shared__ __attribute__((aligned(16))) float dml[16][68];  // [row][dmu(Z) | dlv(Z)]
   __shared__ float scratch[16];
   const int bid = blockIdx.x;
   STAMP(4, 0);
-  if (bid >= nrow + nw3) {
+  if (bid >= nrow + nw3 + nw4) {
     // loss = sum(BCE partials) + beta * sum(KLD partials) of this step's forward
     const int nk = cdiv_d(a.M, 16) * kWaves;
     const int nb = cdiv_d(cdiv_d(a.M, 16) * cdiv_d(a.D, 16), 2) * kWaves;
@@ -485,6 +489,16 @@ __global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3)
       st->epoch_loss += (double)loss;
       st->epoch_count += 1.0;
     }
+    return;
+  }
+  if (bid >= nrow + nw3) {
+    // dW4[D, H] = dlog^T h3 (k = batch), db4 = column sums of dlog. Needs only
+    // F2/F3 outputs; here (not in B1 beside the 200 dh3 blocks) the launch
+    // stays within one workgroup per CU
+    ATrans A{a.dlog, a.D, a.D, a.M};
+    BRowMajor Bh{a.h3, a.H, a.H, a.M};
+    EpiWGrad epi{a.gW4, a.gb4, a.H, a.D, a.H};
+    WGRAD(A, Bh, epi, a.D, a.H, bid - nrow - nw3, red);
     return;
   }
   if (bid >= nrow) {
@@ -679,9 +693,9 @@ VaeGrid vae_grid(const VaeArgs& a) {
   g.f2 = ti * geo.groups;
   g.f3 = cdiv(ti * cdiv(a.D, 16), 2);
   g.b1_dh3 = ti * cdiv(a.H, 16);
-  g.b1 = g.b1_dh3 + wgrad_blocks(a.D, a.H);
+  g.b1 = g.b1_dh3;
   g.b2_rows = ti * geo.groups;
-  g.b2 = g.b2_rows + wgrad_blocks(a.H, a.Z) + 1;
+  g.b2 = g.b2_rows + wgrad_blocks(a.H, a.Z) + wgrad_blocks(a.D, a.H) + 1;
   g.b3_w2 = wgrad_blocks(2 * a.Z, a.H);
   g.b3_w1 = wgrad_blocks(a.H, a.D);
   const long long n4 = (a.s_end - a.s_beg) / 4;
@@ -723,9 +737,10 @@ extern "C" int mdt_vae_backward(const VaeArgs* a, hipStream_t s, int part) {
   const int rc = mdt_vae_check(a);
   if (rc) return rc;
   const VaeGrid g = vae_grid(*a);
-  if (part == 0 || part == 1) hipLaunchKernelGGL(vae_b1, dim3(g.b1), dim3(kThreads), 0, s, *a, g.b1_dh3);
+  if (part == 0 || part == 1) hipLaunchKernelGGL(vae_b1, dim3(g.b1), dim3(kThreads), 0, s, *a);
   if (part == 0 || part == 2)
-    hipLaunchKernelGGL(vae_b2, dim3(g.b2), dim3(kThreads), 0, s, *a, g.b2_rows, g.b2 - g.b2_rows - 1);
+    hipLaunchKernelGGL(vae_b2, dim3(g.b2), dim3(kThreads), 0, s, *a, g.b2_rows, wgrad_blocks(a->H, a->Z),
+                       wgrad_blocks(a->D, a->H));
   if (part == 0 || part == 3)
     hipLaunchKernelGGL(vae_b3, dim3(g.b3), dim3(kThreads), 0, s, *a, g.b3_w2, g.b3_w1);
   return (int)hipGetLastError();

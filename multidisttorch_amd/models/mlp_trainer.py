@@ -200,8 +200,8 @@ class MlpVaeTrainer(GraphedEval):
         self.use_graphs = self._graphs_wanted and graph_capturable(reducer)
 
     def bucket_bounds(self, bucket_mb=None):
-        """The fused step finishes gradients in two groups (fc4 after B1, the
-        rest after B3): two buckets, or one when bucket_mb == 0."""
+        """The fused step finishes gradients in two groups (fc4 after B2,
+        the rest after B3): two buckets, or one when bucket_mb == 0."""
         return [0, self.numel] if bucket_mb == 0 else [0, self.split, self.numel]
 
     def default_bucket_bounds(self):
@@ -236,8 +236,8 @@ class MlpVaeTrainer(GraphedEval):
             self.reducer.set_inline(not early)
         if early:
             e.backward(X, idx, M, 1, False)
-            self.reducer.launch(1)          # fc4 bucket: overlaps B2/B3
             e.backward(X, idx, M, 2, False)
+            self.reducer.launch(1)          # fc4 bucket (final after B2): overlaps B3
             e.backward(X, idx, M, 3, False)
             self.reducer.launch(0)
             self.reducer.wait_all()

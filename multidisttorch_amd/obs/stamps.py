@@ -49,9 +49,51 @@ def _ranges(M=128, D=784, H=400, Z=20, fuse=True):
     b2r = ti * cd(cd(H, 16), 8)
     b2w = wg(H, Z)
     b3w2, b3w1 = wg(2 * Z, H), wg(H, D)
-    return {"B1": [("dh3", 0, b1), ("dW4", b1, b1 + wg(D, H))],
-            "B2": [("rows", 0, b2r), ("dW3", b2r, b2r + b2w), ("loss", b2r + b2w, b2r + b2w + 1)],
+    b2w4 = wg(D, H)
+    return {"B1": [("dh3", 0, b1)],
+            "B2": [("rows", 0, b2r), ("dW3", b2r, b2r + b2w), ("dW4", b2r + b2w, b2r + b2w + b2w4),
+                   ("loss", b2r + b2w + b2w4, b2r + b2w + b2w4 + 1)],
             "B3": [("dW2", 0, b3w2), ("dW1", b3w2, b3w2 + b3w1), ("adam", b3w2 + b3w1, BLOCKS)]}
+
+
+def placement(st: np.ndarray) -> dict:
+    """Per kernel: how many CUs ran its blocks, and block durations split by
+    whether another block of the same kernel overlapped it on the same CU
+    (slot 7 = XCC/CU id of the wave, written with slot 0)."""
+    out = {}
+    for k, name in enumerate(KERNELS):
+        s = st[k]
+        v = s[:, 0, 0] > 0
+        if not v.any():
+            continue
+        blocks = np.nonzero(v)[0]
+        t0 = np.where(s[blocks, :, 0] > 0, s[blocks, :, 0], np.iinfo(np.int64).max).min(axis=1)
+        t1 = s[blocks, :, :7].max(axis=(1, 2))
+        cu = s[blocks, 0, 7]
+        shared = np.zeros(len(blocks), bool)
+        per_cu = {}
+        for i, c in enumerate(cu):
+            per_cu.setdefault(int(c), []).append(i)
+        for idxs in per_cu.values():
+            for i in idxs:
+                for j in idxs:
+                    if i != j and t0[i] < t1[j] and t0[j] < t1[i]:
+                        shared[i] = True
+        d = (t1 - t0) * 10e-3
+        rec = dict(blocks=int(len(blocks)), cus=len(per_cu), max_blocks_per_cu=max(len(x) for x in per_cu.values()),
+                   shared_blocks=int(shared.sum()))
+        for lab, m in (("alone", ~shared), ("shared", shared)):
+            if m.any():
+                rec[f"dur_{lab}_median_us"] = float(np.median(d[m]))
+                rec[f"dur_{lab}_max_us"] = float(d[m].max())
+        for label, lo, hi in _ranges().get(name, []):
+            m = (blocks >= lo) & (blocks < hi)
+            if m.any():
+                rec[f"{label}_shared"] = int((shared & m).sum())
+                rec[f"{label}_n"] = int(m.sum())
+                rec[f"{label}_start_last_us"] = float((t0[m].max() - t0.min()) * 10e-3)
+        out[name] = rec
+    return out
 
 
 def analyse(st: np.ndarray) -> dict:
@@ -94,7 +136,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
     a = ap.parse_args(argv)
-    res = analyse(collect())
+    st = collect()
+    res = analyse(st)
+    res["placement"] = placement(st)
     print(json.dumps(res, indent=1))
     if a.json:
         with open(a.json, "w") as f:
