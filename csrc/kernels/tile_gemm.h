@@ -27,6 +27,7 @@
 
 namespace mdt {
 
+
 struct Frag {  // a lane's bound operand row/column
   const float* base;
   float mask;
@@ -289,9 +290,16 @@ __device__ __forceinline__ f32x16 wave_tile32(const AL& A, const BL& B, int i0, 
 // Block of WAVES waves: TPB 32x32 tiles per block, KSPLIT = WAVES/TPB waves
 // per tile. Epilogue run<16>(rows, col, v) per lane (see gemm_tiles); with
 // ROWSUM run<1>({i}, -1, {rowsum}) from the tiles of column 0. `lds` must hold WAVES*1024 floats.
+// `stamp` (profiling only, obs/stamps.py): the wave's stamp row; slots 2 and 3
+// get the time after the wave's GEMM and after the combine barrier.
+__device__ __forceinline__ void stamp_at(unsigned long long* row, int slot) {
+  if (row && lane_id() == 0) row[slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 template <int WAVES, int TPB, int NPW, bool ROWSUM, class AL, class BL, class EPI>
 __device__ __forceinline__ void gemm_tiles32(const AL& A, const BL& B, EPI& epi, int K, int tiles_i,
-                                             int tiles_j, int blk, float* lds) {
+                                             int tiles_j, int blk, float* lds,
+                                             unsigned long long* stamp = nullptr) {
   constexpr int KSPLIT = WAVES / TPB;
   static_assert(KSPLIT * TPB == WAVES, "WAVES must be a multiple of TPB");
   const int w = __builtin_amdgcn_readfirstlane(wave_id());

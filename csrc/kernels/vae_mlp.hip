@@ -405,6 +405,11 @@ __host__ __device__ inline int wgrad_blocks(int out_rows, int in_cols) {
 }
 #define WGRAD(A, B, EPI, OUT, IN, BLK, LDS) \
   gemm_tiles32<kWaves, kWgTPB, kWgNPW, true>(A, B, EPI, a.M, cdiv_d(OUT, 32), cdiv_d(IN, 32), BLK, LDS)
+#define WGRAD_ST(A, B, EPI, OUT, IN, BLK, LDS, K)                                                     \
+  gemm_tiles32<kWaves, kWgTPB, kWgNPW, true>(                                                         \
+      A, B, EPI, a.M, cdiv_d(OUT, 32), cdiv_d(IN, 32), BLK, LDS,                                      \
+      (a.stamps && blockIdx.x < kStampBlocks)                                                         \
+          ? a.stamps + (((size_t)(K) * kStampBlocks + blockIdx.x) * 8 + wave_id()) * 8 : nullptr)
 
 __global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[kWaves * 256];
@@ -642,7 +647,7 @@ __global__ void __launch_bounds__(kThreads) vae_b3(VaeArgs a, int nblk_w2, int n
     ATrans A{a.dh1, a.H, a.H, a.M};
     BRowMajor Bx{a.xb, a.D, a.D, a.M};
     EpiWGradAdam epi{a.G, a.P, a.Mo, a.Vo, a.oW1, a.ob1, a.D, a.H, a.D, c};
-    WGRAD(A, Bx, epi, a.H, a.D, bid - nblk_w2, lds);
+    WGRAD_ST(A, Bx, epi, a.H, a.D, bid - nblk_w2, lds, 5);
   } else {
     const int nb = gridDim.x - nblk_w2 - nblk_w1;
     adam_stream(a.P, a.G, a.Mo, a.Vo, a.s_beg, a.s_end, bid - nblk_w2 - nblk_w1, nb, c);

@@ -135,8 +135,11 @@ def analyse(st: np.ndarray) -> dict:
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
+    ap.add_argument("--raw", default=None, help="save the raw stamp array (.npy)")
     a = ap.parse_args(argv)
     st = collect()
+    if a.raw:
+        np.save(a.raw, st)
     res = analyse(st)
     res["placement"] = placement(st)
     print(json.dumps(res, indent=1))
