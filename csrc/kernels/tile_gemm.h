@@ -138,6 +138,10 @@ __device__ __forceinline__ void wave_tiles(const AL& A, const BL& B, int i0, int
 #pragma unroll
       for (int t = 0; t < NT; ++t) B.load(fb[t], k0, b[t][u]);
     }
+    // every load of the round is issued before the first MFMA waits: left
+    // alone the scheduler sinks the later chunks' loads between the MFMAs,
+    // each behind its own vmcnt(0) (one round trip per chunk)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < NCW; ++u) {
       if constexpr (ROWSUM) rs += (a[u][0] + a[u][1]) + (a[u][2] + a[u][3]);
@@ -270,6 +274,7 @@ __device__ __forceinline__ f32x16 wave_tile32(const AL& A, const BL& B, int i0, 
       a[u] = A.load1(fa, k, p < kp1 ? 1.f : 0.f);
       b[u] = B.load1(fb, k);
     }
+    __builtin_amdgcn_sched_barrier(0);  // all loads of the round first (see wave_tiles)
 #pragma unroll
     for (int u = 0; u < NPW; u += 2) {
       acc0 = mfma32x32x2(a[u], b[u], acc0);

@@ -113,17 +113,21 @@ __global__ void __launch_bounds__(kThreads) vae_f1(VaeArgs a) {
   const int i0 = ti * 16, j = tj * 16 + (lane & 15);
   const int q = lane >> 4;
   const int Z2 = 2 * a.Z;
-  // prefetch: bias, and the W2 slice this wave multiplies in the slab step
+  // The cursor heads the launch's one dependent chain (cursor -> batch row
+  // index -> image row), so it is loaded first; the bias and the W2 slice of
+  // the slab step are prefetched raw and masked only where they are used, so
+  // no wait for them lands in front of the GEMM's loads.
+  const int cursor = a.st->cursor;
   const float bj = a.b1[min(j, a.H - 1)];
-  float wb[4] = {0.f, 0.f, 0.f, 0.f};
+  float4 w2v = {0.f, 0.f, 0.f, 0.f};
+  float w2m = 0.f;
   if (w < geo.ntm) {
     const int n = w * 16 + (lane & 15);
     const int k0 = tj * 16 + 4 * q;
-    const float4 v = *reinterpret_cast<const float4*>(a.W2 + (size_t)min(n, Z2 - 1) * a.H + min(k0, a.H - 4));
-    const float m = (n < Z2 && k0 < a.H) ? 1.f : 0.f;
-    wb[0] = v.x * m; wb[1] = v.y * m; wb[2] = v.z * m; wb[3] = v.w * m;
+    w2v = *reinterpret_cast<const float4*>(a.W2 + (size_t)min(n, Z2 - 1) * a.H + min(k0, a.H - 4));
+    w2m = (n < Z2 && k0 < a.H) ? 1.f : 0.f;
   }
-  const int* rows = a.idx + (size_t)a.st->cursor * a.B;
+  const int* rows = a.idx + (size_t)cursor * a.B;
   ARowGather A{a.X, rows, a.D, a.M, a.D};
   BWeightNT Bw{a.W1, a.D, a.H, a.D};
   const int nch = cdiv_d(a.D, 16);
@@ -142,6 +146,7 @@ __global__ void __launch_bounds__(kThreads) vae_f1(VaeArgs a) {
   __syncthreads();
   STAMP(0, 1);
   if (w < geo.ntm) {
+    const float wb[4] = {w2v.x * w2m, w2v.y * w2m, w2v.z * w2m, w2v.w * w2m};
     const f32x4 sl = lds_tile_mma(ht, wb);
     float* dst = a.slab_mv + ((size_t)(ti * geo.th + tj) * 16) * geo.sw + w * 16 + (lane & 15);
 #pragma unroll
@@ -195,15 +200,16 @@ __global__ void __launch_bounds__(kThreads) vae_f2(VaeArgs a) {
   // prefetch: W3 fragments (K = Z <= 32 -> 2 chunks) and b3 for this wave's tile
   const int jt = g * kWaves + w;
   const int j = jt * 16 + (lane & 15);
-  float wb[2][4];
+  // (raw prefetch, masked where used: no wait in front of the slab loads)
+  float4 w3v[2];
+  float w3m[2];
   {
     const float* wr = a.W3 + (size_t)min(j, a.H - 1) * a.Z;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int k0 = c * 16 + 4 * q;
-      const float4 v = *reinterpret_cast<const float4*>(wr + min(k0, a.Z - 4));
-      const float m = (j < a.H && k0 < a.Z) ? 1.f : 0.f;
-      wb[c][0] = v.x * m; wb[c][1] = v.y * m; wb[c][2] = v.z * m; wb[c][3] = v.w * m;
+      w3v[c] = *reinterpret_cast<const float4*>(wr + min(k0, a.Z - 4));
+      w3m[c] = (j < a.H && k0 < a.Z) ? 1.f : 0.f;
     }
   }
   const float bj = a.b3[min(j, a.H - 1)];
@@ -217,13 +223,15 @@ __global__ void __launch_bounds__(kThreads) vae_f2(VaeArgs a) {
       const int r = pr / quads, cq = pr - r * quads;
       const float4* base = reinterpret_cast<const float4*>(a.slab_mv + ((size_t)(ti * geo.th) * 16 + r) * geo.sw) + cq;
       const size_t sstride = (size_t)16 * geo.sw / 4;
+      float4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = base[min(half * 16 + u, geo.th - 1) * sstride];
+      __builtin_amdgcn_sched_barrier(0);  // all 16 slab loads in flight before the first add
       float4 acc4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
-        const int sidx = half * 16 + u;
-        const float4 v = base[min(sidx, geo.th - 1) * sstride];
-        const float m = sidx < geo.th ? 1.f : 0.f;
-        acc4.x += v.x * m; acc4.y += v.y * m; acc4.z += v.z * m; acc4.w += v.w * m;
+        const float m = half * 16 + u < geo.th ? 1.f : 0.f;
+        acc4.x += v[u].x * m; acc4.y += v[u].y * m; acc4.z += v[u].z * m; acc4.w += v[u].w * m;
       }
       *reinterpret_cast<float4*>(&part[half][r][cq * 4]) = acc4;
     }
@@ -263,10 +271,10 @@ __global__ void __launch_bounds__(kThreads) vae_f2(VaeArgs a) {
       const int k0 = cc * 16 + 4 * q;
       const float4 av = *reinterpret_cast<const float4*>(&zt[rr0][min(k0, 32)]);
       const bool in = k0 < a.Z;  // select, not multiply: unwritten LDS may hold NaN bits
-      acc = mfma16x16x4(in ? av.x : 0.f, wb[cc][0], acc);
-      acc = mfma16x16x4(in ? av.y : 0.f, wb[cc][1], acc);
-      acc = mfma16x16x4(in ? av.z : 0.f, wb[cc][2], acc);
-      acc = mfma16x16x4(in ? av.w : 0.f, wb[cc][3], acc);
+      acc = mfma16x16x4(in ? av.x : 0.f, w3v[cc].x * w3m[cc], acc);
+      acc = mfma16x16x4(in ? av.y : 0.f, w3v[cc].y * w3m[cc], acc);
+      acc = mfma16x16x4(in ? av.z : 0.f, w3v[cc].z * w3m[cc], acc);
+      acc = mfma16x16x4(in ? av.w : 0.f, w3v[cc].w * w3m[cc], acc);
     }
     if (j < a.H) {
 #pragma unroll
@@ -426,13 +434,15 @@ __global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a) {
     float mk[4];
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) mk[rr] = a.h3[(size_t)min(i0 + 4 * q + rr, a.M - 1) * a.H + min(j, a.H - 1)];
-    float wb[4] = {0.f, 0.f, 0.f, 0.f};
+    // raw prefetch, masked where used (no wait in front of the GEMM's loads)
+    float wr[4] = {0.f, 0.f, 0.f, 0.f}, wm[4] = {0.f, 0.f, 0.f, 0.f};
     if (w < geo.ntz) {  // B(k, n) = W3[(tj*16 + k) * Z + w*16 + n]
       const int n = w * 16 + (lane & 15);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int k = tj * 16 + 4 * q + t;
-        wb[t] = a.W3[(size_t)min(k, a.H - 1) * a.Z + min(n, a.Z - 1)] * ((k < a.H && n < a.Z) ? 1.f : 0.f);
+        wr[t] = a.W3[(size_t)min(k, a.H - 1) * a.Z + min(n, a.Z - 1)];
+        wm[t] = (k < a.H && n < a.Z) ? 1.f : 0.f;
       }
     }
     ARowMajor A{a.dlog, a.D, a.M, a.D};
@@ -452,6 +462,7 @@ __global__ void __launch_bounds__(kThreads) vae_b1(VaeArgs a) {
     }
     __syncthreads();
     if (w < geo.ntz) {
+      const float wb[4] = {wr[0] * wm[0], wr[1] * wm[1], wr[2] * wm[2], wr[3] * wm[3]};
       const f32x4 sl = lds_tile_mma(ht, wb);
       float* dst = a.slab_dz + ((size_t)(ti * geo.th + tj) * 16) * geo.swz + w * 16 + (lane & 15);
 #pragma unroll
@@ -523,13 +534,13 @@ __global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3,
   const int j = jt * 16 + (lane & 15);
   // prefetch: W2 fragments (K = 2Z <= 64 -> up to 4 chunks), h1 mask, and
   // this thread's mu / lv / eps
-  float wb[4][4];
+  float wb[4][4];  // raw; masked where used (no wait in front of the slab loads)
 #pragma unroll
   for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int k = cc * 16 + 4 * q + t;
-      wb[cc][t] = a.W2[(size_t)min(k, Z2 - 1) * a.H + min(j, a.H - 1)] * ((k < Z2 && j < a.H) ? 1.f : 0.f);
+      wb[cc][t] = a.W2[(size_t)min(k, Z2 - 1) * a.H + min(j, a.H - 1)];
     }
   float mk[4];
 #pragma unroll
@@ -557,13 +568,15 @@ __global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3,
       const int rr = pr / quads, cq = pr - rr * quads;
       const float4* base = reinterpret_cast<const float4*>(a.slab_dz + ((size_t)(ti * geo.th) * 16 + rr) * geo.swz) + cq;
       const size_t sstride = (size_t)16 * geo.swz / 4;
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = base[min(qq * 8 + u, geo.th - 1) * sstride];
+      __builtin_amdgcn_sched_barrier(0);  // all slab loads in flight before the first add
       float4 acc4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int sidx = qq * 8 + u;
-        const float4 v = base[min(sidx, geo.th - 1) * sstride];
-        const float m = sidx < geo.th ? 1.f : 0.f;
-        acc4.x += v.x * m; acc4.y += v.y * m; acc4.z += v.z * m; acc4.w += v.w * m;
+        const float m = qq * 8 + u < geo.th ? 1.f : 0.f;
+        acc4.x += v[u].x * m; acc4.y += v[u].y * m; acc4.z += v[u].z * m; acc4.w += v[u].w * m;
       }
       *reinterpret_cast<float4*>(&part[(qq * 16 + rr) * geo.swz + cq * 4]) = acc4;
     }
@@ -595,10 +608,13 @@ __global__ void __launch_bounds__(kThreads) vae_b2(VaeArgs a, int nrow, int nw3,
       const int k0 = cc * 16 + 4 * q;
       const float4 av = *reinterpret_cast<const float4*>(&dml[rr0][min(k0, 64)]);
       const bool in = k0 < Z2;  // select, not multiply: unwritten LDS may hold NaN bits
-      acc = mfma16x16x4(in ? av.x : 0.f, wb[cc][0], acc);
-      acc = mfma16x16x4(in ? av.y : 0.f, wb[cc][1], acc);
-      acc = mfma16x16x4(in ? av.z : 0.f, wb[cc][2], acc);
-      acc = mfma16x16x4(in ? av.w : 0.f, wb[cc][3], acc);
+      float b[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) b[t] = wb[cc][t] * ((k0 + t < Z2 && j < a.H) ? 1.f : 0.f);
+      acc = mfma16x16x4(in ? av.x : 0.f, b[0], acc);
+      acc = mfma16x16x4(in ? av.y : 0.f, b[1], acc);
+      acc = mfma16x16x4(in ? av.z : 0.f, b[2], acc);
+      acc = mfma16x16x4(in ? av.w : 0.f, b[3], acc);
     }
     if (j < a.H) {
 #pragma unroll
