@@ -30,6 +30,7 @@ __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, P
   if (!pc.pair) {
     const int n = blockIdx.x;
     fwd_body<StepLayout>(fa, lds, n);
+    if (!fa.train) return;  // eval: forward only
     lds_barrier();
     bwd_body<StepLayout, true>(ba, lds, n);
     return;
@@ -70,6 +71,7 @@ __global__ void __launch_bounds__(kThreads) f28_step_k(FwdArgs fa, BwdArgs ba, P
   if (mode == kModeExit) return;
   if (mode == kModeSolo) {
     fwd_rest<StepLayout>(fa, lds, n);
+    if (!fa.train) return;  // eval: forward only
     lds_barrier();
     bwd_body<StepLayout, true>(ba, lds, n);
     return;
@@ -185,6 +187,27 @@ int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train
 }
 
 int mdt_f28_pair_words() { return f28::kXW; }
+
+// Forward only (eval: train = 0) through the step kernel's paired form: two
+// workgroups per sample, so an eval batch of M samples fills 2M CUs instead of
+// the solo f28_fwd_k's M. Same arithmetic as the solo forward (the paired and
+// solo forms are bitwise equal); the backward half of the kernel is skipped.
+int mdt_f28_forward_pair(const long long* p, const long long* pp, int B, int M, unsigned stream, hipStream_t s) {
+  if (M <= 0 || M > B) return 1;
+  if (!pp || !pp[0] || !pp[1] || !pp[2]) return 2;
+  f28::FwdArgs fa{};
+  fill_fwd(fa, p, B, stream, 0);
+  fa.pf_slices = 0;
+  f28::BwdArgs ba{};
+  f28::PairCtl pc{};
+  pc.M = M;
+  pc.pair = 1;
+  pc.xg = P<unsigned long long>(pp, 0);
+  pc.pairw = P<int>(pp, 1);
+  pc.err = P<unsigned>(pp, 2);
+  hipLaunchKernelGGL(f28::f28_step_k, dim3(2 * M), dim3(f28::kThreads), 0, s, fa, ba, pc);
+  return (int)hipGetLastError();
+}
 
 // One launch per training step: forward then backward, two workgroups per
 // sample when `pair` (pp = pair table), else one.

@@ -627,6 +627,9 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
     TF(kTKld)[0] = Scr[0];
     if (float* d4 = TF(kTDb4)) d4[0] = sg;
   }
+  // eval (forward only): both halves end here; X1-X3 are consumed (cleared),
+  // X4-X6 never written, so the granules are zero for the next launch
+  if (!train) return;
 
   pstamp(8);
   // ---- Q1: dec2 backward-data on own channels (8 per thread) x dec1 ReLU mask; X4 publishes gd1

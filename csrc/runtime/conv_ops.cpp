@@ -70,6 +70,7 @@ int mdt_pack_jobs_multi(const mdt::JobBlob* jobs, int n, void* dst);
 int mdt_pack_jobs_multi_stamps(void* img, void* stamps);
 int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s);
 int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train, hipStream_t s);
+int mdt_f28_forward_pair(const long long* p, const long long* pp, int B, int M, unsigned stream, hipStream_t s);
 int mdt_f28_backward(const long long* p, int M, hipStream_t s);
 int mdt_f28_step(const long long* pf, const long long* pb, const long long* pp, int B, int M, unsigned stream,
                  int pair, int delay_us, hipStream_t s);
@@ -460,11 +461,27 @@ void f28_check_data(const std::vector<c10::optional<at::Tensor>>& t, int64_t B) 
   TORCH_CHECK(t[13]->numel() % B == 0, "f28: idx must hold whole batches of ", B, ", has ", t[13]->numel());
 }
 
-void f28_forward(const std::vector<c10::optional<at::Tensor>>& t, int64_t B, int64_t M, int64_t stream, bool train) {
+std::vector<long long> f28_pair_ptrs(const std::vector<c10::optional<at::Tensor>>& pair, int64_t M, int dev) {
+  const std::vector<Slot> ps = {{"xchg", 'l', 2 * (int64_t)mdt_f28_pair_words(), false, false},
+                                {"pairw", 'i', 1, false, false},
+                                {"err", 'i', 1, true, false}};
+  return f28_ptrs(pair, ps, M, dev);
+}
+
+// `pair` (eval only, train = false): the same three tensors as f28_step's;
+// the forward then runs two workgroups per sample (mdt_f28_forward_pair).
+void f28_forward(const std::vector<c10::optional<at::Tensor>>& t, int64_t B, int64_t M, int64_t stream, bool train,
+                 const std::vector<c10::optional<at::Tensor>>& pair) {
   TORCH_CHECK(M > 0 && M <= B, "f28_forward: bad M ", M, " for B ", B);
+  TORCH_CHECK(pair.empty() || !train, "f28_forward: the paired forward is eval-only");
   f28_check_data(t, B);
   const int dev = t[0].has_value() ? (int)t[0]->device().index() : 0;
   const auto p = f28_ptrs(t, f28_fwd_slots(B, train), M, dev);
+  if (!pair.empty()) {
+    const auto pp = f28_pair_ptrs(pair, M, dev);
+    rc(mdt_f28_forward_pair(p.data(), pp.data(), (int)B, (int)M, (unsigned)stream, cur()), "f28_forward(pair)");
+    return;
+  }
   rc(mdt_f28_forward(p.data(), (int)B, (int)M, (unsigned)stream, train ? 1 : 0, cur()), "f28_forward");
 }
 
@@ -488,12 +505,7 @@ void f28_step(const std::vector<c10::optional<at::Tensor>>& tf, const std::vecto
   const auto pf = f28_ptrs(tf, f28_fwd_slots(B, true), M, dev);
   const auto pb = f28_ptrs(tb, f28_bwd_slots(), M, dev);
   std::vector<long long> pp;
-  if (!pair.empty()) {
-    const std::vector<Slot> ps = {{"xchg", 'l', 2 * (int64_t)mdt_f28_pair_words(), false, false},
-                                  {"pairw", 'i', 1, false, false},
-                                  {"err", 'i', 1, true, false}};
-    pp = f28_ptrs(pair, ps, M, dev);
-  }
+  if (!pair.empty()) pp = f28_pair_ptrs(pair, M, dev);
   rc(mdt_f28_step(pf.data(), pb.data(), pp.empty() ? nullptr : pp.data(), (int)B, (int)M, (unsigned)stream,
                   pp.empty() ? 0 : 1, (int)pair_delay_us, cur()),
      "f28_step");
@@ -716,7 +728,7 @@ void bind_conv(pybind11::module& m) {
   m.def("pack_jobs_multi", &pack_jobs_multi, py::arg("jobs"), py::arg("stamps") = py::none());
   m.def("launch_jobs_multi", &launch_jobs_multi);
   m.def("f28_forward", &f28_forward, py::arg("tensors"), py::arg("B"), py::arg("M"), py::arg("stream"),
-        py::arg("train"));
+        py::arg("train"), py::arg("pair") = std::vector<c10::optional<at::Tensor>>{});
   m.def("f28_backward", &f28_backward, py::arg("tensors"), py::arg("M"));
   m.def("f28_pair_words", &mdt_f28_pair_words);
   m.def("f28_step", &f28_step, py::arg("fwd_tensors"), py::arg("bwd_tensors"), py::arg("B"), py::arg("M"),

@@ -263,6 +263,8 @@ class ConvVaeTrainer(GraphedEval):
         # the merged step with two workgroups per sample (conv28_pair.h): a
         # B = 128 trial fills all 256 CUs instead of 128. MDT_F28_PAIR=0 (A/B): one per sample
         self.f28_pair = os.getenv("MDT_F28_PAIR", "1") != "0"
+        # eval passes through the same paired form, forward only (MDT_F28_EVAL_PAIR=0: solo f28_fwd_k)
+        self._eval_pair = os.getenv("MDT_F28_EVAL_PAIR", "1") != "0"
         # DDP on the fused 28x28 step: the decoder bucket goes out before the
         # encoder weight gradients (True), or every bucket after the whole
         # backward on one stream (False); "auto" (default): overlap only when
@@ -1437,8 +1439,10 @@ class ConvVaeTrainer(GraphedEval):
             # layer path's dozen; its loss job advances the eval step exactly
             # like the layer path's step_begin (same Philox keys, same ring slot)
             bce, kld = self.f28_part.narrow(0, 0, self.B), self.f28_part.narrow(0, self.B, self.B)
+            # paired (two workgroups per sample, 2M CUs) unless MDT_F28_EVAL_PAIR=0
+            pair = [self.f28_xg, self.f28_pairw, self.f28_err] if self.f28_pair and self._eval_pair else []
             self.C.f28_forward(self._eval_fwd28(X, idx, want_recon), self.B, M, EVAL_STREAM + self.rng_stream,
-                               False)
+                               False, pair=pair)
             self.C.loss_finalize2(bce, M, kld, M, st.eval_state, st.hparams, True, advance_step=True)
             return
         self._forward_hip(M, st.eval_state, EVAL_STREAM + self.rng_stream, want_recon=want_recon, train=False,

@@ -57,3 +57,39 @@ def test_graphed_eval_is_bitwise_eager(kind, native_ext):
         assert a[3]["cursor"] == b[3]["cursor"] and a[3]["step"] == b[3]["step"]
         if a[1] is not None:
             assert torch.equal(a[1], b[1])
+
+
+def test_conv28_paired_eval_is_bitwise_solo(native_ext, monkeypatch):
+    """The eval forward through the step kernel's paired form (two workgroups
+    per sample, backward skipped) equals the solo f28_fwd_k pass bit for bit,
+    with a tail batch, and leaves the pair state clean (error word 0, a
+    training step after it still pairs)."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(11)
+    Xtr = torch.rand(512, 784, generator=g).to(dev)
+    Xte = torch.rand(300, 784, generator=g).to(dev)
+    idx_tr = torch.arange(512, dtype=torch.int32, device=dev)
+    out = {}
+    for pair in ("0", "1"):
+        monkeypatch.setenv("MDT_F28_EVAL_PAIR", pair)
+        tr = _make("conv28", True, dev)
+        assert tr._eval_pair == (pair == "1") and tr.f28_pair
+        tr.bind_train_data(Xtr, idx_tr)
+        tr.set_cursor(0, 4)
+        tr.train_steps(2)
+        res = []
+        for want in (True, False):
+            total, first = tr.evaluate(Xte, torch.arange(300, dtype=torch.int32, device=dev), want_first_recon=want)
+            torch.cuda.synchronize()
+            res.append((total, None if first is None else first.cpu(), tr.loss_history(eval=True)[:3].copy()))
+        tr.train_steps(2)
+        torch.cuda.synchronize()
+        assert int(tr.f28_err.item()) == 0
+        res.append(tr.params.cpu())
+        out[pair] = res
+    for a, b in zip(out["0"][:2], out["1"][:2]):
+        assert a[0] == b[0], (a[0], b[0])
+        np.testing.assert_array_equal(a[2], b[2])
+        if a[1] is not None:
+            assert torch.equal(a[1], b[1])
+    assert torch.equal(out["0"][2], out["1"][2])
