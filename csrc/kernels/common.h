@@ -76,6 +76,19 @@ __device__ __forceinline__ float normal_from_bits(uint32_t a, uint32_t b) {
   return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
 }
 
+// Write-through stores for a kernel's large outputs that the NEXT launch
+// reads. Plain stores leave their lines dirty in the XCD's L2 until the
+// end-of-kernel release writes them back -- a tail of ~bytes / 6 TB/s after
+// the last wave (~2 us behind a 17 MB bf16 activation, profiles/r5_wt_stores)
+// that nothing overlaps. An agent-scope relaxed atomic store lowers to
+// `global_store ... sc1`: the bytes go out while the rest of the grid still
+// computes. Used where measured faster (the direct convs' bf16 outputs); the
+// thin convs' outputs and f32 outputs measured no better (the consumer then
+// reads from the Infinity Cache instead of L2).
+__device__ __forceinline__ void st_wt8(void* p, unsigned long long v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Slow path of the xGMI all-reduce waits (p2p_allreduce.hip, comm_jobs.h),
 // called by every lane of the polling wave after an unsuccessful poll: true
 // (wave-uniform) when a wait already failed (`status` != 0, this or an earlier
