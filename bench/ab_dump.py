@@ -28,9 +28,10 @@ def dump(model: str, out: str, steps: int):
     from multidisttorch_amd.ops import native
 
     dev = torch.device("cuda", 0)
-    B = 128
+    B = 64 if model == "conv128" else 128
+    D = 128 * 128 if model == "conv128" else 784
     n = 6 * B + 40  # six full batches and a tail of 40
-    X = torch.rand(n, 784, generator=torch.Generator().manual_seed(5)).to(dev)
+    X = torch.rand(n, D, generator=torch.Generator().manual_seed(5)).to(dev)
     idx = torch.randperm(n, generator=torch.Generator().manual_seed(6)).to(torch.int32).to(dev)
     if model == "mlp":
         from multidisttorch_amd.models.mlp_trainer import MlpVaeTrainer
@@ -39,7 +40,9 @@ def dump(model: str, out: str, steps: int):
     else:
         from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
 
-        tr = ConvVaeTrainer(batch_size=B, image=28, z=32, device=dev, backend="hip", seed=3, use_graphs=False)
+        im = 128 if model == "conv128" else 28
+        tr = ConvVaeTrainer(batch_size=B, image=im, z=64 if im == 128 else 32, device=dev, backend="hip", seed=3,
+                            use_graphs=False)
     tr.bind_train_data(X, idx)
     tr.set_cursor(0, 7)
     tr.train_steps(steps)  # eager
@@ -69,7 +72,7 @@ def compare(a: str, b: str) -> int:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="mlp", choices=["mlp", "conv28"])
+    ap.add_argument("--model", default="mlp", choices=["mlp", "conv28", "conv128"])
     ap.add_argument("--out")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--compare", nargs=2)

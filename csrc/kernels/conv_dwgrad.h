@@ -212,17 +212,43 @@ __device__ __forceinline__ void dwgrad_body(const DwArgs& a, uint8_t* lds, int b
         for (int v = 0; v < 16; ++v) acc[i][j][v] += xg[((i * FN + j) * 16 + v) * 64 + lane];
   }
   dc_stamp(a.stamps, 3);
-  // partial row n: [CO][ky*4 + kx][C]
-  float* out = a.out + (size_t)n * CO * CF::K2 + (size_t)(ky * 4 + kx) * C;
+  // partial row n: [CO][ky*4 + kx][C]. It leaves through 16-B write-through
+  // (sc1) buffer stores, like the im2col weight-gradient slabs
+  // (conv_igemm_dev.h wgrad_epilogue): each 32x32 fragment is transposed
+  // through a wave-private LDS tile (row pitch 40 floats: the two half-waves'
+  // rows land on different banks) so a lane holds 4 consecutive columns.
+  // KS == 2 stages in this wave's own exchange slot (it has just read it);
+  // KS == 1 waits for every wave to leave the ring first.
+  if constexpr (CF::KS == 1) __syncthreads();
+  constexpr int PITCH = 40;
+  static_assert(4 * 32 * PITCH * 4 <= CF::LDS && (CF::KS == 1 || 32 * PITCH <= FM * FN * 16 * 64), "dwgrad staging");
+  float* stg = reinterpret_cast<float*>(lds) + (size_t)kx * (CF::KS == 2 ? FM * FN * 16 * 64 : 32 * PITCH);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(a.out + (size_t)n * CO * CF::K2, 0, CO * CF::K2 * 4, 0x00020000);
+  typedef unsigned uvec4 __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-    for (int fn = 0; fn < FN; ++fn)
+    for (int fn = 0; fn < FN; ++fn) {
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int co = fm * 32 + (v & 3) + 8 * (v >> 2) + 4 * half;
-        out[(size_t)co * CF::K2 + fn * 32 + (lane & 31)] = acc[fm][fn][v];
+      for (int v = 0; v < 16; ++v) stg[((v & 3) + 8 * (v >> 2) + 4 * half) * PITCH + (lane & 31)] = acc[fm][fn][v];
+      __builtin_amdgcn_wave_barrier();  // one wave's LDS ops run in order; keep the compiler's too
+      f32x4 t[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = r * 64 + lane;
+        t[r] = *reinterpret_cast<const f32x4*>(stg + (i >> 3) * PITCH + 4 * (i & 7));
       }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = r * 64 + lane;
+        const int co = fm * 32 + (i >> 3);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uvec4, t[r]), rs,
+                                               (co * CF::K2 + (ky * 4 + kx) * C + fn * 32 + 4 * (i & 7)) * 4, 0,
+                                               16 /* sc1 */);
+      }
+    }
   dc_stamp(a.stamps, 4);
 }
 
