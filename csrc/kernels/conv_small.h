@@ -146,10 +146,19 @@ struct CombineReparamArgs {
 // `red` >= 1024 + 16 floats (16-B aligned)
 __device__ __forceinline__ void combine_reparam_rows_body(const CombineReparamArgs& a, float* red, int i) {
   const int Z = a.Z, W = 2 * Z, RG = 1024 / W, t = threadIdx.x;
+  const bool own = t < Z;
+  // the step, seeds and bias before the slab sum: loaded after it they were a
+  // second dependent round trip at the kernel's end
+  const long long stp = a.st->step - 1;
+  const uint32_t seed_lo = a.hp->seed_lo, seed_hi = a.hp->seed_hi;
+  float bm = 0.f, bl = 0.f;
+  if (own && a.bias) {
+    bm = a.bias[t];
+    bl = a.bias[Z + t];
+  }
   combine_rows_partial(a.slab, a.ks, (long long)a.B * W, (long long)i * W, W, red);
   __syncthreads();
   float kl = 0.f, mu = 0.f, lv = 0.f, ep = 0.f, zz = 0.f;
-  const bool own = t < Z;
   if (own) {
     const int c = t;
     for (int r = 0; r < RG; ++r) {
@@ -157,13 +166,12 @@ __device__ __forceinline__ void combine_reparam_rows_body(const CombineReparamAr
       lv += red[r * W + Z + c];
     }
     if (a.bias) {
-      mu += a.bias[c];
-      lv += a.bias[Z + c];
+      mu += bm;
+      lv += bl;
     }
-    const long long stp = a.st->step - 1;
     const u32x4 bits = philox4x32_10(u32x4{(uint32_t)(i * Z + c), a.stream, (uint32_t)((unsigned long long)stp & 0xffffffffu),
                                            (uint32_t)((unsigned long long)stp >> 32)},
-                                     a.hp->seed_lo, a.hp->seed_hi);
+                                     seed_lo, seed_hi);
     ep = normal_from_bits(bits.x, bits.y);
     const float sd = expf(0.5f * lv);
     zz = mu + ep * sd;
@@ -248,18 +256,20 @@ struct CombineReparamBwdArgs {
 // `red` >= 1024 floats (16-B aligned)
 __device__ __forceinline__ void combine_reparam_bwd_rows_body(const CombineReparamBwdArgs& a, float* red, int i) {
   const int Z = a.Z, RG = 1024 / Z, t = threadIdx.x;
+  // this lane's mu / logvar / eps and beta before the slab sum (one round trip
+  // fewer at the kernel's end)
+  const int c = t < Z ? t : 0, e = i * Z + c;
+  const float beta = a.hp->kl_beta;
+  const float mu = a.mulv[(size_t)i * 2 * Z + c], lv = a.mulv[(size_t)i * 2 * Z + Z + c], ee = a.eps[e];
   combine_rows_partial(a.slab, a.ks, (long long)a.B * Z, (long long)i * Z, Z, red);
   __syncthreads();
   if (t >= Z) return;
-  const int c = t, e = i * Z + c;
   float g = 0.f;
   for (int r = 0; r < RG; ++r) g += red[r * Z + c];
   if (a.dz) a.dz[e] = g;
-  const float beta = a.hp->kl_beta;
-  const float mu = a.mulv[(size_t)i * 2 * Z + c], lv = a.mulv[(size_t)i * 2 * Z + Z + c];
   const float sd = expf(0.5f * lv);
   const float dm = g + beta * mu;
-  const float dl = 0.5f * g * a.eps[e] * sd + 0.5f * beta * (sd * sd - 1.f);
+  const float dl = 0.5f * g * ee * sd + 0.5f * beta * (sd * sd - 1.f);
   a.dmulv[(size_t)i * 2 * Z + c] = dm;
   a.dmulv[(size_t)i * 2 * Z + Z + c] = dl;
   if (a.dmulv16) {
