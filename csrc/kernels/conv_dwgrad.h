@@ -259,7 +259,13 @@ __global__ void __launch_bounds__(CF::THREADS) dwgrad_k(DwArgs a) {
 }
 
 //               C   H  CO RPS S KS
-using DwL1 = DwCfg<32, 64, 64, 2, 3, 2>;  // 64x64x32 -> 32x32x64 (enc2 / dec3): 15.9 -> 14.2 us with two k-groups
+#ifndef MDT_DW1_RPS  // A/B builds (ring depth / rows per stage of DwL1)
+#define MDT_DW1_RPS 4
+#endif
+#ifndef MDT_DW1_S
+#define MDT_DW1_S 3
+#endif
+using DwL1 = DwCfg<32, 64, 64, MDT_DW1_RPS, MDT_DW1_S, 2>;  // 64x64x32 -> 32x32x64 (enc2 / dec3): 15.9 -> 14.2 us with two k-groups
 using DwL2 = DwCfg<64, 32, 128, 4, 3>;   // 32x32x64 -> 16x16x128 (enc3 / dec2)
 
 }  // namespace mdt
