@@ -98,7 +98,7 @@ def main(argv=None):
     from multidisttorch_amd.data.datasets import mnist_like
     from multidisttorch_amd.data.sampler import shard_indices
     from multidisttorch_amd.models.mlp_trainer import MlpVaeTrainer
-    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+    from multidisttorch_amd.parallel.ddp import SELFTEST_LOG, make_arena_reducer
 
     from multidisttorch_amd.runtime.bootstrap import _stdout_to_stderr
 
@@ -147,6 +147,7 @@ def main(argv=None):
         return tr
 
     trainers, streams = [], []
+    selftest = None
     img = 28 if a.model in ("mlp", "conv28") else 128
     if gid is not None:
         pg = handles[gid]
@@ -161,8 +162,12 @@ def main(argv=None):
                 dist.broadcast(trainer.params, src=dist.get_global_rank(pg, 0), group=pg)
                 trainer.refresh_weights()
                 mb = None if a.bucket_mb in (None, "") else float(a.bucket_mb)
+                n_log = len(SELFTEST_LOG)
                 trainer.attach_reducer(make_arena_reducer(pg, trainer.grads, trainer.bucket_bounds(mb),
                                                           comm_jobs=getattr(trainer, "comm_jobs", False)))
+                if len(SELFTEST_LOG) > n_log:  # the fused xGMI data plane's construction-time self-test
+                    st = SELFTEST_LOG[-1]
+                    selftest = {"result": st["result"], "ms": st["ms"], "two_shot": st["two_shot"]}
             # reference sampler replicas W // group size (vae-hpo.py:146); packing: one shard per trial
             idx = shard_indices(len(train), (world // n_per) * T, tid)
             trainer.bind_train_data(train.data, idx)
@@ -276,6 +281,7 @@ def main(argv=None):
                 "valid": bool(flag.item() > 0),
                 "health": health or None,
                 "replicas_bitwise_equal": replicas_equal,
+                "reducer_selftest": selftest,
                 "reducer": (type(trainer.reducer).__name__ if trainer is not None
                             and getattr(trainer, "reducer", None) is not None else None),
                 # vs_baseline: the reference publishes no numbers (BASELINE.json

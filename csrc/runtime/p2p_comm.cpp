@@ -33,6 +33,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <iterator>
 #include <list>
@@ -52,18 +53,28 @@ namespace mdt {
 // reducer-free 28x28 step then stopped being run-to-run bitwise in the
 // processes where that happened (profiles/r4_determinism; the mechanism is
 // still open). Sizes are rounded up to a power of two (>= 1 MiB) so reducers
-// with different bucket layouts share regions, and at most kMaxFree regions
-// per device stay parked: beyond that the oldest one is freed after a device
-// sync (autotune's throw-away reducers no longer pin one region per layout).
+// with different bucket layouts share regions; a parked region is kept for the
+// life of the process (the round-5 eviction of the oldest region
+// re-opened exactly the reuse path above). The parked count is bounded by the
+// peak number of reducers alive at once per size class.
+// MDT_UC_POOL=0 turns the pool off (regions go back to the runtime with
+// hipFree, the round-3 behaviour): the A/B switch of profiles/r6_determinism.
 class UncachedPool {
  public:
-  static constexpr int kMaxFree = 4;
+  static bool enabled() {
+    static const bool on = [] {
+      const char* v = std::getenv("MDT_UC_POOL");
+      return !(v && v[0] == '0');
+    }();
+    return on;
+  }
   static size_t size_class(size_t bytes) {
     size_t c = (size_t)1 << 20;
     while (c < bytes) c <<= 1;
     return c;
   }
   static void* take(int dev, size_t bytes) {
+    if (!enabled()) return nullptr;
     std::lock_guard<std::mutex> g(mu());
     auto& l = free_list();
     for (auto it = l.rbegin(); it != l.rend(); ++it) {  // the most recently freed region of that class
@@ -76,19 +87,12 @@ class UncachedPool {
     return nullptr;
   }
   static void give(int dev, size_t bytes, void* p) {
-    std::lock_guard<std::mutex> g(mu());
-    auto& l = free_list();
-    l.push_back({dev, bytes, p});
-    int n = 0;
-    for (const auto& r : l) n += r.dev == dev;
-    if (n <= kMaxFree) return;
-    for (auto it = l.begin(); it != l.end(); ++it) {
-      if (it->dev != dev) continue;
-      (void)hipDeviceSynchronize();  // no kernel of this device still touches it
-      (void)hipFree(it->p);
-      l.erase(it);
+    if (!enabled()) {  // the caller synchronized the device: no kernel still touches it
+      (void)hipFree(p);
       return;
     }
+    std::lock_guard<std::mutex> g(mu());
+    free_list().push_back({dev, bytes, p});
   }
   static int64_t parked(int dev) {
     std::lock_guard<std::mutex> g(mu());
@@ -178,6 +182,7 @@ class XgmiP2PReducer : public StreamBuckets {
     // any stream may still read ctx_ / the abort word / the region below
     (void)hipDeviceSynchronize();
     if (ctx_) (void)hipFree(ctx_);
+    for (void* m : test_mem_) (void)hipFree(m);
     for (int p = 0; p < s_; ++p)
       if (p != me_ && peer_base_[p] && opened_[p]) (void)hipIpcCloseMemHandle(peer_base_[p]);
     if (base_) UncachedPool::give(device_, (size_t)alloc_bytes_, base_);
@@ -261,24 +266,44 @@ class XgmiP2PReducer : public StreamBuckets {
     TORCH_CHECK(connected_ || s_ == 1, "XgmiP2PReducer: connect() before comm_ctx()");
     if (!ctx_) {
       DeviceGuard dg(device_);
-      CommCtx c{};
-      for (int p = 0; p < kP2PMaxRanks; ++p) {
-        c.peer_recv[p] = p < s_ ? (float*)((char*)peer_base_[p] + frecv_byte_) : nullptr;
-        c.peer_flags[p] = p < s_ ? (unsigned*)((char*)peer_base_[p] + fflags_byte_) : nullptr;
-      }
-      c.status = (int*)((char*)base_ + status_byte_);
-      c.abort_flag = abort_dev_;
-      c.ep_base = ep_base_;
-      c.numel = flat_.numel();
-      c.me = me_;
-      c.s = s_;
-      c.two_shot = fused_two_ ? 1 : 0;
-      c.scale = scale_;
-      c.timeout_ticks = timeout_ticks_;
+      const CommCtx c = host_ctx();
       MDT_HIP_CHECK(hipMalloc(&ctx_, sizeof(CommCtx)));
       MDT_HIP_CHECK(hipMemcpy(ctx_, &c, sizeof(CommCtx), hipMemcpyHostToDevice));
     }
     return (int64_t)(uintptr_t)ctx_;
+  }
+
+  // CommCtx of the construction-time data-plane self-test
+  // (parallel/ddp.py::selftest_fused): the production peer mappings, layout
+  // and scale, but its own status word, epoch base 0 (the test runs epochs
+  // 1 and 2; rebase_epochs moves the trainer's epochs past them), a short
+  // timeout and the given one-/two-shot form. Freed with the reducer.
+  int64_t selftest_ctx(double timeout_s, bool two_shot) {
+    TORCH_CHECK(fused_, "XgmiP2PReducer: built without fused=True");
+    TORCH_CHECK(connected_ || s_ == 1, "XgmiP2PReducer: connect() before selftest_ctx()");
+    DeviceGuard dg(device_);
+    void* mem = nullptr;
+    MDT_HIP_CHECK(hipMalloc(&mem, 256 + sizeof(CommCtx)));
+    test_mem_.push_back(mem);
+    MDT_HIP_CHECK(hipMemset(mem, 0, 256));
+    CommCtx c = host_ctx();
+    c.status = (int*)mem;
+    c.ep_base = 0;
+    c.two_shot = (two_shot && s_ > 2) ? 1 : 0;
+    c.timeout_ticks = (long long)(timeout_s * 1e8);
+    MDT_HIP_CHECK(hipMemcpy((char*)mem + 256, &c, sizeof(CommCtx), hipMemcpyHostToDevice));
+    return (int64_t)(uintptr_t)((char*)mem + 256);
+  }
+  // status word of a self-test ctx (device sync first: every job has ended)
+  int64_t selftest_status(int64_t ctx) {
+    DeviceGuard dg(device_);
+    bool known = false;
+    for (void* m : test_mem_) known = known || (int64_t)(uintptr_t)((char*)m + 256) == ctx;
+    TORCH_CHECK(known, "selftest_status: not a self-test ctx of this reducer");
+    MDT_HIP_CHECK(hipDeviceSynchronize());
+    int v = 0;
+    MDT_HIP_CHECK(hipMemcpy(&v, (char*)(uintptr_t)ctx - 256, sizeof(int), hipMemcpyDeviceToHost));
+    return v;
   }
   std::vector<int64_t> grids() const { return std::vector<int64_t>(grid_.begin(), grid_.end()); }
   std::vector<int64_t> two_shot() const { return std::vector<int64_t>(two_.begin(), two_.end()); }
@@ -312,9 +337,28 @@ class XgmiP2PReducer : public StreamBuckets {
   }
 
  private:
+  CommCtx host_ctx() const {
+    CommCtx c{};
+    for (int p = 0; p < kP2PMaxRanks; ++p) {
+      c.peer_recv[p] = p < s_ ? (float*)((char*)peer_base_[p] + frecv_byte_) : nullptr;
+      c.peer_flags[p] = p < s_ ? (unsigned*)((char*)peer_base_[p] + fflags_byte_) : nullptr;
+    }
+    c.status = (int*)((char*)base_ + status_byte_);
+    c.abort_flag = abort_dev_;
+    c.ep_base = ep_base_;
+    c.numel = flat_.numel();
+    c.me = me_;
+    c.s = s_;
+    c.two_shot = fused_two_ ? 1 : 0;
+    c.scale = scale_;
+    c.timeout_ticks = timeout_ticks_;
+    return c;
+  }
+
   int me_, s_;
   bool fused_ = false, fused_two_ = false;
   void* ctx_ = nullptr;
+  std::vector<void*> test_mem_;
   long long frecv_byte_ = 0, fflags_byte_ = 0, alloc_bytes_ = 0;
   int64_t ep_base_ = 0;
   int* abort_host_ = nullptr;
@@ -346,6 +390,8 @@ void bind_p2p(pybind11::module& m) {
                .def("fused", &XgmiP2PReducer::fused)
                .def("fused_two_shot", &XgmiP2PReducer::fused_two_shot)
                .def("comm_ctx", &XgmiP2PReducer::comm_ctx)
+               .def("selftest_ctx", &XgmiP2PReducer::selftest_ctx, py::arg("timeout_s"), py::arg("two_shot"))
+               .def("selftest_status", &XgmiP2PReducer::selftest_status)
                .def("scale", &XgmiP2PReducer::scale)
                .def("grids", &XgmiP2PReducer::grids)
                .def("two_shot", &XgmiP2PReducer::two_shot)

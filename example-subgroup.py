@@ -38,4 +38,11 @@ if __name__ == "__main__":
     want = int(os.getenv("MDT_EXAMPLE_WORLD", "8"))
     assert comm_size == want, f"This example is set to use {want} processes."
     run(rank, comm_size)
+    # orderly teardown (every entry point does): no rank leaves while a peer's
+    # gloo/RCCL threads still talk to it -- exiting straight after the gather
+    # let the interpreter's teardown race a peer's exit (SIGABRT)
+    from multidisttorch_amd.runtime.bootstrap import global_barrier, shutdown
+
+    global_barrier()
+    shutdown()
     print("Done.")

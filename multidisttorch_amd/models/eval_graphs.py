@@ -15,7 +15,8 @@ also produce the reconstruction images), the remaining full batches replay one
 captured graph of S batches, the tail batch a graph of its own. The index list
 lives in a persistent buffer (its address is baked into the graphs; each pass
 copies the caller's indices into it), graphs are keyed by (S, M, dataset
-address and length, buffer address), and capturing restores the eval state
+address and length, buffer address; only the latest dataset's are kept), and
+capturing restores the eval state
 the warm-up batch advanced. Numerics are those of the eager pass (same kernels
 in the same order).
 """
@@ -49,6 +50,13 @@ class GraphedEval:
 
     def _eval_graph(self, S: int, M: int, X: torch.Tensor, idx: torch.Tensor):
         key = (S, M, X.data_ptr(), X.shape[0], idx.data_ptr())
+        # graphs of the latest eval set only: a caller that passes
+        # a new (e.g. temporary) X drops the graphs -- and their private memory
+        # pools -- captured for the previous one instead of accumulating them
+        xkey = (X.data_ptr(), X.shape[0], idx.data_ptr())
+        if getattr(self, "_eval_xkey", None) != xkey:
+            self._eval_graphs = {}
+            self._eval_xkey = xkey
         g = self._eval_graphs.get(key)
         if g is None:
             st = self._eval_state()

@@ -36,7 +36,7 @@ from ..ops import native
 __all__ = ["XgmiModel", "plan_buckets", "make_arena_reducer", "PyBucketReducer", "ArenaDDP",
            "broadcast_params", "rccl_comm_ptr", "reducer_kind", "make_p2p_reducer", "P2P_KINDS",
            "two_shot_min_bytes", "group_on_one_node", "overlap_pays", "graph_capturable",
-           "XGMI_KINDS"]
+           "XGMI_KINDS", "verify_group_agreement", "selftest_fused", "SELFTEST_LOG"]
 
 
 class XgmiModel:
@@ -245,13 +245,14 @@ def make_arena_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: b
         pg = dist.distributed_c10d._get_default_group()
     kind = kind or (reducer_kind(pg, flat, comm_jobs) if prefer_native else "python")
     b = [int(x) for x in bounds]
+    verify_group_agreement(pg, flat, b, kind)
     if kind in XGMI_KINDS or kind in P2P_KINDS:
         red = (make_p2p_reducer(pg, flat, b, average, two_shot=XGMI_KINDS[kind], fused=True, scale=scale)
                if kind in XGMI_KINDS else make_p2p_reducer(pg, flat, b, average, two_shot=P2P_KINDS[kind]))
         if red is not None:
             return red
         kind = "rccl" if dist.get_backend(pg) == "nccl" else "c10d"
-        print(f"[mdt] peer mapping over xGMI failed in a group of {dist.get_world_size(pg)}: "
+        print(f"[mdt] peer mapping or data-plane self-test over xGMI failed in a group of {dist.get_world_size(pg)}: "
               f"falling back to the {kind} reducer", file=sys.stderr, flush=True)
     if kind == "rccl":
         size = dist.get_world_size(pg)
@@ -283,10 +284,149 @@ def overlap_pays(first_bucket_bytes: int, split_cost_us: float, link_gbps: float
 # reducer kind -> two-shot rule: "auto" (buckets >= MDT_P2P_TWO_SHOT_MB, default 4, in groups >= 3),
 # "never" (one-shot), "always"
 P2P_KINDS = {"p2p": "auto", "p2p1": "never", "p2p2": "always"}
-# fused all-reduce jobs (comm_jobs.h): "xgmi" one-shot or, in groups >= 3 with
-# an arena of at least MDT_P2P_TWO_SHOT_MB (default 4: the 12-18 MB 128x128
-# model, not the 1.5 MB 28x28 one), two-shot per unit; "xgmi1" / "xgmi2" force
-XGMI_KINDS = {"xgmi": "auto", "xgmi1": "never", "xgmi2": "always"}
+# fused all-reduce jobs (comm_jobs.h): "xgmi" = one-shot (the
+# two-shot form has only run with ranks sharing one GPU, so it stays opt-in
+# until a multi-GPU record shows it correct and faster); "xgmi2" two-shot for
+# every unit; "xgmia" two-shot in groups >= 3 with an arena of at least
+# MDT_P2P_TWO_SHOT_MB (default 4: the 12-18 MB 128x128 model); "xgmi1" = "xgmi"
+XGMI_KINDS = {"xgmi": "never", "xgmi1": "never", "xgmi2": "always", "xgmia": "auto"}
+
+# construction-time self-test records of the fused data plane, newest last:
+# {"result": "ok" | "fallback" | "skipped", "ms": float, "two_shot": bool, "status": [...]}
+SELFTEST_LOG: List[dict] = []
+
+
+def _desc_code(x) -> int:
+    import zlib
+
+    return zlib.crc32(repr(x).encode()) & 0x7FFFFFFF
+
+
+def verify_group_agreement(pg, flat: torch.Tensor, bounds: Sequence[int], kind: str):
+    """Every member of ``pg`` must build the same reducer before any gradient
+    moves: arena numel and dtype, bucket bounds, reducer kind and its
+    two-shot threshold. The fused xGMI jobs store into a peer's region by
+    ARENA OFFSET, so a size or layout mismatch would be out-of-bounds remote
+    writes on another GPU, and RCCL would hang on unequal counts; here it is a
+    RuntimeError on EVERY member, naming the ranks that differ from group
+    rank 0. Collective (all members call it).
+
+    Reference counterpart: DDP's constructor verifies parameter shapes across
+    the group and broadcasts their metadata before the first all-reduce
+    (``_verify_param_shape_across_processes`` + metadata broadcast under
+    /root/reference/vae-hpo.py:130)."""
+    if pg is None or not dist.is_initialized():
+        return
+    s = dist.get_world_size(pg)
+    if s == 1:
+        return
+    rule = XGMI_KINDS.get(kind, P2P_KINDS.get(kind, "never"))
+    fields = ["numel", "dtype", "nbuckets", "bounds", "kind", "two_shot_min_bytes"]
+    mine = [flat.numel(), _desc_code(str(flat.dtype)), len(bounds) - 1, _desc_code(tuple(int(x) for x in bounds)),
+            _desc_code(kind), two_shot_min_bytes(rule, s)]
+    on_dev = flat.is_cuda and dist.get_backend(pg) == "nccl"
+    t = torch.tensor(mine, dtype=torch.int64, device=flat.device if on_dev else "cpu")
+    got = [torch.empty_like(t) for _ in range(s)]
+    dist.all_gather(got, t, group=pg)
+    rows = [g.cpu().tolist() for g in got]
+    bad = [(q, [f for f, a, b in zip(fields, rows[q], rows[0]) if a != b]) for q in range(1, s) if rows[q] != rows[0]]
+    if bad:
+        detail = "; ".join(f"group rank {q} differs in {', '.join(f)}" for q, f in bad)
+        raise RuntimeError(f"intra-group reducer disagreement (this is group rank {dist.get_rank(pg)}): {detail} "
+                           f"(group rank 0: numel {rows[0][0]}, {rows[0][2]} buckets, kind {kind!r} here)")
+
+
+def _members_share_a_device(pg, dev: torch.device) -> bool:
+    """True when two members of ``pg`` run on the same physical GPU (host +
+    PCI location; one-GPU multi-rank rehearsals). Collective."""
+    import socket
+
+    p = torch.cuda.get_device_properties(dev)
+    me = f"{socket.gethostname()}/{p.pci_domain_id}:{p.pci_bus_id}:{p.pci_device_id}"
+    ids = [None] * dist.get_world_size(pg)
+    dist.all_gather_object(ids, me, group=pg)
+    return len(set(ids)) < len(ids)
+
+
+def selftest_fused(red, pg, flat: torch.Tensor, timeout_s: Optional[float] = None) -> bool:
+    """Data-plane self-test of a connected fused xGMI reducer, before any real
+    gradient moves: one push+reduce of a rank-coded pattern over the whole
+    arena through the production jobs (``comm_unit_body`` in a
+    ``jobs_multi_k`` launch, the production peer mappings, layout and 1/s
+    scale), one-shot and -- when the reducer selected it -- two-shot, each with
+    a ``timeout_s`` (default 2 s, ``MDT_XGMI_SELFTEST_TIMEOUT_S``) bound on
+    every wait. The result must be BITWISE the rank-order sum x scale on every
+    member (the pattern's values are exact in f32 at any group size), and
+    the verdict is MIN-reduced over the group, so all members keep the fused
+    reducer or all fall back together. On success the reducer's epochs are
+    moved past the two used here. Collective."""
+    C = native.require()
+    s, r = dist.get_world_size(pg), dist.get_rank(pg)
+    timeout_s = timeout_s or float(os.getenv("MDT_XGMI_SELFTEST_TIMEOUT_S", "2"))
+    dev, n = flat.device, flat.numel()
+    import time
+
+    from ..runtime.faults import injected_rank
+
+    t0 = time.perf_counter()
+    i = torch.arange(n, device=dev, dtype=torch.int64)
+
+    def pattern(q):  # integers in [-2046, 2046] x 2^-6: any rank-order sum of <= 8 is exact
+        return ((i * 40503 + q * 9973 + 7) % 4093 - 2046).to(torch.float32) * (2.0 ** -6)
+
+    expect = pattern(0)
+    for q in range(1, s):
+        expect = expect + pattern(q)
+    expect = expect * torch.tensor(red.scale(), dtype=torch.float32, device=dev)
+    segs = C.make_grad_segs([[0, n, 0, 1, 0, 0, 0, 0, -1]], dev.index or 0)
+    units = [[0, u, min(1024, n - u)] for u in range(0, n, 1024)]
+    units_t = C.make_grad_units(units, dev.index or 0)
+    state = C.TrialState(dev.index or 0)
+    forms = [False] + ([True] if red.fused_two_shot() else [])
+    on_dev = dist.get_backend(pg) == "nccl"
+    # members on distinct devices (the production layout) run push+reduce in
+    # ONE workgroup per unit, as the step's tail does; members that share a
+    # device (one-GPU rehearsals) push, meet at a host barrier, then reduce --
+    # a spinning reduce must not hold the CUs a co-located peer's push needs
+    shared = _members_share_a_device(pg, dev)
+    ok, statuses = True, []
+
+    def run(mode, G, ctx):
+        job = C.Job()
+        C.comm_job(G, G, G, G, G, segs, units_t, len(units), state.train_state, state.hparams, False, ctx, mode, job)
+        pack, grid = C.pack_jobs_multi([job])
+        C.launch_jobs_multi(pack.to(dev), grid)
+
+    for k, two in enumerate(forms):
+        G = pattern(r)
+        state.set_step(False, k + 1)  # epoch k + 1 (ctx ep_base 0)
+        ctx = red.selftest_ctx(timeout_s, two)
+        if shared:
+            run(1, G, ctx)
+            torch.cuda.synchronize(dev)
+            dist.barrier(group=pg)
+            run(2, G, ctx)
+        else:
+            run(3, G, ctx)
+        st = int(red.selftest_status(ctx))  # syncs the device
+        statuses.append(st)
+        ok = ok and st == 0 and bool(torch.equal(G, expect))
+    if injected_rank("XGMI_SELFTEST_FAIL") == r:
+        ok = False
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if on_dev else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=pg)
+    agreed = int(flag.item()) == 1
+    if agreed:
+        red.rebase_epochs(len(forms), 0)  # the trainer's first epoch lands past the self-test's
+    ms = (time.perf_counter() - t0) * 1e3
+    SELFTEST_LOG.append({"result": "ok" if agreed else "fallback", "ms": round(ms, 2), "two_shot": len(forms) > 1,
+                         "status": statuses, "local_ok": ok, "group_size": s,
+                         "form": "push|barrier|reduce" if shared else "push+reduce"})
+    if not agreed:
+        print(f"[mdt] group rank {r}: xGMI data-plane self-test failed on "
+              f"{'this rank' if not ok else 'a peer'} (status {statuses}, {ms:.1f} ms): falling back",
+              file=sys.stderr, flush=True)
+    return agreed
 
 
 def two_shot_min_bytes(rule: str, group_size: int) -> int:
@@ -314,6 +454,10 @@ def make_p2p_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: boo
     VAE models' 1-4 MB buckets. Big buckets run two-shot instead
     (reduce-scatter to chunk owners + all-gather, 2/s of the bucket per link;
     ``two_shot``: "auto" | "never" | "always", see ``two_shot_min_bytes``).
+    Before that, every member checks collectively that all exported their
+    region (nobody opens a zero handle), then that all mapped every peer;
+    a fused reducer then passes ``selftest_fused`` (a real push+reduce over
+    the mappings, bitwise-checked) before it is returned.
     All ranks of the group must share one node. Selected with
     ``MDT_REDUCER=p2p`` (or ``kind="p2p"/"p2p1"/"p2p2"``). Returns None on
     every member when any member could not map a peer's region (the caller
@@ -329,32 +473,48 @@ def make_p2p_reducer(pg, flat: torch.Tensor, bounds: Sequence[int], average: boo
     s, r = dist.get_world_size(pg), dist.get_rank(pg)
     max_blocks = max_blocks or int(os.getenv("MDT_P2P_BLOCKS", "64"))
     timeout_s = timeout_s or float(os.getenv("MDT_P2P_TIMEOUT_S", "60"))
+    from ..runtime.faults import injected_rank
+
     red = C.XgmiP2PReducer(r, s, flat, [int(x) for x in bounds], average, float(scale), max_blocks, timeout_s,
                            two_shot_min_bytes(two_shot, s), fused)
-    if s > 1:
-        ok = 1
-        try:
-            h = red.ipc_handle()
-        except RuntimeError:
-            ok, h = 0, torch.zeros(64, dtype=torch.uint8)
-        on_dev = dist.get_backend(pg) == "nccl"
-        if on_dev:
-            h = h.to(flat.device)
-        hs = [torch.empty_like(h) for _ in range(s)]
-        dist.all_gather(hs, h, group=pg)
-        # every peer zeroed its region (the ctor syncs the device) before publishing its handle
-        if ok:
-            try:
-                if os.getenv("MDT_TEST_IPC_FAIL_RANK", "") == str(r):
-                    raise RuntimeError("injected hipIpcOpenMemHandle failure (MDT_TEST_IPC_FAIL_RANK)")
-                red.connect([x.cpu() for x in hs])
-            except RuntimeError as e:
-                ok = 0
-                print(f"[mdt] group rank {r}: cannot map a peer's memory: {e}", file=sys.stderr, flush=True)
+    if s == 1:
+        return red
+    on_dev = dist.get_backend(pg) == "nccl"
+
+    def agree(ok: int) -> bool:  # MIN over the group: every member takes the same branch
         flag = torch.tensor([ok], dtype=torch.int32, device=flat.device if on_dev else "cpu")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=pg)
-        if int(flag.item()) == 0:
+        return int(flag.item()) == 1
+
+    ok = 1
+    try:
+        h = red.ipc_handle()
+    except RuntimeError as e:
+        ok, h = 0, torch.zeros(64, dtype=torch.uint8)
+        print(f"[mdt] group rank {r}: cannot export the receive region: {e}", file=sys.stderr, flush=True)
+    # a failed export anywhere: nobody opens a handle (an all-zero one included)
+    if not agree(ok):
+        return None
+    if on_dev:
+        h = h.to(flat.device)
+    hs = [torch.empty_like(h) for _ in range(s)]
+    dist.all_gather(hs, h, group=pg)
+    # every peer zeroed its region (the ctor syncs the device) before publishing its handle
+    try:
+        if injected_rank("IPC_FAIL") == r:
+            raise RuntimeError("injected hipIpcOpenMemHandle failure (MDT_TEST_IPC_FAIL_RANK)")
+        red.connect([x.cpu() for x in hs])
+    except RuntimeError as e:
+        ok = 0
+        print(f"[mdt] group rank {r}: cannot map a peer's memory: {e}", file=sys.stderr, flush=True)
+    if not agree(ok):
+        return None
+    if fused and os.getenv("MDT_XGMI_SELFTEST", "1") != "0":
+        if not selftest_fused(red, pg, flat):
             return None
+    elif fused:
+        SELFTEST_LOG.append({"result": "skipped", "ms": 0.0, "two_shot": bool(red.fused_two_shot()), "status": [],
+                             "local_ok": True, "group_size": s})
     return red
 
 

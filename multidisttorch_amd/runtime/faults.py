@@ -44,7 +44,7 @@ from typing import Dict, Optional
 
 __all__ = ["InjectedFault", "TrialTimeout", "TrialCorrupted", "maybe_inject", "fault_step", "guarded", "group_timeout_s",
            "heartbeat_s", "parse_fault", "create_health_groups", "health_group", "trial_watch", "agree_healthy",
-           "TrialWatch"]
+           "TrialWatch", "injected_rank"]
 
 
 class InjectedFault(RuntimeError):
@@ -209,6 +209,17 @@ def maybe_inject(**where):
         if where.get(k) != v:
             return
     raise InjectedFault(f"injected fault at {where}")
+
+
+def injected_rank(name: str) -> Optional[int]:
+    """Test-only seam of the data-plane fallbacks: the group rank named by
+    ``MDT_TEST_<name>_RANK`` (e.g. ``IPC_FAIL``: that member's peer mapping
+    fails; ``XGMI_SELFTEST_FAIL``: its data-plane self-test reports a
+    mismatch), or None. Production never sets these; every consumer is a
+    collective decision, so an injected failure exercises exactly the path a
+    real one takes."""
+    v = os.getenv(f"MDT_TEST_{name}_RANK", "")
+    return int(v) if v.strip().lstrip("-").isdigit() else None
 
 
 def group_timeout_s() -> float:

@@ -46,7 +46,7 @@ def main():
     dev = torch.device("cuda", 0)
     os.environ["MDT_P2P_TIMEOUT_S"] = "20"
     from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
-    from multidisttorch_amd.parallel.ddp import broadcast_params, make_arena_reducer
+    from multidisttorch_amd.parallel.ddp import SELFTEST_LOG, broadcast_params, make_arena_reducer
 
     B = 128 if image == 28 else 16
     z = 32 if image == 28 else 64
@@ -77,7 +77,9 @@ def main():
         tr = make(stream)
         broadcast_params([tr.params], dist.group.WORLD)  # DDP ctor broadcast (gloo: via host copy)
         tr.refresh_weights()
+        n_log = len(SELFTEST_LOG)
         red = make_arena_reducer(dist.group.WORLD, tr.grads, tr.bucket_bounds(bucket_mb), kind=kind)
+        selftest = SELFTEST_LOG[-1] if len(SELFTEST_LOG) > n_log else None
         tr.attach_reducer(red)
         if kind == "xgmi" and image == 28 and mode == "split":
             # push and reduce in separate launches with a host barrier between
@@ -97,7 +99,7 @@ def main():
                           phash=hashlib.sha1(tr.params.cpu().numpy().tobytes()).hexdigest(),
                           two_shot=bool(red.fused_two_shot()) if hasattr(red, "fused_two_shot") else None, split=bool(tr.comm_split_tail), pair=bool(getattr(tr, "f28_pair", False)),
                           cu_mask=os.environ.get("HSA_CU_MASK"), status=int(red.status()) if hasattr(red, "status") else 0, nb=int(red.num_buckets()),
-                          launched=int(red.launched_count()), loss=hist.tolist(),
+                          launched=int(red.launched_count()), loss=hist.tolist(), selftest=selftest,
                           finite=bool(torch.isfinite(tr.params).all().item()))
         if phase == "same_eps" and r == 0:
             ref = make(0)

@@ -277,6 +277,8 @@ def test_conv_p2p_multiprocess_ddp(s, image, graphs, mb, kind, mode, tail):
             assert r[ph]["status"] == 0 and r[ph]["finite"], (ph, r)
             assert all(r[ph]["same"]), (ph, r)  # replicas bitwise identical at every check
             assert r[ph]["split"] == (mode == "split"), (ph, r)
+            if kind.startswith("xgmi"):  # the data-plane self-test ran and passed before training
+                assert r[ph]["selftest"] and r[ph]["selftest"]["result"] == "ok", (ph, r)
             if mode == "cu":
                 assert r[ph]["cu_mask"], (ph, r)  # the rank really ran on its CU share
                 if image == 28:
@@ -309,6 +311,32 @@ def test_xgmi_falls_back_when_a_peer_cannot_be_mapped():
             assert r[ph]["reducer"] == "BucketReducer", r
             assert all(r[ph]["same"]) and r[ph]["finite"], (ph, r)
     assert "falling back to the c10d reducer" in text
+
+
+def test_xgmi_selftest_failure_falls_back_on_every_member():
+    """The construction-time data-plane self-test (parallel/ddp.py
+    ``selftest_fused``) failing on ONE member (injected with
+    MDT_TEST_XGMI_SELFTEST_FAIL_RANK=1 after a real push+reduce ran) makes
+    every member drop the fused reducer together: both take the collective
+    fallback (gloo world -> the c10d reducer), train, and end with bitwise-equal
+    replicas."""
+    from multidisttorch_amd.launch import launch
+
+    env = {"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2", "MDT_CU_SPLIT": "1", "MDT_TEST_XGMI_SELFTEST_FAIL_RANK": "1"}
+    rc, outs = launch([sys.executable, os.path.join(HERE, "conv_ddp_worker.py"), "28", "1", "none", "xgmi", "prod",
+                       "0"], 2, emulate="torchrun", timeout=150, extra_env=env, capture=True)
+    text = "\n".join(o or "" for o in outs)
+    assert rc == 0, text[-4000:]
+    res = [json.loads(l[7:]) for l in text.splitlines() if l.startswith("RESULT ")]
+    assert len(res) == 2, text[-4000:]
+    for r in res:
+        for ph in ("same_eps", "indep_eps"):
+            st = r[ph]["selftest"]
+            assert st["result"] == "fallback" and st["status"] == [0], (ph, r)  # the data plane itself was fine
+            assert st["local_ok"] == (r["rank"] != 1), (ph, r)
+            assert r[ph]["reducer"] == "BucketReducer", r
+            assert all(r[ph]["same"]) and r[ph]["finite"], (ph, r)
+    assert "self-test failed" in text and "falling back to the c10d reducer" in text
 
 
 def _worker_results(s, image, kind, tail=0):

@@ -93,3 +93,32 @@ def test_conv28_paired_eval_is_bitwise_solo(native_ext, monkeypatch):
         if a[1] is not None:
             assert torch.equal(a[1], b[1])
     assert torch.equal(out["0"][2], out["1"][2])
+
+
+def test_eval_graph_cache_keeps_the_latest_eval_set_only(native_ext):
+    """eval graphs are cached per eval set; a new X (e.g. a
+    temporary ``.contiguous()`` copy each epoch) drops the previous set's
+    graphs instead of capturing more and more of them, and the pass over the
+    new set is still bitwise the eager pass."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(12)
+    Xtr = torch.rand(512, 784, generator=g).to(dev)
+    idx_tr = torch.arange(512, dtype=torch.int32, device=dev)
+    tr = _make("conv28", True, dev)
+    ref = _make("conv28", False, dev)
+    for t in (tr, ref):
+        t.bind_train_data(Xtr, idx_tr)
+        t.set_cursor(0, 4)
+        t.train_steps(1)
+    idx = torch.arange(300, dtype=torch.int32, device=dev)
+    counts = []
+    for k in range(4):
+        Xte = torch.rand(300, 784, generator=g).to(dev)  # a fresh tensor every pass
+        total, _ = tr.evaluate(Xte, idx, want_first_recon=False)
+        rtotal, _ = ref.evaluate(Xte, idx, want_first_recon=False)
+        torch.cuda.synchronize()
+        assert total == rtotal, (k, total, rtotal)
+        counts.append(len(tr._eval_graphs))
+        assert all(key[2] == Xte.data_ptr() for key in tr._eval_graphs)
+        del Xte
+    assert max(counts) == counts[0] == 2, counts  # (full-batch graph, tail graph) of the latest set

@@ -69,6 +69,21 @@ def test_native_and_python_reducer():
         assert r["ready_native"] == [3.0, 3.0] and r["ready_py"] == [3.0, 3.0]
 
 
+@pytest.mark.parametrize("what,field", [("numel", "numel"), ("bounds", "bounds"), ("kind", "kind")])
+def test_reducer_disagreement_raises_on_every_member(what, field):
+    """Construction-time agreement (DDP ctor X3/X4 analogue):
+    a member whose arena is one element larger (or whose bucket bounds or
+    reducer kind differ) makes EVERY member raise, naming group rank 1, before
+    any peer memory is mapped or any gradient moves."""
+    rc, outs = _run([WORKER, "disagree", what], 2)
+    assert rc == 0, "\n".join(outs)
+    res = _results(outs)
+    assert len(res) == 2
+    for r in res:
+        assert r["err"] and "group rank 1 differs in" in r["err"] and field in r["err"], r
+        assert r["after"] == 2.0
+
+
 def test_arena_ddp_matches_torch_ddp():
     rc, outs = _run([WORKER, "arena_ddp"], 2)
     assert rc == 0, "\n".join(outs)

@@ -15,6 +15,16 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
+def _finish():
+    """Control-plane barrier, then process-group teardown: no rank exits while
+    a peer still talks to it (the reference's example-subgroup.py exits
+    without teardown; that raced gloo's threads at exit)."""
+    from multidisttorch_amd.runtime.bootstrap import global_barrier, shutdown
+
+    global_barrier()
+    shutdown()
+
+
 def out(**kw):
     print("RESULT " + json.dumps(kw), flush=True)
 
@@ -37,7 +47,7 @@ def mode_groups(k):
         print0("hello from group", g, process_group=groups[g])
     global_barrier()
     out(world=ws, rank=wr, member=member, grank=grank, gathered=gathered)
-    dist.destroy_process_group()
+    _finish()
 
 
 def mode_reducer():
@@ -66,7 +76,31 @@ def mode_reducer():
         red2.wait_all()
         res["ready_" + ("native" if native else "py")] = float(flat2[0]), float(flat2[100])
     out(rank=wr, **res)
-    dist.destroy_process_group()
+    _finish()
+
+
+def mode_disagree(what):
+    """Members build reducers that do not agree (rank 1's arena one element
+    larger, other bucket bounds, or another reducer kind): EVERY member must
+    raise before any gradient moves, naming the differing rank."""
+    from multidisttorch_amd.runtime.bootstrap import setup_ddp
+    from multidisttorch_amd.parallel.ddp import make_arena_reducer
+
+    ws, wr = setup_ddp(verbose=False)
+    pg = dist.new_group(list(range(ws)))
+    n = 1000 + (1 if what == "numel" and wr == 1 else 0)
+    bounds = [0, 300 if what == "bounds" and wr == 1 else 200, n]
+    kind = "python" if what == "kind" and wr == 1 else "c10d"
+    err = None
+    try:
+        make_arena_reducer(pg, torch.zeros(n), bounds, kind=kind)
+    except RuntimeError as e:
+        err = str(e)
+    # the agreement check itself keeps the group usable: one more collective works
+    t = torch.ones(1)
+    dist.all_reduce(t, group=pg)
+    out(rank=wr, err=err, after=float(t.item()))
+    _finish()
 
 
 def mode_arena_ddp():
@@ -96,7 +130,7 @@ def mode_arena_ddp():
     err = max(float((p1.grad - p2.grad).abs().max()) for p1, p2 in zip(m1.parameters(), m2.parameters()))
     nb = len(ours.bucket_bounds) - 1
     out(rank=wr, err=err, buckets=nb)
-    dist.destroy_process_group()
+    _finish()
 
 
 def mode_trainer_ddp():
@@ -120,7 +154,7 @@ def mode_trainer_ddp():
     allp = [torch.zeros_like(p) for _ in range(ws)]
     dist.all_gather(allp, p)
     out(rank=wr, maxdiff=float(max((a - allp[0]).abs().max() for a in allp)), step=tr.step_count)
-    dist.destroy_process_group()
+    _finish()
 
 
 def mode_autotune():
@@ -151,7 +185,7 @@ def mode_autotune():
     dist.all_gather(allp, p)
     out(rank=wr, best=best, n=len(timings), maxdiff=float(max((a - allp[0]).abs().max() for a in allp)),
         cached=os.path.exists(cache))
-    dist.destroy_process_group()
+    _finish()
 
 
 def mode_health(k):
@@ -215,7 +249,7 @@ def mode_health(k):
             res["silence_after_s"] = round(time.monotonic() - t0, 2)
     global_barrier()
     out(**res)
-    dist.destroy_process_group()
+    _finish()
 
 
 if __name__ == "__main__":
@@ -224,6 +258,8 @@ if __name__ == "__main__":
         mode_groups(int(sys.argv[2]))
     elif mode == "reducer":
         mode_reducer()
+    elif mode == "disagree":
+        mode_disagree(sys.argv[2])
     elif mode == "arena_ddp":
         mode_arena_ddp()
     elif mode == "trainer_ddp":

@@ -19,15 +19,18 @@ def test_png_files(tmp_path):
 
 
 def test_png_pixels_equal_torchvision_layout(tmp_path):
-    """Single-channel grids are written as 8-bit grayscale with exactly the
-    pixels of torchvision's (three equal RGB planes) grid, tail row included."""
+    """Single-channel grids are written as 8-bit RGB (the reference's
+    torchvision format, mode 'RGB') with exactly the pixels of torchvision's
+    grid (three equal planes), tail row included."""
     from PIL import Image
 
     t = torch.rand(13, 1, 20, 12)
     save_image(t, str(tmp_path / "g.png"), nrow=4)
-    got = np.array(Image.open(tmp_path / "g.png"))
-    ref = make_grid(t, nrow=4).mul(255).add_(0.5).clamp_(0, 255).to(torch.uint8).numpy()
-    assert got.ndim == 2 and np.array_equal(got, ref[0]) and np.array_equal(ref[0], ref[1])
+    im = Image.open(tmp_path / "g.png")
+    assert im.mode == "RGB"
+    got = np.array(im)
+    ref = make_grid(t, nrow=4).mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to(torch.uint8).numpy()
+    assert got.ndim == 3 and np.array_equal(got, ref) and np.array_equal(ref[..., 0], ref[..., 1])
     rgb = torch.rand(3, 3, 8, 8)
     save_image(rgb, str(tmp_path / "c.png"), nrow=2)
     got = np.array(Image.open(tmp_path / "c.png"))
