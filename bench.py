@@ -167,7 +167,8 @@ def main(argv=None):
                                                           comm_jobs=getattr(trainer, "comm_jobs", False)))
                 if len(SELFTEST_LOG) > n_log:  # the fused xGMI data plane's construction-time self-test
                     st = SELFTEST_LOG[-1]
-                    selftest = {"result": st["result"], "ms": st["ms"], "two_shot": st["two_shot"]}
+                    selftest = {"result": st["result"], "ms": st["ms"], "two_shot": st["two_shot"],
+                                "form": st.get("form"), "marks_ms": st.get("marks_ms")}
             # reference sampler replicas W // group size (vae-hpo.py:146); packing: one shard per trial
             idx = shard_indices(len(train), (world // n_per) * T, tid)
             trainer.bind_train_data(train.data, idx)

@@ -340,11 +340,14 @@ def _members_share_a_device(pg, dev: torch.device) -> bool:
     """True when two members of ``pg`` run on the same physical GPU (host +
     PCI location; one-GPU multi-rank rehearsals). Collective."""
     import socket
+    import zlib
 
     p = torch.cuda.get_device_properties(dev)
-    me = f"{socket.gethostname()}/{p.pci_domain_id}:{p.pci_bus_id}:{p.pci_device_id}"
-    ids = [None] * dist.get_world_size(pg)
-    dist.all_gather_object(ids, me, group=pg)
+    me = [zlib.crc32(socket.gethostname().encode()), p.pci_domain_id, p.pci_bus_id, p.pci_device_id]
+    t = torch.tensor(me, dtype=torch.int64, device=dev if dist.get_backend(pg) == "nccl" else "cpu")
+    got = [torch.empty_like(t) for _ in range(dist.get_world_size(pg))]
+    dist.all_gather(got, t, group=pg)
+    ids = [tuple(g.tolist()) for g in got]
     return len(set(ids)) < len(ids)
 
 
@@ -369,6 +372,11 @@ def selftest_fused(red, pg, flat: torch.Tensor, timeout_s: Optional[float] = Non
     from ..runtime.faults import injected_rank
 
     t0 = time.perf_counter()
+    marks = {}
+
+    def mark(k):
+        marks[k] = round((time.perf_counter() - t0) * 1e3, 2)
+
     i = torch.arange(n, device=dev, dtype=torch.int64)
 
     def pattern(q):  # integers in [-2046, 2046] x 2^-6: any rank-order sum of <= 8 is exact
@@ -388,7 +396,9 @@ def selftest_fused(red, pg, flat: torch.Tensor, timeout_s: Optional[float] = Non
     # ONE workgroup per unit, as the step's tail does; members that share a
     # device (one-GPU rehearsals) push, meet at a host barrier, then reduce --
     # a spinning reduce must not hold the CUs a co-located peer's push needs
+    mark("setup")
     shared = _members_share_a_device(pg, dev)
+    mark("identity")
     ok, statuses = True, []
 
     def run(mode, G, ctx):
@@ -409,6 +419,7 @@ def selftest_fused(red, pg, flat: torch.Tensor, timeout_s: Optional[float] = Non
         else:
             run(3, G, ctx)
         st = int(red.selftest_status(ctx))  # syncs the device
+        mark(f"form{k}")
         statuses.append(st)
         ok = ok and st == 0 and bool(torch.equal(G, expect))
     if injected_rank("XGMI_SELFTEST_FAIL") == r:
@@ -421,7 +432,7 @@ def selftest_fused(red, pg, flat: torch.Tensor, timeout_s: Optional[float] = Non
     ms = (time.perf_counter() - t0) * 1e3
     SELFTEST_LOG.append({"result": "ok" if agreed else "fallback", "ms": round(ms, 2), "two_shot": len(forms) > 1,
                          "status": statuses, "local_ok": ok, "group_size": s,
-                         "form": "push|barrier|reduce" if shared else "push+reduce"})
+                         "form": "push|barrier|reduce" if shared else "push+reduce", "marks_ms": marks})
     if not agreed:
         print(f"[mdt] group rank {r}: xGMI data-plane self-test failed on "
               f"{'this rank' if not ok else 'a peer'} (status {statuses}, {ms:.1f} ms): falling back",
