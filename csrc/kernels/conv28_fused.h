@@ -448,37 +448,58 @@ __device__ __forceinline__ void fwd_p01(const FwdArgs& a, uint8_t* lds, int n, A
   after_p0();
 
   stamp(a.stamps, 1);
-  // ---- P1: enc1 (1 -> 32, 28x28 -> 14x14, VALU), ReLU. Two threads per
-  // output pixel (16 channels each): 392 of the 512 threads instead of 196
-  // with a 512-FMA chain each.
-  if (tid < 392) {
-    const int pix = tid >> 1, hc = tid & 1;
-    const int oy = pix / 14, ox = pix - 14 * (pix / 14);
-    float acc[16];
+  // ---- P1: enc1 (1 -> 32, 28x28 -> 14x14), ReLU, on exact-f32 MFMA
+  // (v_mfma_f32_16x16x4_f32): D[channel][pixel] = W1[channel][tap] x
+  // im2col(x)[tap][pixel] + bias, 2 channel tiles x 13 pixel tiles x 4 tap
+  // steps; wave w takes pixel tiles w and w + 8. A lane ends with four
+  // consecutive channels of one pixel: one 8-B bf16 store to the LDS image
+  // and one to a1. The f32 VALU form (392 threads x 256 FMAs) spent 1.56 us
+  // of this phase in its tap loop (profiles/r6_f28_gather).
+  {
+    const int col = lane & 15, kq = lane >> 4;
+    float wa[2][4];  // A: W1[16 mt + col][4 ks + kq] (tap-major LDS copy)
 #pragma unroll
-    for (int c = 0; c < 16; ++c) acc[c] = reinterpret_cast<const float*>(lds + L::Bias)[kB1 + 16 * hc + c];
-#pragma unroll 4
-    for (int t = 0; t < 16; ++t) {
-      const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
-      const bool ok = (unsigned)iy < 28u && (unsigned)ix < 28u;
-      const float x = ok ? Xs[iy * 28 + ix] : 0.f;
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const float4 wv = reinterpret_cast<const float4*>(W1s + t * 32 + 16 * hc)[c4];
-        acc[4 * c4 + 0] = fmaf(x, wv.x, acc[4 * c4 + 0]);
-        acc[4 * c4 + 1] = fmaf(x, wv.y, acc[4 * c4 + 1]);
-        acc[4 * c4 + 2] = fmaf(x, wv.z, acc[4 * c4 + 2]);
-        acc[4 * c4 + 3] = fmaf(x, wv.w, acc[4 * c4 + 3]);
+      for (int ks = 0; ks < 4; ++ks) wa[mt][ks] = W1s[(4 * ks + kq) * 32 + 16 * mt + col];
+    const float* Bias1 = reinterpret_cast<const float*>(lds + L::Bias) + kB1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nt = w + 8 * j;
+      if (nt < 13) {
+        const int pix = 16 * nt + col;
+        const bool live = pix < 196;
+        const int oy = pix / 14, ox = pix - 14 * (pix / 14);
+        float xb4[4];  // B: im2col(x)[4 ks + kq][pix]
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int t = 4 * ks + kq;
+          const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
+          xb4[ks] = live && (unsigned)iy < 28u && (unsigned)ix < 28u ? Xs[iy * 28 + ix] : 0.f;
+        }
+        f32x4 acc[2];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[mt][r] = Bias1[16 * mt + 4 * kq + r];
+        }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) acc[mt] = mfma16x16x4(wa[mt][ks], xb4[ks], acc[mt]);
+        if (live) {
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const int c0 = 16 * mt + 4 * kq;  // four consecutive channels
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (__bf16)fmaxf(acc[mt][r], 0.f);
+            *reinterpret_cast<bf16x4*>(A1s + img14(pix, c0 >> 3) + ((c0 & 7) << 1)) = o;
+            if (a.train) *reinterpret_cast<bf16x4*>(a.a1 + ((size_t)n * 196 + pix) * 32 + c0) = o;
+          }
+        }
       }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ch = 2 * hc + h;
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (__bf16)fmaxf(acc[8 * h + e], 0.f);
-      *reinterpret_cast<bf16x8*>(A1s + img14(pix, ch)) = o;
-      if (a.train) *reinterpret_cast<bf16x8*>(a.a1 + ((size_t)n * 196 + pix) * 32 + 8 * ch) = o;
     }
   }
   w2regs.store(W3s);  // enc2 weights (dec1's tap images replace them after P2); the caller's barrier publishes
@@ -787,53 +808,57 @@ __device__ __forceinline__ void bwd_body(const BwdArgs& a, uint8_t* lds, int n) 
   }
 
   stamp(a.stamps, 1);
-  // ---- Q1: dec2 backward-data (conv 1 -> 32 on the dlogits, 28 -> 14) x dec1 ReLU mask.
-  // Two threads per pixel (16 channels each), as in P1.
-  if (tid < 392) {
-    const int pix = tid >> 1, hc = tid & 1;
-    const int oy = pix / 14, ox = pix - 14 * (pix / 14);
-    float acc[16];
+  // ---- Q1: dec2 backward-data (conv 1 -> 32 on the dlogits, 28 -> 14) x dec1 ReLU mask,
+  // on exact-f32 MFMA as enc1 in P1 (the paired body's Q1 runs the same per-
+  // element MFMA sequence on its own channel tile: pair == solo bitwise).
+  {
+    const int col = lane & 15, kq = lane >> 4;
+    float wa[2][4];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) acc[c] = 0.f;
-    // the dec1 ReLU mask, loaded before the FMAs so its latency overlaps them
-    bf16x8 mk[2];
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      mk[h] = MERGED ? reinterpret_cast<const bf16x8*>(lds + L::D1 + pix * 64)[2 * hc + h]
-                     : reinterpret_cast<const bf16x8*>(a.d1 + ((size_t)n * 196 + pix) * 32)[2 * hc + h];
-#pragma unroll 4
-    for (int t = 0; t < 16; ++t) {
-      const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
-      const bool ok = (unsigned)iy < 28u && (unsigned)ix < 28u;
-      const float g = ok ? Gs[iy * 28 + ix] : 0.f;
+      for (int ks = 0; ks < 4; ++ks) wa[mt][ks] = W4s[(4 * ks + kq) * 32 + 16 * mt + col];
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const float4 wv = reinterpret_cast<const float4*>(W4s + t * 32 + 16 * hc)[c4];
-        acc[4 * c4 + 0] = fmaf(g, wv.x, acc[4 * c4 + 0]);
-        acc[4 * c4 + 1] = fmaf(g, wv.y, acc[4 * c4 + 1]);
-        acc[4 * c4 + 2] = fmaf(g, wv.z, acc[4 * c4 + 2]);
-        acc[4 * c4 + 3] = fmaf(g, wv.w, acc[4 * c4 + 3]);
+    for (int j = 0; j < 2; ++j) {
+      const int nt = w + 8 * j;
+      if (nt < 13) {
+        const int pix = 16 * nt + col;
+        const bool live = pix < 196;
+        const int oy = pix / 14, ox = pix - 14 * (pix / 14);
+        float gb[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int t = 4 * ks + kq;
+          const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
+          gb[ks] = live && (unsigned)iy < 28u && (unsigned)ix < 28u ? Gs[iy * 28 + ix] : 0.f;
+        }
+        f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) acc[mt] = mfma16x16x4(wa[mt][ks], gb[ks], acc[mt]);
+        if (live) {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const int c0 = 16 * mt + 4 * kq;
+            const bf16x4 m = MERGED ? *reinterpret_cast<const bf16x4*>(lds + L::D1 + pix * 64 + c0 * 2)
+                                    : *reinterpret_cast<const bf16x4*>(a.d1 + ((size_t)n * 196 + pix) * 32 + c0);
+            bf16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = (float)m[e] > 0.f ? acc[mt][e] : 0.f;
+              o[e] = (__bf16)v;
+              // dec1 bias partials: transposed through LDS, then 8 lanes per
+              // channel sum strided pixels in a fixed order (below)
+              CSB[(c0 + e) * 197 + pix] = v;
+            }
+            *reinterpret_cast<bf16x4*>(GD1s + img14(pix, c0 >> 3) + ((c0 & 7) << 1)) = o;
+            *reinterpret_cast<bf16x4*>(a.gd1 + ((size_t)n * 196 + pix) * 32 + c0) = o;
+          }
+        }
       }
     }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ch = 2 * hc + h;
-      const bf16x8 m = mk[h];
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = (float)m[e] > 0.f ? acc[8 * h + e] : 0.f;
-        acc[8 * h + e] = v;
-        o[e] = (__bf16)v;
-      }
-      *reinterpret_cast<bf16x8*>(GD1s + img14(pix, ch)) = o;
-      *reinterpret_cast<bf16x8*>(a.gd1 + ((size_t)n * 196 + pix) * 32 + 8 * ch) = o;
-    }
-    // dec1 bias partials: transpose the f32 values through LDS, then 8 lanes
-    // per channel sum strided pixels and combine in a fixed order (a wave_sum
-    // per channel was 192 dependent cross-lane steps per wave: ~5 us)
-#pragma unroll
-    for (int c = 0; c < 16; ++c) CSB[(16 * hc + c) * 197 + pix] = acc[c];
   }
   lds_barrier();
   if (tid < 256) {

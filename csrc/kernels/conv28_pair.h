@@ -632,39 +632,58 @@ __device__ __forceinline__ void pair_rest(uint8_t* lds, int n, int r) {
   if (!train) return;
 
   pstamp(8);
-  // ---- Q1: dec2 backward-data on own channels (8 per thread) x dec1 ReLU mask; X4 publishes gd1
+  // ---- Q1: dec2 backward-data on own channels x dec1 ReLU mask; X4 publishes gd1.
+  // Exact-f32 MFMA (v_mfma_f32_16x16x4_f32, as enc1 in P1): D[own channel]
+  // [pixel] = W4[channel][tap] x im2col(dlogits)[tap][pixel], 13 pixel tiles x
+  // 4 tap steps, wave w takes pixel tiles w and w + 8; a lane ends with four
+  // consecutive own channels of one pixel.
   __bf16* const gd1p = TB(kTGd1);
-  if (tid < 392) {
-    const int pix = tid >> 1, h = tid & 1, cg = 2 * r + h;  // 8-channel chunk cg of 4
-    const int oy = pix / 14, ox = pix - 14 * (pix / 14);
-    float acc[8];
+  {
+    const int col = lane & 15, kq = lane >> 4;
+    float wa[4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-    const bf16x8 m = reinterpret_cast<const bf16x8*>(lds + L::D1 + pix * 64)[cg];
-#pragma unroll 4
-    for (int t = 0; t < 16; ++t) {
-      const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
-      const bool ok = (unsigned)iy < 28u && (unsigned)ix < 28u;
-      const float g = ok ? Gs[iy * 28 + ix] : 0.f;
-      const float4 w0 = reinterpret_cast<const float4*>(W4s + t * 32 + 8 * cg)[0];
-      const float4 w1 = reinterpret_cast<const float4*>(W4s + t * 32 + 8 * cg)[1];
-      acc[0] = fmaf(g, w0.x, acc[0]); acc[1] = fmaf(g, w0.y, acc[1]);
-      acc[2] = fmaf(g, w0.z, acc[2]); acc[3] = fmaf(g, w0.w, acc[3]);
-      acc[4] = fmaf(g, w1.x, acc[4]); acc[5] = fmaf(g, w1.y, acc[5]);
-      acc[6] = fmaf(g, w1.z, acc[6]); acc[7] = fmaf(g, w1.w, acc[7]);
+    for (int ks = 0; ks < 4; ++ks) wa[ks] = W4s[(4 * ks + kq) * 32 + 16 * r + col];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nt = w + 8 * j;
+      if (nt < 13) {
+        const int pix = 16 * nt + col;
+        const bool live = pix < 196;
+        const int oy = pix / 14, ox = pix - 14 * (pix / 14);
+        float gb[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int t = 4 * ks + kq;
+          const int iy = 2 * oy - 1 + (t >> 2), ix = 2 * ox - 1 + (t & 3);
+          gb[ks] = live && (unsigned)iy < 28u && (unsigned)ix < 28u ? Gs[iy * 28 + ix] : 0.f;
+        }
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc = mfma16x16x4(wa[ks], gb[ks], acc);
+        if (live) {
+          const int cl = 4 * kq, c0 = 16 * r + cl;  // own-local / global first channel of the four
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          const bf16x4 m = *reinterpret_cast<const bf16x4*>(lds + L::D1 + pix * 64 + c0 * 2);
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = (float)m[e] > 0.f ? acc[e] : 0.f;
+            o[e] = (__bf16)v;
+            CSB[(cl + e) * 197 + pix] = v;  // dec1 bias partials (own channel cl + e)
+          }
+          *reinterpret_cast<bf16x4*>(GD1s + img14(pix, c0 >> 3) + ((c0 & 7) << 1)) = o;
+          *reinterpret_cast<bf16x4*>(gd1p + pix * 32 + c0) = o;
+          // granule layout [4][392] (unchanged): channel pair (e, e + 1) of own
+          // chunk h at [(e >> 1)][2 pix + h]
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int c = cl + 2 * q, h = c >> 3, e = c & 7;
+            xput(xo + kX4 + (e >> 1) * 392 + 2 * pix + h, tg + 4,
+                 bf16bits(o[2 * q]) | (bf16bits(o[2 * q + 1]) << 16), near);
+          }
+        }
+      }
     }
-    bf16x8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float v = (float)m[e] > 0.f ? acc[e] : 0.f;
-      o[e] = (__bf16)v;
-      CSB[(8 * h + e) * 197 + pix] = v;  // dec1 bias partials (own channel 8 h + e)
-    }
-    *reinterpret_cast<bf16x8*>(GD1s + img14(pix, cg)) = o;
-    *reinterpret_cast<bf16x8*>(gd1p + pix * 32 + 8 * cg) = o;
-#pragma unroll
-    for (int e = 0; e < 8; e += 2)  // granule layout [4][392]: one wave store = 512 contiguous bytes
-      xput(xo + kX4 + (e >> 1) * 392 + tid, tg + 4, bf16bits(o[e]) | (bf16bits(o[e + 1]) << 16), near);
   }
   // Q3's first dec_fc weight loads (own rows), in flight during X4 and Q2
   const int jr = lane >> 2;
