@@ -86,6 +86,11 @@ struct FwdArgs {
   float* db4_part;       // [M] (dec2 bias gradient partials)
   unsigned long long* stamps;  // optional [grid][16] s_memrealtime at phase ends (profiling)
   int pf_slices;         // P0 L2-prefetch slices per XCD (workgroups sharing one XCD)
+  // next-batch prefetch (training only, null = off): the previous step's
+  // finalize gathered this step's rows into xn [B][784] and wrote xtag[n] =
+  // the TrainState.step they are for (grad_finalize_k, BatchGather)
+  const float* xn;
+  const unsigned* xtag;
 };
 
 struct BwdArgs {
@@ -389,10 +394,19 @@ __device__ __forceinline__ void fwd_p01(const FwdArgs& a, uint8_t* lds, int n, A
   // row, W1, biases) go first; the enc2 image loads and the prefetch DMAs go
   // after them and stay in flight through P1 (P0 ends on an LDS-only barrier).
   {
-    const int row = a.idx[(size_t)a.st->cursor * a.B + n];
-    const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)row * 784);
+    // The batch row: when the previous step's finalize already gathered it
+    // (xtag[n] == step), ONE round trip (the row load is issued before the
+    // tag is known); otherwise the dependent cursor -> index -> row chain
+    // (first step after the host moved the cursor / data, eval passes, DDP
+    // steps). profiles/r6_f28_gather: the chain is ~0.4 us of P0.
     float4 xv = {0.f, 0.f, 0.f, 0.f};
-    if (tid < 196) xv = src[tid];
+    const bool pre_ok = a.train && a.xn != nullptr;
+    if (pre_ok && tid < 196) xv = reinterpret_cast<const float4*>(a.xn + (size_t)n * 784)[tid];
+    if (!pre_ok || a.xtag[n] != (unsigned)a.st->step) {
+      const int row = a.idx[(size_t)a.st->cursor * a.B + n];
+      const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)row * 784);
+      if (tid < 196) xv = src[tid];
+    }
     const float w1 = W.W1f[tid], w4 = W.W4f[tid];
     float bv = 0.f;
     if (tid < kNBias)

@@ -137,6 +137,8 @@ void fill_fwd(f28::FwdArgs& a, const long long* p, int B, unsigned stream, int t
   a.db4_part = P<float>(p, 28);
   a.stamps = P<unsigned long long>(p, 29);
   a.pf_slices = 16;
+  a.xn = P<const float>(p, 30);
+  a.xtag = P<const unsigned>(p, 31);
 }
 
 void fill_bwd(f28::BwdArgs& a, const long long* p, int M) {

@@ -156,9 +156,13 @@ __global__ void __launch_bounds__(256) adam_cast_k(float* P, const float* G, flo
 }
 
 template <bool FENCE>
-__global__ void __launch_bounds__(kFinalizeThreads) grad_finalize_k(FinalizeArgs fa) {
+__global__ void __launch_bounds__(kFinalizeThreads) grad_finalize_k(FinalizeArgs fa, BatchGather bg) {
   __shared__ float red[kFinalizeThreads];
   __shared__ AdamC cs;
+  if ((int)blockIdx.x >= bg.nunits) {  // next-batch gather blocks (only when bg.xn is set)
+    batch_gather_body(bg, (int)blockIdx.x - bg.nunits);
+    return;
+  }
   grad_finalize_body(fa, red, &cs, blockIdx.x);
   // diagnostic (MDT_FIN_FENCE=1): an explicit agent-scope release of the
   // parameter / bf16 stores before the kernel-end release
@@ -251,19 +255,23 @@ int mdt_adam_cast(float* P, const float* G, float* Mo, float* Vo, void* w16, con
 }
 
 int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs, const void* units,
-                      int nunits, const void* st, const void* hp, int do_adam, hipStream_t s) {
+                      int nunits, const void* st, const void* hp, int do_adam, const float* gX, const int* gidx,
+                      float* xn, unsigned* xtag, int gB, hipStream_t s) {
   if (nunits <= 0) return 0;
   const FinalizeArgs fa{P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16), reinterpret_cast<const GradSeg*>(segs),
                         reinterpret_cast<const GradUnit*>(units), reinterpret_cast<const TrainState*>(st),
                         reinterpret_cast<const HParams*>(hp), do_adam};
+  const bool gather = xn && xtag && gX && gidx && gB > 0;
+  const BatchGather bg{gX, gidx, reinterpret_cast<const TrainState*>(st), xn, xtag, gB, nunits};
+  const int grid = nunits + (gather ? gather_blocks(gB) : 0);
   static const bool fence = [] {
     const char* e = getenv("MDT_FIN_FENCE");
     return e && e[0] == '1';
   }();
   if (fence)
-    hipLaunchKernelGGL(grad_finalize_k<true>, dim3(nunits), dim3(kFinalizeThreads), 0, s, fa);
+    hipLaunchKernelGGL(grad_finalize_k<true>, dim3(grid), dim3(kFinalizeThreads), 0, s, fa, bg);
   else
-    hipLaunchKernelGGL(grad_finalize_k<false>, dim3(nunits), dim3(kFinalizeThreads), 0, s, fa);
+    hipLaunchKernelGGL(grad_finalize_k<false>, dim3(grid), dim3(kFinalizeThreads), 0, s, fa, bg);
   return (int)hipGetLastError();
 }
 

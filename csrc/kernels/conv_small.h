@@ -325,6 +325,32 @@ struct FinalizeArgs {
 
 constexpr int kFinalizeThreads = 256;
 
+// Next-batch gather riding in the 28x28 step's finalize launch (blocks after
+// the finalize units): by then the loss job has advanced the cursor and the
+// step, so rows idx[cursor * B + n] are the NEXT step's batch; they go to xn
+// with xtag[n] = step, which the step kernel's P0 checks before taking its
+// row from xn in one round trip (conv28_fused.h fwd_p01). Same launch, so
+// the kernel boundary publishes both to the next step.
+struct BatchGather {
+  const float* X;      // dataset [rows][784]
+  const int* idx;      // epoch index list (whole batches of B)
+  const TrainState* st;
+  float* xn;           // [B][784], null = off
+  unsigned* xtag;      // [B]
+  int B, nunits;       // blocks [nunits, nunits + gather_blocks(B)) gather
+};
+__host__ __device__ constexpr int gather_blocks(int B) { return (B * 196 + kFinalizeThreads - 1) / kFinalizeThreads; }
+
+__device__ __forceinline__ void batch_gather_body(const BatchGather& g, int b) {
+  const int e = b * kFinalizeThreads + (int)threadIdx.x;  // float4 index over [B][196]
+  const int n = e / 196, c = e - 196 * (e / 196);
+  if (n < g.B) {
+    const int row = g.idx[(size_t)g.st->cursor * g.B + n];
+    reinterpret_cast<float4*>(g.xn + (size_t)n * 784)[c] = reinterpret_cast<const float4*>(g.X + (size_t)row * 784)[c];
+    if (c == 0) g.xtag[n] = (unsigned)g.st->step;
+  }
+}
+
 // Partial-slab sums shared by the finalize bodies here and the fused
 // all-reduce jobs (comm_jobs.h): one summation order everywhere, so a
 // gradient finalized on its own and one finalized inside a collective job

@@ -36,7 +36,8 @@ int mdt_step_begin(void* st, const void* hp, hipStream_t s);
 int mdt_adam_cast(float* P, const float* G, float* Mo, float* Vo, void* w16, const void* segs, int nseg,
                   long long total, const void* st, const void* hp, int do_adam, hipStream_t s);
 int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs, const void* units,
-                      int nunits, const void* st, const void* hp, int do_adam, hipStream_t s);
+                      int nunits, const void* st, const void* hp, int do_adam, const float* gX, const int* gidx,
+                      float* xn, unsigned* xtag, int gB, hipStream_t s);
 int mdt_wtrans(const void* w16, void* w16t, const void* segs, const void* units, int nunits, hipStream_t s);
 int mdt_thin_conv(const void* X, int x_is_f32, const float* Wf, mdt::ConvDesc d, const float* bias, int relu, void* y16,
                   const void* omask, float* colsum, const int* idx, void* st, const void* hp, int B, float* xb,
@@ -392,8 +393,10 @@ struct Slot {
 
 std::vector<long long> f28_ptrs(const std::vector<c10::optional<at::Tensor>>& t, const std::vector<Slot>& slots,
                                 int64_t M, int dev) {
-  TORCH_CHECK(t.size() == slots.size(), "f28: expected ", slots.size(), " tensors, got ", t.size());
-  std::vector<long long> p(t.size(), 0);
+  TORCH_CHECK(t.size() <= slots.size(), "f28: expected ", slots.size(), " tensors, got ", t.size());
+  for (size_t i = t.size(); i < slots.size(); ++i)  // trailing slots left out: must be optional (null)
+    TORCH_CHECK(slots[i].optional, "f28: expected ", slots.size(), " tensors, got ", t.size());
+  std::vector<long long> p(slots.size(), 0);
   for (size_t i = 0; i < t.size(); ++i) {
     const Slot& s = slots[i];
     if (!t[i].has_value() || !t[i]->defined()) {
@@ -434,7 +437,8 @@ std::vector<Slot> f28_fwd_slots(int64_t B, bool train) {
       {"mulv", 'f', 64, false, !train},    {"eps", 'f', 32, false, !train},   {"z16", 'b', 32, false, !train},
       {"d0", 'b', 3136, false, !train},    {"d1", 'b', 6272, false, !train},  {"dlog", 'f', 784, false, !train},
       {"recon", 'f', 784, false, true},    {"bce_part", 'f', 1, false, false}, {"kld_part", 'f', 1, false, false},
-      {"db4_part", 'f', 1, false, true},   {"stamps", 'l', 32, false, true}};
+      {"db4_part", 'f', 1, false, true},   {"stamps", 'l', 32, false, true},
+      {"xn", 'f', 784, false, true},       {"xtag", 'i', 1, false, true}};
   slots.insert(slots.end(), rest.begin(), rest.end());
   return slots;
 }
@@ -568,7 +572,7 @@ void adam_cast(at::Tensor P, const at::Tensor& G, at::Tensor M, at::Tensor V, at
 
 void grad_finalize(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::Tensor w16, const at::Tensor& segs,
                    const at::Tensor& units, int64_t nunits, const at::Tensor& state, const at::Tensor& hparams,
-                   bool do_adam, Job* job) {
+                   bool do_adam, Job* job, const std::vector<at::Tensor>& gather, int64_t gather_B) {
   TORCH_CHECK(units.numel() >= nunits * (int64_t)sizeof(GradUnit), "grad_finalize: unit table too small");
   if (job) {
     rc(mdt_job_finalize(&job->main, P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(),
@@ -577,9 +581,31 @@ void grad_finalize(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::T
        "job_finalize");
     return;
   }
+  // optional next-batch gather (the fused 28x28 step): [X, idx, xn, xtag] and the batch size
+  const float* gX = nullptr;
+  const int* gidx = nullptr;
+  float* xn = nullptr;
+  unsigned* xtag = nullptr;
+  if (!gather.empty()) {
+    TORCH_CHECK(gather.size() == 4 && gather_B > 0, "grad_finalize: gather = [X, idx, xn, xtag] with gather_B > 0");
+    const int dev = P.get_device();
+    const char* nm[4] = {"X", "idx", "xn", "xtag"};
+    for (int i = 0; i < 4; ++i)
+      TORCH_CHECK(gather[i].is_cuda() && gather[i].get_device() == dev && gather[i].is_contiguous(),
+                  "grad_finalize: gather ", nm[i], " must be a contiguous tensor on the arena's device");
+    TORCH_CHECK(gather[0].scalar_type() == torch::kFloat32 && gather[0].numel() % 784 == 0, "grad_finalize: X [rows][784] f32");
+    TORCH_CHECK(gather[1].scalar_type() == torch::kInt32 && gather[1].numel() % gather_B == 0,
+                "grad_finalize: idx int32 in whole batches");
+    TORCH_CHECK(gather[2].scalar_type() == torch::kFloat32 && gather[2].numel() >= gather_B * 784, "grad_finalize: xn");
+    TORCH_CHECK(gather[3].scalar_type() == torch::kInt32 && gather[3].numel() >= gather_B, "grad_finalize: xtag");
+    gX = gather[0].data_ptr<float>();
+    gidx = gather[1].data_ptr<int>();
+    xn = gather[2].data_ptr<float>();
+    xtag = reinterpret_cast<unsigned*>(gather[3].data_ptr<int>());
+  }
   rc(mdt_grad_finalize(P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(),
                        w16.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits, state.data_ptr(),
-                       hparams.data_ptr(), do_adam ? 1 : 0, cur()),
+                       hparams.data_ptr(), do_adam ? 1 : 0, gX, gidx, xn, xtag, (int)gather_B, cur()),
      "grad_finalize");
 }
 
@@ -772,7 +798,8 @@ void bind_conv(pybind11::module& m) {
   });
   m.def("grad_finalize", &grad_finalize, py::arg("P"), py::arg("G"), py::arg("M"), py::arg("V"), py::arg("w16"),
         py::arg("segs"), py::arg("units"), py::arg("nunits"), py::arg("state"), py::arg("hparams"),
-        py::arg("do_adam"), py::arg("job") = py::none());
+        py::arg("do_adam"), py::arg("job") = py::none(), py::arg("gather") = std::vector<at::Tensor>{},
+        py::arg("gather_B") = 0);
   m.def("comm_job", &comm_job, py::arg("P"), py::arg("G"), py::arg("M"), py::arg("V"), py::arg("w16"),
         py::arg("segs"), py::arg("units"), py::arg("nunits"), py::arg("state"), py::arg("hparams"),
         py::arg("do_adam"), py::arg("ctx"), py::arg("mode"), py::arg("job"));

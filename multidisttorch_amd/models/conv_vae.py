@@ -369,7 +369,16 @@ class ConvVaeTrainer(GraphedEval):
         default intra-node reducer for this trainer is then kind "xgmi"."""
         return self.backend == "hip" and self.fuse_jobs
 
+    def _invalidate_prefetch(self):
+        """The host moved the cursor, the step or the data: rows the last
+        finalize gathered are not the next step's (f28 P0 falls back to the
+        index chain until the next finalize gathers again)."""
+        xt = getattr(self, "f28_xtag", None)
+        if xt is not None:
+            xt.fill_(-1)
+
     def set_step(self, step):
+        self._invalidate_prefetch()
         if self.backend == "hip":
             red = self.reducer
             if red is not None and hasattr(red, "rebase_epochs"):
@@ -380,6 +389,8 @@ class ConvVaeTrainer(GraphedEval):
             self._st["step"] = int(step)
 
     def set_cursor(self, cursor, nbatches, eval=False):
+        if not eval:
+            self._invalidate_prefetch()
         if self.backend == "hip":
             self.state.set_cursor(eval, int(cursor), int(nbatches))
         else:
@@ -413,6 +424,7 @@ class ConvVaeTrainer(GraphedEval):
         if pad:
             idx = torch.cat([idx, idx[:1].expand(pad)])
         self._data = (X.contiguous(), idx.contiguous(), n, nb)
+        self._invalidate_prefetch()
         self._graphs.clear()
         self._plans28.clear()
 
@@ -578,6 +590,12 @@ class ConvVaeTrainer(GraphedEval):
             self.f28_xg = torch.zeros(B * 2 * self.C.f28_pair_words(), dtype=torch.int64, device=dev)
             self.f28_pairw = torch.zeros(B, dtype=torch.int32, device=dev)
             self.f28_err = torch.zeros(1, dtype=torch.int32, device=dev)
+            # next-batch prefetch: the finalize of step k gathers step k+1's rows
+            # into f28_xn and tags them with the step they are for (f28_xtag);
+            # -1 = nothing gathered (the host invalidates on cursor/data/step moves)
+            self.f28_xn = torch.zeros(B * self.D, **f32)
+            self.f28_xtag = torch.full((B,), -1, dtype=torch.int32, device=dev)
+            self.f28_prefetch = os.getenv("MDT_F28_PREFETCH", "1") != "0"
         self._cast_weights()
 
     def _n_bce(self, M):
@@ -1131,7 +1149,7 @@ class ConvVaeTrainer(GraphedEval):
         a1, a2, d0, d1 = self.acts["enc1"], self.acts["enc2"], self.acts["dec_fc"], self.acts["dec1"]
         gd1, gd0, ga2, ga1 = self.gacts["dec1"], self.gacts["dec_fc"], self.gacts["enc2"], self.gacts["enc1"]
         fwd = w + [X, idx, st.train_state, st.hparams, self.xb, a1, a2, self.mulv, self.eps, self.z16, d0, d1,
-                   self.dlog32, None, bce, kld, db4, self.f28_stamps[0]]
+                   self.dlog32, None, bce, kld, db4, self.f28_stamps[0], self.f28_xn, self.f28_xtag]
         bwd = w + [st.hparams, self.mulv, self.eps, a1, a2, d0, d1, self.dlog32, gd1, gd0, dbd, self.dmulv,
                    self.dmulv16, ga2, ga1, db3, db2, db1, self.f28_stamps[1]]
         # weight gradients: (G, X) per layer in the conv view (see _backward_hip)
@@ -1189,7 +1207,9 @@ class ConvVaeTrainer(GraphedEval):
         if red is None:
             C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
             C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
-                            p["nunits"], st.train_state, st.hparams, not self.f28_skip_adam)
+                            p["nunits"], st.train_state, st.hparams, not self.f28_skip_adam,
+                            gather=([self._data[0], self._data[1], self.f28_xn, self.f28_xtag]
+                                    if self.f28_prefetch else []), gather_B=self.B)
             return
         if self._comm_ctx():
             # fused xGMI all-reduce (comm_jobs.h), one stream: decoder weight

@@ -493,3 +493,38 @@ def test_f28_near_path_is_exercised_and_bitwise(native_ext):
     assert res[True][2] > 0, "no same-XCD pair took the near hand-off"
     np.testing.assert_array_equal(res[True][0], res[False][0])
     assert torch.equal(res[True][1], res[False][1])
+
+
+def test_f28_next_batch_prefetch_is_bitwise_and_tagged(native_ext):
+    """The finalize of step k gathers step k+1's rows into f28_xn with
+    xtag = step (the step kernel's P0 then skips the cursor -> index -> row
+    chain): training with and without the prefetch is bitwise equal across
+    graphs, tail batches and host cursor moves, and after a step the tags
+    name the current step and xn holds exactly the next batch's rows."""
+    dev = torch.device("cuda")
+    B, nb, tail = 128, 3, 40
+    g = torch.Generator().manual_seed(21)
+    X = torch.rand(nb * B + tail, 784, generator=g).to(dev)
+    idx = torch.randperm(nb * B + tail, generator=g).to(torch.int32).to(dev)
+    res = {}
+    for pre in (False, True):
+        tr = _trainer(B=B, seed=5, use_graphs=True, graph_steps=2)
+        tr.f28_prefetch = pre
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, nb + 1)
+        tr.train_steps(nb)
+        tr.train_steps(1, M=tail)
+        tr.set_cursor(1, nb + 1)  # host moves the cursor: the gathered rows are stale
+        tr.train_steps(2)
+        torch.cuda.synchronize()
+        st = tr.read_state()
+        if pre:
+            assert (tr.f28_xtag == st["step"]).all()
+            cur = st["cursor"]
+            rows = tr._data[1][cur * B:(cur + 1) * B].long()
+            assert torch.equal(tr.f28_xn.view(B, 784), X[rows])
+        else:
+            assert (tr.f28_xtag == -1).all()
+        res[pre] = (tr.loss_history()[:nb + 3].copy(), tr.params.clone())
+    np.testing.assert_array_equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])
