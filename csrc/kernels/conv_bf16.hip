@@ -159,11 +159,15 @@ template <bool FENCE>
 __global__ void __launch_bounds__(kFinalizeThreads) grad_finalize_k(FinalizeArgs fa, BatchGather bg) {
   __shared__ float red[kFinalizeThreads];
   __shared__ AdamC cs;
-  if ((int)blockIdx.x >= bg.nunits) {  // next-batch gather blocks (only when bg.xn is set)
-    batch_gather_body(bg, (int)blockIdx.x - bg.nunits);
+  // next-batch gather blocks first (only when bg.xn is set): their dependent
+  // cursor -> index -> row chain then overlaps the finalize units instead of
+  // trailing the grid
+  const int gb = bg.xn ? gather_blocks(bg.B) : 0;
+  if ((int)blockIdx.x < gb) {
+    batch_gather_body(bg, (int)blockIdx.x);
     return;
   }
-  grad_finalize_body(fa, red, &cs, blockIdx.x);
+  grad_finalize_body(fa, red, &cs, (int)blockIdx.x - gb);
   // diagnostic (MDT_FIN_FENCE=1): an explicit agent-scope release of the
   // parameter / bf16 stores before the kernel-end release
   if constexpr (FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -262,7 +266,7 @@ int mdt_grad_finalize(float* P, float* G, float* Mo, float* Vo, void* w16, const
                         reinterpret_cast<const GradUnit*>(units), reinterpret_cast<const TrainState*>(st),
                         reinterpret_cast<const HParams*>(hp), do_adam};
   const bool gather = xn && xtag && gX && gidx && gB > 0;
-  const BatchGather bg{gX, gidx, reinterpret_cast<const TrainState*>(st), xn, xtag, gB, nunits};
+  const BatchGather bg{gX, gidx, reinterpret_cast<const TrainState*>(st), gather ? xn : nullptr, xtag, gB, nunits};
   const int grid = nunits + (gather ? gather_blocks(gB) : 0);
   static const bool fence = [] {
     const char* e = getenv("MDT_FIN_FENCE");

@@ -325,8 +325,8 @@ struct FinalizeArgs {
 
 constexpr int kFinalizeThreads = 256;
 
-// Next-batch gather riding in the 28x28 step's finalize launch (blocks after
-// the finalize units): by then the loss job has advanced the cursor and the
+// Next-batch gather riding in the 28x28 step's finalize launch (blocks ahead
+// of the finalize units): by then the loss job has advanced the cursor and the
 // step, so rows idx[cursor * B + n] are the NEXT step's batch; they go to xn
 // with xtag[n] = step, which the step kernel's P0 checks before taking its
 // row from xn in one round trip (conv28_fused.h fwd_p01). Same launch, so
@@ -337,7 +337,7 @@ struct BatchGather {
   const TrainState* st;
   float* xn;           // [B][784], null = off
   unsigned* xtag;      // [B]
-  int B, nunits;       // blocks [nunits, nunits + gather_blocks(B)) gather
+  int B, nunits;       // blocks [0, gather_blocks(B)) gather, the finalize units follow
 };
 __host__ __device__ constexpr int gather_blocks(int B) { return (B * 196 + kFinalizeThreads - 1) / kFinalizeThreads; }
 
