@@ -51,3 +51,5 @@ constexpr int kCommAborted = 999999;  // status after an abort (distinct from 1 
 }  // namespace mdt
 
 extern "C" int mdt_p2p_allreduce(const mdt::P2PArgs* a, int grid, hipStream_t stream);
+extern "C" int mdt_selftest_fill(float* g, long long n, int q, hipStream_t stream);
+extern "C" int mdt_selftest_check(const float* g, long long n, int s, float scale, int* bad, hipStream_t stream);

@@ -209,7 +209,49 @@ __global__ void __launch_bounds__(256) p2p_allreduce_k(P2PArgs a) {
   if (threadIdx.x == 0) a.ep[g] = e;
 }
 
+// Construction-time data-plane self-test (parallel/ddp.py::selftest_fused):
+// the rank-coded pattern and the bitwise check of the reduced result, as
+// kernels of this extension (no framework elementwise kernels, whose first
+// use in a fresh process costs milliseconds of module loading each).
+// pattern(q, i) = ((i * 40503 + q * 9973 + 7) mod 4093 - 2046) * 2^-6: any
+// sum of <= 8 of them is exact in f32, so the expected value is the plain sum
+// times the reducer's scale, bitwise, in any order.
+__device__ __forceinline__ float selftest_pattern(long long i, int q) {
+  return (float)((int)((i * 40503LL + (long long)q * 9973LL + 7LL) % 4093LL) - 2046) * 0.015625f;
+}
+
+__global__ void __launch_bounds__(256) selftest_fill_k(float* g, long long n, int q) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    g[i] = selftest_pattern(i, q);
+}
+
+__global__ void __launch_bounds__(256) selftest_check_k(const float* g, long long n, int s, float scale, int* bad) {
+  int miss = 0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float acc = selftest_pattern(i, 0);
+    for (int q = 1; q < s; ++q) acc += selftest_pattern(i, q);
+    acc *= scale;
+    miss += __float_as_uint(acc) != __float_as_uint(g[i]);
+  }
+  if (miss) atomicAdd(bad, miss);
+}
+
 }  // namespace mdt
+
+extern "C" int mdt_selftest_fill(float* g, long long n, int q, hipStream_t stream) {
+  if (n < 1) return 1;
+  const long long b = (n + 255) / 256;
+  hipLaunchKernelGGL(mdt::selftest_fill_k, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(256), 0, stream, g, n, q);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mdt_selftest_check(const float* g, long long n, int s, float scale, int* bad, hipStream_t stream) {
+  if (n < 1 || s < 1) return 1;
+  const long long b = (n + 255) / 256;
+  hipLaunchKernelGGL(mdt::selftest_check_k, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(256), 0, stream, g, n, s, scale,
+                     bad);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mdt_p2p_allreduce(const mdt::P2PArgs* a, int grid, hipStream_t stream) {
   if (grid < 1 || a->s < 1 || a->s > mdt::kP2PMaxRanks || a->me < 0 || a->me >= a->s || a->n < 1) return 1;

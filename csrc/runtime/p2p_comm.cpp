@@ -51,8 +51,10 @@ namespace mdt {
 // handed out again to torch's caching allocator, and later trainers'
 // activations and partial slabs landed in it (scripts/diag/diag_uc_reuse.py); the
 // reducer-free 28x28 step then stopped being run-to-run bitwise in the
-// processes where that happened (profiles/r4_determinism; the mechanism is
-// still open). Sizes are rounded up to a power of two (>= 1 MiB) so reducers
+// processes where that happened (profiles/r4_determinism). On the round-6
+// tree the pool-off A/B no longer reproduces, and a freed range reused by a
+// later buffer stays bitwise (profiles/r6_determinism): the pool is kept as a
+// safe default, not as a fix. Sizes are rounded up to a power of two (>= 1 MiB) so reducers
 // with different bucket layouts share regions; a parked region is kept for the
 // life of the process (the round-5 eviction of the oldest region
 // re-opened exactly the reuse path above). The parked count is bounded by the
@@ -183,6 +185,7 @@ class XgmiP2PReducer : public StreamBuckets {
     (void)hipDeviceSynchronize();
     if (ctx_) (void)hipFree(ctx_);
     for (void* m : test_mem_) (void)hipFree(m);
+    if (test_bad_) (void)hipFree(test_bad_);
     for (int p = 0; p < s_; ++p)
       if (p != me_ && peer_base_[p] && opened_[p]) (void)hipIpcCloseMemHandle(peer_base_[p]);
     if (base_) UncachedPool::give(device_, (size_t)alloc_bytes_, base_);
@@ -294,6 +297,32 @@ class XgmiP2PReducer : public StreamBuckets {
     MDT_HIP_CHECK(hipMemcpy((char*)mem + 256, &c, sizeof(CommCtx), hipMemcpyHostToDevice));
     return (int64_t)(uintptr_t)((char*)mem + 256);
   }
+  // The self-test's rank-coded pattern of rank q in `g` (f32, flat-arena
+  // sized), and the count of elements of `g` that differ bitwise from the
+  // rank-order sum of all s patterns x this reducer's scale (syncs the device).
+  void selftest_fill(at::Tensor g, int64_t q) {
+    TORCH_CHECK(g.is_cuda() && g.scalar_type() == torch::kFloat32 && g.is_contiguous() && g.numel() == flat_.numel(),
+                "selftest_fill: f32 tensor of the arena's size");
+    DeviceGuard dg(device_);
+    TORCH_CHECK(mdt_selftest_fill(g.data_ptr<float>(), g.numel(), (int)q, c10::hip::getCurrentHIPStream().stream()) == 0,
+                "selftest_fill launch failed");
+  }
+  int64_t selftest_check(const at::Tensor& g) {
+    TORCH_CHECK(g.is_cuda() && g.scalar_type() == torch::kFloat32 && g.is_contiguous() && g.numel() == flat_.numel(),
+                "selftest_check: f32 tensor of the arena's size");
+    DeviceGuard dg(device_);
+    if (!test_bad_) {
+      MDT_HIP_CHECK(hipMalloc(&test_bad_, sizeof(int)));
+    }
+    hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+    MDT_HIP_CHECK(hipMemsetAsync(test_bad_, 0, sizeof(int), st));
+    TORCH_CHECK(mdt_selftest_check(g.data_ptr<float>(), g.numel(), s_, scale_, test_bad_, st) == 0,
+                "selftest_check launch failed");
+    int bad = 0;
+    MDT_HIP_CHECK(hipMemcpyAsync(&bad, test_bad_, sizeof(int), hipMemcpyDeviceToHost, st));
+    MDT_HIP_CHECK(hipStreamSynchronize(st));
+    return bad;
+  }
   // status word of a self-test ctx (device sync first: every job has ended)
   int64_t selftest_status(int64_t ctx) {
     DeviceGuard dg(device_);
@@ -359,6 +388,7 @@ class XgmiP2PReducer : public StreamBuckets {
   bool fused_ = false, fused_two_ = false;
   void* ctx_ = nullptr;
   std::vector<void*> test_mem_;
+  int* test_bad_ = nullptr;
   long long frecv_byte_ = 0, fflags_byte_ = 0, alloc_bytes_ = 0;
   int64_t ep_base_ = 0;
   int* abort_host_ = nullptr;
@@ -392,6 +422,8 @@ void bind_p2p(pybind11::module& m) {
                .def("comm_ctx", &XgmiP2PReducer::comm_ctx)
                .def("selftest_ctx", &XgmiP2PReducer::selftest_ctx, py::arg("timeout_s"), py::arg("two_shot"))
                .def("selftest_status", &XgmiP2PReducer::selftest_status)
+               .def("selftest_fill", &XgmiP2PReducer::selftest_fill)
+               .def("selftest_check", &XgmiP2PReducer::selftest_check)
                .def("scale", &XgmiP2PReducer::scale)
                .def("grids", &XgmiP2PReducer::grids)
                .def("two_shot", &XgmiP2PReducer::two_shot)
