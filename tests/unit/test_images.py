@@ -36,3 +36,22 @@ def test_png_pixels_equal_torchvision_layout(tmp_path):
     got = np.array(Image.open(tmp_path / "c.png"))
     ref = make_grid(rgb, nrow=2).mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to(torch.uint8).numpy()
     assert np.array_equal(got, ref)
+
+
+def test_parallel_deflate_is_a_valid_zlib_stream(tmp_path):
+    """Big grids are deflated in independent segments inside one zlib stream
+    (utils/images.py::_deflate): zlib and PIL read it back exactly."""
+    import zlib
+
+    from PIL import Image
+
+    from multidisttorch_amd.utils import images
+
+    data = np.random.default_rng(0).integers(0, 8, 3 << 20, dtype=np.uint8).tobytes()
+    assert len(data) >= images._DEFLATE_MIN_BYTES and images.PNG_DEFLATE_THREADS > 1
+    assert zlib.decompress(images._deflate(data, 1)) == data
+    t = torch.rand(64, 1, 128, 128)
+    save_image(t, str(tmp_path / "big.png"))
+    got = np.array(Image.open(tmp_path / "big.png"))
+    ref = make_grid(t).mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to(torch.uint8).numpy()
+    assert np.array_equal(got, ref)
