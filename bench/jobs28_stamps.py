@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--merged", action="store_true", help="the merged table: + gather + per-layer finalize jobs")
     a = ap.parse_args()
     from multidisttorch_amd.data.datasets import synthetic_images
     from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
@@ -37,12 +38,22 @@ def main():
     torch.cuda.synchronize()
     C, p = tr.C, tr._plan28(B)
     names = ["enc1", "enc2", "enc_head", "dec_fc", "dec1", "dec2", "loss"]
-    nblk = [j.nblk for j in p["jobs"]]
+    if a.merged:
+        assert tr.f28_fin_merge
+        _, _, jobs, wait = tr._merged_pack28(p)
+        names += (["gather"] if tr.f28_prefetch else []) + ["fin_" + n for n in tr._FIN_ORDER28]
+    else:
+        tr.f28_fin_merge = False
+        jobs, wait = p["jobs"], []
+    nblk = [j.nblk for j in jobs]
     grid0 = sum(nblk)
     stamps = torch.zeros(2 * grid0, dtype=torch.int64, device=dev)
-    pack, grid = C.pack_jobs_multi(p["jobs"], stamps=stamps)
+    pack, grid = C.pack_jobs_multi(jobs, stamps=stamps, wait=wait, dep_ctr=tr.f28_dep if wait else None)
     assert grid == grid0
-    p["jobs_pack"], p["jobs_grid"] = pack.to(dev), grid
+    if a.merged:
+        p[("merged", True)] = (pack.to(dev), grid, jobs, wait)
+    else:
+        p["jobs_pack"], p["jobs_grid"] = pack.to(dev), grid
     runs = []
     for _ in range(a.steps):
         stamps.zero_()
@@ -63,7 +74,7 @@ def main():
     res["kernel_us"] = float(np.median(per[..., 1].max(1)))
     print(f"jobs_multi_k grid {grid}: kernel (first start -> last end) {res['kernel_us']:.2f} us")
     for n, r in res["jobs"].items():
-        print(f"  {n:9s} blocks {r['blocks']:4d}  start med {r['start_med']:5.2f}  block dur med {r['dur_med']:5.2f} "
+        print(f"  {n:12s} blocks {r['blocks']:4d}  start med {r['start_med']:5.2f}  block dur med {r['dur_med']:5.2f} "
               f"max {r['dur_max']:5.2f}  last end {r['end_max']:5.2f} us")
     if a.json:
         with open(a.json, "w") as f:

@@ -29,6 +29,29 @@ __device__ __forceinline__ AdamC adam_consts_block(const TrainState* st, const H
   return *sh;
 }
 
+// Same constants when the step state was advanced earlier IN THIS LAUNCH by
+// another workgroup (dependent jobs_multi_k launch): beta^t through sc1 vector
+// loads, so neither this CU's L1 nor the scalar cache can serve an old copy.
+__device__ __forceinline__ AdamC adam_consts_block_sc1(const TrainState* st, const HParams* hp, AdamC* sh) {
+  if (threadIdx.x == 0) {
+    TrainState* s = const_cast<TrainState*>(st);
+    const double b1pow = __builtin_bit_cast(
+        double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(&s->b1pow), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT));
+    const double b2pow = __builtin_bit_cast(
+        double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(&s->b2pow), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT));
+    AdamC c;
+    c.step_size = (float)(hp->lr_d / (1.0 - b1pow));
+    c.bc2s = (float)sqrt(1.0 - b2pow);
+    c.b1 = hp->beta1; c.b2 = hp->beta2; c.eps = hp->eps; c.wd = hp->weight_decay;
+    c.gs = hp->grad_scale; c.lr = hp->lr; c.decoupled = hp->decoupled_wd;
+    *sh = c;
+  }
+  __syncthreads();
+  return *sh;
+}
+
 __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float g, const AdamC& c) {
   float gr = g * c.gs;
   if (c.wd != 0.f) {

@@ -124,10 +124,11 @@ enum JobKindBase : int {
   kJobWtrans = 5004,
   kJobLossStep = 5005,   // loss reduction + step advance (fused 28x28 step)
   kJobComm = 5006,       // fused xGMI all-reduce + Adam over finalize units (comm_jobs.h)
+  kJobGather = 5007,     // next-batch row gather behind the loss job (dependent multi-job launch)
   kJobDconv = 6000,      // + direct cfg       (patch-resident direct conv, conv_direct.h)
 };
 
 // Up to kMaxMultiJobs jobs of any kind of the multi-job kernel (jobs_multi_k).
-constexpr int kMaxMultiJobs = 8;
+constexpr int kMaxMultiJobs = 16;
 
 }  // namespace mdt

@@ -136,6 +136,15 @@ struct JComm {
   }
 };
 
+// next-batch gather of the fused 28x28 step after the loss job of the same
+// launch (conv_small.h batch_gather_dep_body)
+struct JGather {
+  static constexpr int ID = kJobGather, LDS = 0;
+  static __device__ __forceinline__ void run(const JobBlob& j, uint8_t*, int b) {
+    batch_gather_dep_body(job_args<BatchGather>(j), b);
+  }
+};
+
 struct JLossStep {
   static constexpr int ID = kJobLossStep, LDS = 64;
   static __device__ __forceinline__ void run(const JobBlob& j, uint8_t* lds, int) {
@@ -151,11 +160,39 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 // weight gradients + its loss/step job). Unlike jobs_k it needs no
 // instantiation per combination; its register allocation is the maximum over
 // the bodies, which is what those bodies use anyway.
+// Dependencies between the jobs of ONE launch (null ctr = none). A job whose
+// `wait` mask is set runs each of its workgroups only after every workgroup
+// of the masked jobs has finished; those count themselves done:
+//   producer: every wave `s_waitcnt vmcnt(0)` -> workgroup barrier -> one lane
+//     (signal 2 only: agent release, for plain stores) -> relaxed agent add
+//     to its job's counter (signal 1: the job's handed-off bytes all leave
+//     through sc1 stores, nothing dirty in this XCD's L2 to write back);
+//   consumer: one lane polls the counters with relaxed agent (sc1) loads and
+//     s_sleep -> workgroup barrier -> EVERY load of handed-off bytes is an sc1
+//     vector load (FinalizeArgs.dep, batch_gather_dep_body): no L1 line and no
+//     scalar-cache line can serve an old copy.
+// Deadlock-free by construction of the tables: waiting jobs come after their
+// producers in the grid and producers never wait, so a spinning workgroup
+// only ever waits for workgroups dispatched before it. A poll that sees no
+// progress for kDepTimeoutTicks records the job in ctr[err] and goes on (the
+// host checks that word: dep_error); the last waiting workgroup to pass its
+// wait re-zeroes the counters for the next launch.
+#ifndef MDT_DEP_SLEEP
+#define MDT_DEP_SLEEP 2
+#endif
+constexpr int kDepStride = 32;  // words between counters (one 128-B line each)
+constexpr int kDepDone = kMaxMultiJobs, kDepErr = kMaxMultiJobs + 1, kDepWords = (kMaxMultiJobs + 2) * kDepStride;
+constexpr unsigned long long kDepTimeoutTicks = 5000000ull;  // 50 ms of the 100 MHz s_memrealtime
+
 struct JobPackN {
   JobBlob j[kMaxMultiJobs];
   int start[kMaxMultiJobs + 1];
   int n;
   unsigned long long* stamps;  // profiling (null = off): per workgroup {start, end} s_memrealtime
+  unsigned* ctr;               // dependency counters [kDepWords] (null = independent jobs)
+  unsigned wait[kMaxMultiJobs];          // bit k: wait for job k
+  unsigned char signal[kMaxMultiJobs];   // 0 none, 1 sc1 stores, 2 plain stores (release first)
+  int nwait_blocks;                      // workgroups of all waiting jobs
 };
 
 constexpr int kMultiLds = cmax(cmax(cmax(wgrad_lds_bytes<W0>(), wgrad_lds_bytes<W1>()),
@@ -187,10 +224,62 @@ __device__ __forceinline__ void run_multi_job(const JobBlob& j, uint8_t* lds, in
   switch (j.kind) {
     case kJobLossStep: JLossStep::run(j, lds, lb); break;
     case kJobLoss: JLoss::run(j, lds, lb); break;
-    case kJobFinalize: JFinalize::run(j, lds, lb); break;
+    case kJobFinalize:
+      if (job_args<FinalizeArgs>(j).dep)  // a dependent launch: slabs and step state written in it
+        grad_finalize_body_t<true>(job_args<FinalizeArgs>(j), reinterpret_cast<float*>(lds),
+                                   reinterpret_cast<AdamC*>(lds + kFinalizeThreads * 4), lb);
+      else
+        JFinalize::run(j, lds, lb);
+      break;
     case kJobComm: JComm::run(j, lds, lb); break;
     case kJobColsum: JColsum::run(j, lds, lb); break;
+    case kJobGather: JGather::run(j, lds, lb); break;
     default: break;
+  }
+}
+
+__device__ __forceinline__ void dep_wait(const JobPackN* __restrict__ p, unsigned* ctr, unsigned mask, int n) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < n; ++k) {
+      if (!((mask >> k) & 1u)) continue;
+      const unsigned need = (unsigned)(p->start[k + 1] - p->start[k]);
+      while (__hip_atomic_load(ctr + k * kDepStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kDepTimeoutTicks) {
+          __hip_atomic_store(ctr + kDepErr * kDepStride, 1u + (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(MDT_DEP_SLEEP);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// After a waiting workgroup's work (off its critical path): the last one of
+// the launch re-zeroes the counters. Every waiting workgroup has passed its
+// wait by then, and every producer has counted itself (each is waited on in
+// full), so nothing reads or adds to them any more in this launch.
+__device__ __forceinline__ void dep_done(const JobPackN* __restrict__ p, unsigned* ctr, int n) {
+  if (threadIdx.x == 0) {
+    const unsigned done = __hip_atomic_fetch_add(ctr + kDepDone * kDepStride, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (done + 1 == (unsigned)p->nwait_blocks) {
+      for (int k = 0; k < n; ++k) __hip_atomic_store(ctr + k * kDepStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + kDepDone * kDepStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__device__ __forceinline__ void dep_signal(unsigned* ctr, int job, int mode) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
+  __syncthreads();                                  // ... every wave's
+  if (threadIdx.x == 0) {
+    if (mode == 2) {  // plain stores: write this XCD's dirty L2 lines back first
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __hip_atomic_fetch_add(ctr + job * kDepStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -199,19 +288,26 @@ __device__ __forceinline__ void run_multi_job(const JobBlob& j, uint8_t* lds, in
 // makes the compiler copy the whole 2.4 KB pack into per-lane scratch
 // (measured 2368 B/lane, the launch ~10x slower), and selecting it with
 // constant indices inlines every body eight times (1100+ SGPR spills).
+// DEP = false: independent jobs, at most kPlainMultiJobs (the default path,
+// code unchanged by the dependency support); DEP = true: a table packed with
+// mdt_pack_jobs_multi_deps (up to kMaxMultiJobs jobs, counters in p->ctr).
+constexpr int kPlainMultiJobs = 8;
+
+template <bool DEP>
 __global__ void __launch_bounds__(256) jobs_multi_k(const JobPackN* __restrict__ p) {
+  constexpr int NJ = DEP ? kMaxMultiJobs : kPlainMultiJobs;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kMultiLds];
   const int b = blockIdx.x;
   // every start in ONE batch of scalar loads, then count the jobs this block
   // is past (starts ascend over [0, n)): a while loop over p->start was one
   // dependent load per job in front of the table's later (longest) jobs
-  int st[kMaxMultiJobs];
+  int st[NJ];
 #pragma unroll
-  for (int k = 0; k < kMaxMultiJobs; ++k) st[k] = p->start[k];
+  for (int k = 0; k < NJ; ++k) st[k] = p->start[k];
   const int n = p->n;
   int i = 0, s0 = st[0];
 #pragma unroll
-  for (int k = 1; k < kMaxMultiJobs; ++k)
+  for (int k = 1; k < NJ; ++k)
     if (k < n && b >= st[k]) {
       i = k;
       s0 = st[k];
@@ -219,7 +315,17 @@ __global__ void __launch_bounds__(256) jobs_multi_k(const JobPackN* __restrict__
   unsigned long long* stamps = p->stamps;
   unsigned long long t0 = 0;
   if (stamps) t0 = __builtin_amdgcn_s_memrealtime();
-  run_multi_job(p->j[i], lds, b - s0);
+  if constexpr (DEP) {
+    unsigned* ctr = p->ctr;
+    const unsigned wmask = p->wait[i];
+    if (wmask) dep_wait(p, ctr, wmask, n);
+    run_multi_job(p->j[i], lds, b - s0);
+    const int sig = p->signal[i];
+    if (sig) dep_signal(ctr, i, sig);
+    if (wmask) dep_done(p, ctr, n);
+  } else {
+    run_multi_job(p->j[i], lds, b - s0);
+  }
   if (stamps) {  // which job ran where and when: overlap of jobs inside one launch (bench/ddp_structure.py)
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -233,7 +339,8 @@ __host__ inline bool multi_kind_ok(int k) {
   if (k >= kJobWgrad && k <= kJobWgrad + 5) return true;
   if (k >= kJobWgradThin && k <= kJobWgradThin + 5) return true;
   if (k >= kJobWgradThin + 20 && k <= kJobWgradThin + 25) return true;
-  return k == kJobLossStep || k == kJobLoss || k == kJobFinalize || k == kJobColsum || k == kJobComm;
+  return k == kJobLossStep || k == kJobLoss || k == kJobFinalize || k == kJobColsum || k == kJobComm ||
+         k == kJobGather;
 }
 
 template <class A, class B, class C>
@@ -491,14 +598,14 @@ int mdt_job_loss(JobBlob* j, const float* bce_part, int nb, const float* kld_par
 }
 
 int mdt_job_finalize(JobBlob* j, float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs,
-                     const void* units, int nunits, const void* st, const void* hp, int do_adam) {
+                     const void* units, int nunits, const void* st, const void* hp, int do_adam, int dep) {
   memset(j, 0, sizeof(*j));
   if (nunits <= 0) return 1;
   j->kind = kJobFinalize;
   j->nblk = nunits;
   put_args(j, FinalizeArgs{P, G, Mo, Vo, reinterpret_cast<__bf16*>(w16), reinterpret_cast<const GradSeg*>(segs),
                            reinterpret_cast<const GradUnit*>(units), reinterpret_cast<const TrainState*>(st),
-                           reinterpret_cast<const HParams*>(hp), do_adam});
+                           reinterpret_cast<const HParams*>(hp), do_adam, dep ? 1 : 0});
   return 0;
 }
 
@@ -582,10 +689,64 @@ int mdt_pack_jobs_multi(const JobBlob* jobs, int n, void* dst) {
   return grid;
 }
 
+// Dependencies for a packed table (see JobDeps above JobPackN): wait[i] is
+// the bit mask of the jobs job i waits for; ctr the zeroed device counter
+// block (mdt_jobs_dep_words() words). Producers must precede their waiters
+// and must not wait themselves. Returns 0, or -1 for a bad table.
+int mdt_jobs_dep_words() { return kDepWords; }
+int mdt_jobs_dep_err() { return kDepErr * kDepStride; }
+
+static int dep_signal_mode(const JobBlob& j) {
+  const int k = j.kind;
+  if (k == kJobThinWgM || k == kJobThinWgM + 1) {  // sc1 row stores when the slab is 16-B aligned
+    const WgArgs& a = *reinterpret_cast<const WgArgs*>(j.args);
+    return ((uintptr_t)a.out & 15) == 0 ? 1 : 2;
+  }
+  if ((k >= kJobWgrad && k <= kJobWgrad + 5) || (k >= kJobWgradThin && k <= kJobWgradThin + 25)) {
+    const WgArgs& a = *reinterpret_cast<const WgArgs*>(j.args);  // wgrad_epilogue: sc1 slabs when K2 % 4 == 0
+    return (a.K2 & 3) == 0 ? 1 : 2;
+  }
+  return 2;  // loss / step state and anything else: plain stores, release first
+}
+
+int mdt_pack_jobs_multi_deps(void* img, void* ctr, const unsigned* wait, int n) {
+  JobPackN* p = reinterpret_cast<JobPackN*>(img);
+  if (!ctr || n != p->n) return -1;
+  unsigned producers = 0;
+  int nwait = 0;
+  for (int i = 0; i < n; ++i) {
+    const unsigned w = wait[i];
+    if (w >> i) return -1;  // a job may only wait for jobs before it (and never for itself)
+    producers |= w;
+    if (w) nwait += p->start[i + 1] - p->start[i];
+  }
+  for (int i = 0; i < n; ++i) {
+    if (((producers >> i) & 1u) && wait[i]) return -1;  // no chains: producers never wait
+    p->wait[i] = wait[i];
+    p->signal[i] = ((producers >> i) & 1u) ? (unsigned char)dep_signal_mode(p->j[i]) : 0;
+  }
+  if (!nwait) return -1;
+  p->nwait_blocks = nwait;
+  p->ctr = reinterpret_cast<unsigned*>(ctr);
+  return 0;
+}
+
+int mdt_job_gather(JobBlob* j, const float* X, const int* idx, const void* st, float* xn, unsigned* xtag, int B) {
+  memset(j, 0, sizeof(*j));
+  if (!X || !idx || !st || !xn || !xtag || B <= 0) return 1;
+  j->kind = kJobGather;
+  j->nblk = gather_blocks(B);
+  put_args(j, BatchGather{X, idx, reinterpret_cast<const TrainState*>(st), xn, xtag, B, 0});
+  return 0;
+}
+
 // ONE jobs_multi_k launch over a packed table already in device memory.
-int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s) {
+int mdt_launch_jobs_multi(const void* dev_pack, int grid, int dep, hipStream_t s) {
   if (!dev_pack || grid <= 0) return 2;
-  hipLaunchKernelGGL(jobs_multi_k, dim3(grid), dim3(256), 0, s, reinterpret_cast<const JobPackN*>(dev_pack));
+  if (dep)
+    hipLaunchKernelGGL(jobs_multi_k<true>, dim3(grid), dim3(256), 0, s, reinterpret_cast<const JobPackN*>(dev_pack));
+  else
+    hipLaunchKernelGGL(jobs_multi_k<false>, dim3(grid), dim3(256), 0, s, reinterpret_cast<const JobPackN*>(dev_pack));
   return (int)hipGetLastError() ? -1 : 0;
 }
 

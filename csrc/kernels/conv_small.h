@@ -321,6 +321,11 @@ struct FinalizeArgs {
   const TrainState* st;
   const HParams* hp;
   int do_adam;
+  // 1: the slabs and the step state were written IN THIS LAUNCH by other
+  // workgroups (a dependent jobs_multi_k launch, conv_jobs.hip JobDeps): every
+  // load of them is an sc1 vector load (past this CU's L1, never the scalar
+  // cache), behind the counter poll that published them
+  int dep;
 };
 
 constexpr int kFinalizeThreads = 256;
@@ -351,49 +356,96 @@ __device__ __forceinline__ void batch_gather_body(const BatchGather& g, int b) {
   }
 }
 
+// The same gather as a job of a dependent jobs_multi_k launch (kJobGather),
+// after the loss job advanced cursor and step in that launch: both are read
+// with sc1 vector loads behind the poll of the loss job's counter.
+__device__ __forceinline__ void batch_gather_dep_body(const BatchGather& g, int b) {
+  const int e = b * kFinalizeThreads + (int)threadIdx.x;
+  const int n = e / 196, c = e - 196 * (e / 196);
+  if (n < g.B) {
+    TrainState* st = const_cast<TrainState*>(g.st);
+    const int cur = __hip_atomic_load(&st->cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int row = g.idx[(size_t)cur * g.B + n];
+    reinterpret_cast<float4*>(g.xn + (size_t)n * 784)[c] = reinterpret_cast<const float4*>(g.X + (size_t)row * 784)[c];
+    if (c == 0)
+      g.xtag[n] = (unsigned)__hip_atomic_load(reinterpret_cast<unsigned long long*>(&st->step), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Partial-slab sums shared by the finalize bodies here and the fused
 // all-reduce jobs (comm_jobs.h): one summation order everywhere, so a
 // gradient finalized on its own and one finalized inside a collective job
-// carry the same bits.
-// 4 consecutive elements (vec4 units): 4 interleaved accumulators over the slabs
-__device__ __forceinline__ f32x4 slab_sum4(const float* p, long long n, int nsplit) {
+// carry the same bits. `ld(i)` loads element (or 4 elements at) index i of
+// the slab: plain loads (SlabPlain) or, for slabs written earlier in the same
+// launch, sc1 buffer loads (SlabSc1).
+struct SlabPlain {
+  const float* p;
+  __device__ __forceinline__ f32x4 v4(long long i) const { return *reinterpret_cast<const f32x4*>(p + i); }
+  __device__ __forceinline__ float v1(long long i) const { return p[i]; }
+};
+struct SlabSc1 {
+  __amdgpu_buffer_rsrc_t rs;  // whole slab (uniform base), byte offsets < 4 GB
+  __device__ __forceinline__ SlabSc1(const float* slab, long long elems)
+      : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(slab), 0, (int)(elems * 4), 0x00020000)) {}
+  __device__ __forceinline__ f32x4 v4(long long i) const {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 4), 0, 16 /* sc1 */));
+  }
+  __device__ __forceinline__ float v1(long long i) const {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(i * 4), 0, 16 /* sc1 */));
+  }
+};
+// 4 consecutive elements at e (vec4 units): 4 interleaved accumulators over the slabs
+template <class L>
+__device__ __forceinline__ f32x4 slab_sum4_l(const L& ld, long long e, long long n, int nsplit) {
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
   f32x4 a0 = z, a1 = z, a2 = z, a3 = z;
   int s = 0;
   for (; s + 3 < nsplit; s += 4) {
-    a0 += *reinterpret_cast<const f32x4*>(p + (long long)s * n);
-    a1 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 1) * n);
-    a2 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 2) * n);
-    a3 += *reinterpret_cast<const f32x4*>(p + (long long)(s + 3) * n);
+    a0 += ld.v4(e + (long long)s * n);
+    a1 += ld.v4(e + (long long)(s + 1) * n);
+    a2 += ld.v4(e + (long long)(s + 2) * n);
+    a3 += ld.v4(e + (long long)(s + 3) * n);
   }
-  for (; s < nsplit; ++s) a0 += *reinterpret_cast<const f32x4*>(p + (long long)s * n);
+  for (; s < nsplit; ++s) a0 += ld.v4(e + (long long)s * n);
   return z + ((a0 + a1) + (a2 + a3));
 }
 // one element (tail of a vec4 unit), same order as one lane of slab_sum4
-__device__ __forceinline__ float slab_sum1(const float* p, long long n, int nsplit) {
+template <class L>
+__device__ __forceinline__ float slab_sum1_l(const L& ld, long long e, long long n, int nsplit) {
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int s = 0;
   for (; s + 3 < nsplit; s += 4) {
-    a0 += p[(long long)s * n];
-    a1 += p[(long long)(s + 1) * n];
-    a2 += p[(long long)(s + 2) * n];
-    a3 += p[(long long)(s + 3) * n];
+    a0 += ld.v1(e + (long long)s * n);
+    a1 += ld.v1(e + (long long)(s + 1) * n);
+    a2 += ld.v1(e + (long long)(s + 2) * n);
+    a3 += ld.v1(e + (long long)(s + 3) * n);
   }
-  for (; s < nsplit; ++s) a0 += p[(long long)s * n];
+  for (; s < nsplit; ++s) a0 += ld.v1(e + (long long)s * n);
   return 0.f + ((a0 + a1) + (a2 + a3));
 }
-// scalar units: slabs rl, rl + rp, ... of one column (row lane rl of rp)
-__device__ __forceinline__ float slab_partial(const float* p, long long n, int nsplit, int rl, int rp) {
+// scalar units: slabs rl, rl + rp, ... of column e (row lane rl of rp)
+template <class L>
+__device__ __forceinline__ float slab_partial_l(const L& ld, long long e, long long n, int nsplit, int rl, int rp) {
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int s = rl;
   for (; s + 3 * rp < nsplit; s += 4 * rp) {
-    a0 += p[(long long)s * n];
-    a1 += p[(long long)(s + rp) * n];
-    a2 += p[(long long)(s + 2 * rp) * n];
-    a3 += p[(long long)(s + 3 * rp) * n];
+    a0 += ld.v1(e + (long long)s * n);
+    a1 += ld.v1(e + (long long)(s + rp) * n);
+    a2 += ld.v1(e + (long long)(s + 2 * rp) * n);
+    a3 += ld.v1(e + (long long)(s + 3 * rp) * n);
   }
-  for (; s < nsplit; s += rp) a0 += p[(long long)s * n];
+  for (; s < nsplit; s += rp) a0 += ld.v1(e + (long long)s * n);
   return (a0 + a1) + (a2 + a3);
+}
+__device__ __forceinline__ f32x4 slab_sum4(const float* p, long long n, int nsplit) {
+  return slab_sum4_l(SlabPlain{p}, 0, n, nsplit);
+}
+__device__ __forceinline__ float slab_sum1(const float* p, long long n, int nsplit) {
+  return slab_sum1_l(SlabPlain{p}, 0, n, nsplit);
+}
+__device__ __forceinline__ float slab_partial(const float* p, long long n, int nsplit, int rl, int rp) {
+  return slab_partial_l(SlabPlain{p}, 0, n, nsplit, rl, rp);
 }
 
 // Units of more than 256 elements (planned when a segment has <= 16 partial
@@ -402,6 +454,7 @@ __device__ __forceinline__ float slab_partial(const float* p, long long n, int n
 // path (4 interleaved accumulators over the slabs), so results are unchanged.
 // The optimizer tail streams P, m, v (+ slabs) once: 16-B accesses keep
 // 4x the bytes in flight per wave-instruction of the 4-B path.
+template <bool DEP>
 __device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const AdamC& c, const GradUnit& u,
                                                    const GradSeg& sg) {
   const int e0 = u.start + 4 * (int)threadIdx.x;
@@ -412,7 +465,8 @@ __device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const 
   if (left >= 4) {
     f32x4 g;
     if (sg.slab) {
-      g = slab_sum4(sg.slab + e0, n, sg.nsplit);
+      if constexpr (DEP) g = slab_sum4_l(SlabSc1(sg.slab, n * sg.nsplit), e0, n, sg.nsplit);
+      else g = slab_sum4(sg.slab + e0, n, sg.nsplit);
       if (!a.do_adam) *reinterpret_cast<f32x4*>(a.G + o) = g;
     } else {
       g = *reinterpret_cast<const f32x4*>(a.G + o);
@@ -441,7 +495,8 @@ __device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const 
   for (int j = 0; j < left; ++j) {  // segment tail (< 4 elements)
     float g;
     if (sg.slab) {
-      g = slab_sum1(sg.slab + e0 + j, n, sg.nsplit);
+      if constexpr (DEP) g = slab_sum1_l(SlabSc1(sg.slab, n * sg.nsplit), e0 + j, n, sg.nsplit);
+      else g = slab_sum1(sg.slab + e0 + j, n, sg.nsplit);
       if (!a.do_adam) a.G[o + j] = g;
     } else {
       g = a.G[o + j];
@@ -455,18 +510,26 @@ __device__ __forceinline__ void grad_finalize_vec4(const FinalizeArgs& a, const 
   }
 }
 
-__device__ __forceinline__ void grad_finalize_body(const FinalizeArgs& a, float* red, AdamC* cs, int bid) {
+template <bool DEP>
+__device__ __forceinline__ void grad_finalize_body_t(const FinalizeArgs& a, float* red, AdamC* cs, int bid) {
   AdamC c{};
-  if (a.do_adam) c = adam_consts_block(a.st, a.hp, cs);
+  if (a.do_adam) c = DEP ? adam_consts_block_sc1(a.st, a.hp, cs) : adam_consts_block(a.st, a.hp, cs);
   const GradUnit u = a.units[bid];
   const GradSeg sg = a.segs[u.seg];
   if (u.count > kFinalizeThreads) {
-    grad_finalize_vec4(a, c, u, sg);
+    grad_finalize_vec4<DEP>(a, c, u, sg);
     return;
   }
   const int t = threadIdx.x, cnt = u.count, rp = kFinalizeThreads / cnt;
   const int col = t % cnt, rl = t / cnt;
-  red[t] = (sg.slab && rl < rp) ? slab_partial(sg.slab + u.start + col, sg.numel, sg.nsplit, rl, rp) : 0.f;
+  float part = 0.f;
+  if (sg.slab && rl < rp) {
+    if constexpr (DEP)
+      part = slab_partial_l(SlabSc1(sg.slab, sg.numel * sg.nsplit), u.start + col, sg.numel, sg.nsplit, rl, rp);
+    else
+      part = slab_partial(sg.slab + u.start + col, sg.numel, sg.nsplit, rl, rp);
+  }
+  red[t] = part;
   __syncthreads();
   if (rl == 0) {
     const long long o = sg.off + u.start + col;
@@ -485,6 +548,11 @@ __device__ __forceinline__ void grad_finalize_body(const FinalizeArgs& a, float*
       a.w16[o] = (__bf16)p;
     }
   }
+}
+// stand-alone finalize launch and the 3-job combos: nothing in the launch
+// writes the slabs or the step state (FinalizeArgs.dep is 0 there)
+__device__ __forceinline__ void grad_finalize_body(const FinalizeArgs& a, float* red, AdamC* cs, int bid) {
+  grad_finalize_body_t<false>(a, red, cs, bid);
 }
 
 // bf16 weights [CO][k][k][CI] -> parity-ordered transpose [s][s][CI][k/s][k/s][CO]

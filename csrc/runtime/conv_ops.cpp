@@ -49,7 +49,11 @@ int mdt_job_igemm(mdt::JobBlob* g, mdt::JobBlob* c, int mode, const void* A, int
                   mdt::ConvDesc d, const float* bias, int relu, void* y16, float* y32, const void* omask,
                   float* colsum, float* ws, int skip_combine);
 int mdt_job_finalize(mdt::JobBlob* j, float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs,
-                     const void* units, int nunits, const void* st, const void* hp, int do_adam);
+                     const void* units, int nunits, const void* st, const void* hp, int do_adam, int dep);
+int mdt_job_gather(mdt::JobBlob* j, const float* X, const int* idx, const void* st, float* xn, unsigned* xtag, int B);
+int mdt_jobs_dep_words();
+int mdt_jobs_dep_err();
+int mdt_pack_jobs_multi_deps(void* img, void* ctr, const unsigned* wait, int n);
 int mdt_job_wtrans(mdt::JobBlob* j, const void* w16, void* w16t, const void* segs, const void* units, int nunits);
 int mdt_job_comm(mdt::JobBlob* j, float* P, float* G, float* Mo, float* Vo, void* w16, const void* segs,
                  const void* units, int nunits, const void* st, const void* hp, int do_adam, const void* ctx, int mode);
@@ -69,7 +73,7 @@ int mdt_launch_jobs(const mdt::JobBlob* jobs, int n, hipStream_t s);
 int mdt_jobs_multi_bytes();
 int mdt_pack_jobs_multi(const mdt::JobBlob* jobs, int n, void* dst);
 int mdt_pack_jobs_multi_stamps(void* img, void* stamps);
-int mdt_launch_jobs_multi(const void* dev_pack, int grid, hipStream_t s);
+int mdt_launch_jobs_multi(const void* dev_pack, int grid, int dep, hipStream_t s);
 int mdt_f28_forward(const long long* p, int B, int M, unsigned stream, int train, hipStream_t s);
 int mdt_f28_forward_pair(const long long* p, const long long* pp, int B, int M, unsigned stream, hipStream_t s);
 int mdt_f28_backward(const long long* p, int M, hipStream_t s);
@@ -348,8 +352,11 @@ bool launch_jobs(const std::vector<Job*>& jobs) {
 // jobs_multi_k launch: returns (uint8 CPU tensor image, grid). The caller keeps
 // the table in device memory for the lifetime of the plan (graph replays).
 std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs,
-                                                const c10::optional<at::Tensor>& stamps) {
-  TORCH_CHECK(!jobs.empty() && jobs.size() <= 8, "pack_jobs_multi takes 1..8 jobs");
+                                                const c10::optional<at::Tensor>& stamps,
+                                                const std::vector<int64_t>& wait,
+                                                const c10::optional<at::Tensor>& dep_ctr) {
+  TORCH_CHECK(!jobs.empty() && jobs.size() <= (wait.empty() ? 8u : 16u),
+              "pack_jobs_multi takes 1..8 jobs (1..16 with a dependency table)");
   std::vector<JobBlob> v;
   for (auto* j : jobs) {
     TORCH_CHECK(j != nullptr && !j->has_post(), "pack_jobs_multi: null job or job with a follow-up pass");
@@ -364,13 +371,24 @@ std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs,
                 "pack_jobs_multi: stamps must be an int64 CUDA tensor of >= 2 * grid elements");
     mdt_pack_jobs_multi_stamps(img.data_ptr(), stamps->data_ptr());
   }
+  if (!wait.empty()) {  // in-launch dependencies (conv_jobs.hip JobPackN): wait[i] = bit mask of jobs job i waits for
+    TORCH_CHECK(wait.size() == jobs.size(), "pack_jobs_multi: one wait mask per job");
+    TORCH_CHECK(dep_ctr.has_value() && dep_ctr->defined() && dep_ctr->is_cuda() &&
+                    dep_ctr->scalar_type() == torch::kInt32 && dep_ctr->is_contiguous() &&
+                    dep_ctr->numel() >= mdt_jobs_dep_words(),
+                "pack_jobs_multi: dep_ctr must be a zeroed contiguous int32 CUDA tensor of >= ",
+                mdt_jobs_dep_words(), " words");
+    std::vector<unsigned> w(wait.begin(), wait.end());
+    TORCH_CHECK(mdt_pack_jobs_multi_deps(img.data_ptr(), dep_ctr->data_ptr(), w.data(), (int)w.size()) == 0,
+                "pack_jobs_multi: bad dependency table (a job may wait only for earlier jobs that do not wait)");
+  }
   return {img, (int64_t)grid};
 }
 
-void launch_jobs_multi(const at::Tensor& dev_pack, int64_t grid) {
+void launch_jobs_multi(const at::Tensor& dev_pack, int64_t grid, bool dep) {
   TORCH_CHECK(dev_pack.is_cuda() && dev_pack.scalar_type() == torch::kUInt8 &&
                   dev_pack.numel() >= mdt_jobs_multi_bytes(), "launch_jobs_multi: device job table");
-  const int r = mdt_launch_jobs_multi(dev_pack.data_ptr(), (int)grid, cur());
+  const int r = mdt_launch_jobs_multi(dev_pack.data_ptr(), (int)grid, dep ? 1 : 0, cur());
   TORCH_CHECK(r == 0, "mdt: launch_jobs_multi failed (", r, ")");
 }
 
@@ -572,15 +590,17 @@ void adam_cast(at::Tensor P, const at::Tensor& G, at::Tensor M, at::Tensor V, at
 
 void grad_finalize(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::Tensor w16, const at::Tensor& segs,
                    const at::Tensor& units, int64_t nunits, const at::Tensor& state, const at::Tensor& hparams,
-                   bool do_adam, Job* job, const std::vector<at::Tensor>& gather, int64_t gather_B) {
+                   bool do_adam, Job* job, const std::vector<at::Tensor>& gather, int64_t gather_B, bool dep) {
   TORCH_CHECK(units.numel() >= nunits * (int64_t)sizeof(GradUnit), "grad_finalize: unit table too small");
   if (job) {
+    TORCH_CHECK(gather.empty(), "grad_finalize: a finalize job takes no gather (use gather_job)");
     rc(mdt_job_finalize(&job->main, P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(),
                         V.data_ptr<float>(), w16.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits,
-                        state.data_ptr(), hparams.data_ptr(), do_adam ? 1 : 0),
+                        state.data_ptr(), hparams.data_ptr(), do_adam ? 1 : 0, dep ? 1 : 0),
        "job_finalize");
     return;
   }
+  TORCH_CHECK(!dep, "grad_finalize: dep applies to finalize jobs only");
   // optional next-batch gather (the fused 28x28 step): [X, idx, xn, xtag] and the batch size
   const float* gX = nullptr;
   const int* gidx = nullptr;
@@ -607,6 +627,25 @@ void grad_finalize(at::Tensor P, at::Tensor G, at::Tensor M, at::Tensor V, at::T
                        w16.data_ptr(), segs.data_ptr(), units.data_ptr(), (int)nunits, state.data_ptr(),
                        hparams.data_ptr(), do_adam ? 1 : 0, gX, gidx, xn, xtag, (int)gather_B, cur()),
      "grad_finalize");
+}
+
+// Next-batch gather as a job of a dependent multi-job launch (it waits for
+// the launch's loss/step job): rows idx[cursor * B + n] of X -> xn, xtag = step.
+void gather_job(const at::Tensor& X, const at::Tensor& idx, const at::Tensor& state, at::Tensor xn, at::Tensor xtag,
+                int64_t B, Job* job) {
+  TORCH_CHECK(job != nullptr, "gather_job: records into a Job");
+  const int dev = X.get_device();
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&idx, &state, &xn, &xtag})
+    TORCH_CHECK(t->is_cuda() && t->get_device() == dev && t->is_contiguous(), "gather_job: tensors on one device");
+  TORCH_CHECK(X.is_cuda() && X.is_contiguous() && X.scalar_type() == torch::kFloat32 && X.numel() % 784 == 0,
+              "gather_job: X [rows][784] f32");
+  TORCH_CHECK(B > 0 && idx.scalar_type() == torch::kInt32 && idx.numel() % B == 0, "gather_job: idx int32 in whole batches");
+  TORCH_CHECK(xn.scalar_type() == torch::kFloat32 && xn.numel() >= B * 784, "gather_job: xn");
+  TORCH_CHECK(xtag.scalar_type() == torch::kInt32 && xtag.numel() >= B, "gather_job: xtag");
+  TORCH_CHECK(state.numel() >= (int64_t)sizeof(TrainState), "gather_job: state");
+  rc(mdt_job_gather(&job->main, X.data_ptr<float>(), idx.data_ptr<int>(), state.data_ptr(), xn.data_ptr<float>(),
+                    reinterpret_cast<unsigned*>(xtag.data_ptr<int>()), (int)B),
+     "job_gather");
 }
 
 // Record a fused all-reduce job (csrc/kernels/comm_jobs.h) over `nunits`
@@ -751,8 +790,9 @@ void bind_conv(pybind11::module& m) {
       .def_property_readonly("nblk", [](const Job& j) { return j.main.nblk; })
       .def_property_readonly("has_post", &Job::has_post);
   m.def("launch_jobs", &launch_jobs);
-  m.def("pack_jobs_multi", &pack_jobs_multi, py::arg("jobs"), py::arg("stamps") = py::none());
-  m.def("launch_jobs_multi", &launch_jobs_multi);
+  m.def("pack_jobs_multi", &pack_jobs_multi, py::arg("jobs"), py::arg("stamps") = py::none(),
+        py::arg("wait") = std::vector<int64_t>{}, py::arg("dep_ctr") = py::none());
+  m.def("launch_jobs_multi", &launch_jobs_multi, py::arg("dev_pack"), py::arg("grid"), py::arg("dep") = false);
   m.def("f28_forward", &f28_forward, py::arg("tensors"), py::arg("B"), py::arg("M"), py::arg("stream"),
         py::arg("train"), py::arg("pair") = std::vector<c10::optional<at::Tensor>>{});
   m.def("f28_backward", &f28_backward, py::arg("tensors"), py::arg("M"));
@@ -799,7 +839,11 @@ void bind_conv(pybind11::module& m) {
   m.def("grad_finalize", &grad_finalize, py::arg("P"), py::arg("G"), py::arg("M"), py::arg("V"), py::arg("w16"),
         py::arg("segs"), py::arg("units"), py::arg("nunits"), py::arg("state"), py::arg("hparams"),
         py::arg("do_adam"), py::arg("job") = py::none(), py::arg("gather") = std::vector<at::Tensor>{},
-        py::arg("gather_B") = 0);
+        py::arg("gather_B") = 0, py::arg("dep") = false);
+  m.def("gather_job", &gather_job, py::arg("X"), py::arg("idx"), py::arg("state"), py::arg("xn"), py::arg("xtag"),
+        py::arg("B"), py::arg("job"));
+  // dependency counter block of a dependent multi-job launch: (words, index of the error word)
+  m.def("jobs_dep_layout", [] { return std::make_tuple((int64_t)mdt_jobs_dep_words(), (int64_t)mdt_jobs_dep_err()); });
   m.def("comm_job", &comm_job, py::arg("P"), py::arg("G"), py::arg("M"), py::arg("V"), py::arg("w16"),
         py::arg("segs"), py::arg("units"), py::arg("nunits"), py::arg("state"), py::arg("hparams"),
         py::arg("do_adam"), py::arg("ctx"), py::arg("mode"), py::arg("job"));

@@ -460,6 +460,10 @@ class ConvVaeTrainer(GraphedEval):
             if err:
                 msgs.append(f"fused 28x28 step: a paired-workgroup exchange timed out (f28_err={err}); "
                             f"the trial trained on incomplete partial sums")
+            derr = int(self.f28_dep[self._dep_err_idx].item())
+            if derr:
+                msgs.append(f"fused 28x28 step: a finalize job gave up waiting for job {derr - 1} of its launch; "
+                            f"the trial's update used incomplete weight gradients")
         red = self.reducer
         if red is not None and hasattr(red, "status"):
             st = int(red.status())
@@ -596,6 +600,16 @@ class ConvVaeTrainer(GraphedEval):
             self.f28_xn = torch.zeros(B * self.D, **f32)
             self.f28_xtag = torch.full((B,), -1, dtype=torch.int32, device=dev)
             self.f28_prefetch = os.getenv("MDT_F28_PREFETCH", "1") != "0"
+            # MDT_F28_FIN_MERGE=1: finalize + Adam (and the prefetch gather)
+            # inside the weight-gradient launch, each layer's units released by
+            # in-launch counters as that layer's weight gradient completes
+            # (conv_jobs.hip JobPackN deps). Bitwise the two-launch tail but
+            # slower (0.079 vs 0.061 ms/step: the waiting workgroups and the
+            # producers' store drains slow the weight gradients 30-80 %,
+            # profiles/r6_fin_merge), so off by default
+            self.f28_fin_merge = os.getenv("MDT_F28_FIN_MERGE", "0") == "1"
+            words, self._dep_err_idx = self.C.jobs_dep_layout()
+            self.f28_dep = torch.zeros(words, dtype=torch.int32, device=dev)  # counters, zero between launches
         self._cast_weights()
 
     def _n_bce(self, M):
@@ -1187,8 +1201,51 @@ class ConvVaeTrainer(GraphedEval):
                  segs=C.make_grad_segs(segs, dev.index or 0), units=C.make_grad_units(units, dev.index or 0),
                  nunits=len(units), layer_units=layer_units, first_dec=first_dec,
                  dec_pack=dec_pack.to(dev), dec_grid=dec_grid, enc_pack=enc_pack.to(dev), enc_grid=enc_grid)
+        p["names"] = names
         self._plans28[M] = p
         return p
+
+    # finalize jobs of the merged launch, ordered by when their layer's weight
+    # gradient completes (profiles/r6_jobs28: dec_fc 5.4, enc_head 5.8, enc1
+    # 7.2, enc2 8.5, dec2 8.8, dec1 9.1 us into the launch)
+    _FIN_ORDER28 = ("dec_fc", "enc_head", "enc1", "enc2", "dec2", "dec1")
+
+    def _merged_pack28(self, p):
+        """One jobs_multi_k table for the whole optimizer tail of the fused
+        28x28 step: the six weight gradients and the loss/step job, then the
+        next-batch gather (waits for the loss job: it needs the advanced
+        cursor), then one finalize+Adam job per layer (waits for that layer's
+        weight gradient and for the loss job's advanced step). Each waiting
+        workgroup is released by in-launch counters (conv_jobs.hip JobPackN),
+        so a layer's update runs while later layers' gradients are still being
+        computed and the step loses a launch boundary. Bitwise the two-launch
+        form: the same bodies, the same per-element summation order."""
+        adam = not self.f28_skip_adam
+        hit = p.get(("merged", adam))
+        if hit is not None:
+            return hit
+        C, st, names = self.C, self.state, p["names"]
+        jobs = list(p["jobs"])  # names order + loss/step
+        loss_i = len(names)
+        wait = [0] * len(jobs)
+        if self.f28_prefetch:
+            j = C.Job()
+            C.gather_job(self._data[0], self._data[1], st.train_state, self.f28_xn, self.f28_xtag, self.B, j)
+            jobs.append(j)
+            wait.append(1 << loss_i)
+        lu = p["layer_units"]
+        for name in self._FIN_ORDER28:
+            i = next(k for k, l in enumerate(self.spec) if l.name == name)
+            u0, u1 = lu[i], lu[i + 1]
+            j = C.Job()
+            C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"],
+                            p["units"].narrow(0, u0 * 12, (u1 - u0) * 12), u1 - u0, st.train_state, st.hparams,
+                            adam, job=j, dep=True)
+            jobs.append(j)
+            wait.append((1 << names.index(name)) | (1 << loss_i))
+        pack, grid = C.pack_jobs_multi(jobs, wait=wait, dep_ctr=self.f28_dep)
+        hit = p[("merged", adam)] = (pack.to(self.device), grid, jobs, wait)
+        return hit
 
     def _step28(self, M):
         """Fused 28x28 step: forward + backward-data (one launch: f28_step_k,
@@ -1205,6 +1262,10 @@ class ConvVaeTrainer(GraphedEval):
             C.f28_backward(p["bwd"], M)
         red = self.reducer
         if red is None:
+            if self.f28_fin_merge:
+                pack, grid, _, _ = self._merged_pack28(p)
+                C.launch_jobs_multi(pack, grid, dep=True)
+                return
             C.launch_jobs_multi(p["jobs_pack"], p["jobs_grid"])
             C.grad_finalize(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.w16, p["segs"], p["units"],
                             p["nunits"], st.train_state, st.hparams, not self.f28_skip_adam,

@@ -528,3 +528,84 @@ def test_f28_next_batch_prefetch_is_bitwise_and_tagged(native_ext):
         res[pre] = (tr.loss_history()[:nb + 3].copy(), tr.params.clone())
     np.testing.assert_array_equal(res[True][0], res[False][0])
     assert torch.equal(res[True][1], res[False][1])
+
+
+_MERGED_CHILD = r"""
+import sys, torch
+from multidisttorch_amd.models.conv_vae import ConvVaeTrainer
+B, nb = 128, 3
+g = torch.Generator().manual_seed(33)
+X = torch.rand(nb * B, 784, generator=g).cuda()
+idx = torch.randperm(nb * B, generator=g).to(torch.int32).cuda()
+tr = ConvVaeTrainer(batch_size=B, image=28, device=torch.device("cuda"), backend="hip", seed=9, use_graphs=True,
+                    graph_steps=2)
+assert tr.f28_fin_merge  # MDT_F28_FIN_MERGE=1 in the environment
+tr.bind_train_data(X, idx)
+tr.set_cursor(0, nb)
+tr.train_steps(5)
+torch.cuda.synchronize()
+assert tr.health_error() is None, tr.health_error()
+torch.save(tr.params.cpu(), sys.argv[1])
+"""
+
+
+def test_f28_merged_finalize_is_bitwise_the_two_launch_tail(native_ext, tmp_path):
+    """The finalize + Adam (and the prefetch gather) run inside the
+    weight-gradient launch, released per layer by in-launch counters
+    (MDT_F28_FIN_MERGE=1, conv_jobs.hip JobPackN deps): parameters, losses and
+    the gathered next batch are bitwise those of the separate finalize launch,
+    over graphs, a tail batch, a host cursor move and a no-Adam step; the
+    counters are back to zero after every launch and no wait gave up. Also
+    with the launch confined to 32 CUs (HSA_CU_MASK, a child process), where
+    most waiting workgroups are not resident beside their producers."""
+    import os
+    import subprocess
+    import sys
+
+    dev = torch.device("cuda")
+    B, nb, tail = 128, 3, 40
+    g = torch.Generator().manual_seed(23)
+    X = torch.rand(nb * B + tail, 784, generator=g).to(dev)
+    idx = torch.randperm(nb * B + tail, generator=g).to(torch.int32).to(dev)
+    res = {}
+    for merge in (False, True):
+        tr = _trainer(B=B, seed=6, use_graphs=True, graph_steps=2)
+        tr.f28_fin_merge = merge
+        tr.bind_train_data(X, idx)
+        tr.set_cursor(0, nb + 1)
+        tr.train_steps(nb)
+        tr.train_steps(1, M=tail)
+        tr.set_cursor(1, nb + 1)
+        tr.train_steps(2)
+        tr.f28_skip_adam = True
+        tr.train_steps(1)
+        grads = tr.grads.clone()
+        tr.f28_skip_adam = False
+        tr.train_steps(2)
+        torch.cuda.synchronize()
+        assert tr.health_error() is None
+        if merge:
+            assert int(tr.f28_dep.abs().sum()) == 0  # every counter re-zeroed, no error word
+        res[merge] = (tr.loss_history()[:nb + 6].copy(), tr.params.clone(), tr.exp_avg_sq.clone(), grads,
+                      tr.f28_xn.clone(), tr.f28_xtag.clone())
+    np.testing.assert_array_equal(res[True][0], res[False][0])
+    for a, b in zip(res[True][1:], res[False][1:]):
+        assert torch.equal(a, b)
+
+    # reference for the child: same data / seed, separate finalize launch, in this process
+    g = torch.Generator().manual_seed(33)
+    X = torch.rand(nb * B, 784, generator=g).to(dev)
+    idx = torch.randperm(nb * B, generator=g).to(torch.int32).to(dev)
+    tr = _trainer(B=B, seed=9, use_graphs=True, graph_steps=2)
+    tr.f28_fin_merge = False
+    tr.bind_train_data(X, idx)
+    tr.set_cursor(0, nb)
+    tr.train_steps(5)
+    torch.cuda.synchronize()
+    ref = tr.params.cpu()
+    out = tmp_path / "params.pt"
+    env = dict(os.environ, HSA_CU_MASK="0:0-31", MDT_F28_FIN_MERGE="1")
+    r = subprocess.run([sys.executable, "-c", _MERGED_CHILD, str(out)], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert torch.equal(torch.load(out, weights_only=True), ref)
