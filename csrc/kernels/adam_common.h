@@ -34,13 +34,12 @@ __device__ __forceinline__ AdamC adam_consts_block(const TrainState* st, const H
 // loads, so neither this CU's L1 nor the scalar cache can serve an old copy.
 __device__ __forceinline__ AdamC adam_consts_block_sc1(const TrainState* st, const HParams* hp, AdamC* sh) {
   if (threadIdx.x == 0) {
+    using gu64 = __attribute__((address_space(1))) unsigned long long;  // global, never flat
     TrainState* s = const_cast<TrainState*>(st);
-    const double b1pow = __builtin_bit_cast(
-        double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(&s->b1pow), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT));
-    const double b2pow = __builtin_bit_cast(
-        double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(&s->b2pow), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT));
+    const double b1pow =
+        __builtin_bit_cast(double, __hip_atomic_load((gu64*)&s->b1pow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const double b2pow =
+        __builtin_bit_cast(double, __hip_atomic_load((gu64*)&s->b2pow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     AdamC c;
     c.step_size = (float)(hp->lr_d / (1.0 - b1pow));
     c.bc2s = (float)sqrt(1.0 - b2pow);

@@ -238,15 +238,19 @@ __device__ __forceinline__ void run_multi_job(const JobBlob& j, uint8_t* lds, in
   }
 }
 
+// every counter access is a GLOBAL agent-scope access (never flat)
+using gu32 = __attribute__((address_space(1))) unsigned;
+__device__ __forceinline__ gu32* dep_word(unsigned* ctr, int i) { return (gu32*)(ctr + i * kDepStride); }
+
 __device__ __forceinline__ void dep_wait(const JobPackN* __restrict__ p, unsigned* ctr, unsigned mask, int n) {
   if (threadIdx.x == 0) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (int k = 0; k < n; ++k) {
       if (!((mask >> k) & 1u)) continue;
       const unsigned need = (unsigned)(p->start[k + 1] - p->start[k]);
-      while (__hip_atomic_load(ctr + k * kDepStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+      while (__hip_atomic_load(dep_word(ctr, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > kDepTimeoutTicks) {
-          __hip_atomic_store(ctr + kDepErr * kDepStride, 1u + (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dep_word(ctr, kDepErr), 1u + (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
         __builtin_amdgcn_s_sleep(MDT_DEP_SLEEP);
@@ -262,11 +266,11 @@ __device__ __forceinline__ void dep_wait(const JobPackN* __restrict__ p, unsigne
 // full), so nothing reads or adds to them any more in this launch.
 __device__ __forceinline__ void dep_done(const JobPackN* __restrict__ p, unsigned* ctr, int n) {
   if (threadIdx.x == 0) {
-    const unsigned done = __hip_atomic_fetch_add(ctr + kDepDone * kDepStride, 1u, __ATOMIC_RELAXED,
+    const unsigned done = __hip_atomic_fetch_add(dep_word(ctr, kDepDone), 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     if (done + 1 == (unsigned)p->nwait_blocks) {
-      for (int k = 0; k < n; ++k) __hip_atomic_store(ctr + k * kDepStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr + kDepDone * kDepStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < n; ++k) __hip_atomic_store(dep_word(ctr, k), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dep_word(ctr, kDepDone), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -279,7 +283,7 @@ __device__ __forceinline__ void dep_signal(unsigned* ctr, int job, int mode) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __hip_atomic_fetch_add(ctr + job * kDepStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(dep_word(ctr, job), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

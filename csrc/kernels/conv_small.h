@@ -363,13 +363,14 @@ __device__ __forceinline__ void batch_gather_dep_body(const BatchGather& g, int 
   const int e = b * kFinalizeThreads + (int)threadIdx.x;
   const int n = e / 196, c = e - 196 * (e / 196);
   if (n < g.B) {
+    using gi32 = __attribute__((address_space(1))) int;  // global, never flat
+    using gu64 = __attribute__((address_space(1))) unsigned long long;
     TrainState* st = const_cast<TrainState*>(g.st);
-    const int cur = __hip_atomic_load(&st->cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int cur = __hip_atomic_load((gi32*)&st->cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int row = g.idx[(size_t)cur * g.B + n];
     reinterpret_cast<float4*>(g.xn + (size_t)n * 784)[c] = reinterpret_cast<const float4*>(g.X + (size_t)row * 784)[c];
     if (c == 0)
-      g.xtag[n] = (unsigned)__hip_atomic_load(reinterpret_cast<unsigned long long*>(&st->step), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
+      g.xtag[n] = (unsigned)__hip_atomic_load((gu64*)&st->step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -138,6 +138,50 @@ def protocol_sites(text: str, window: int = 4) -> Dict[str, list]:
     return sites
 
 
+# the in-launch dependency protocol of the dependent multi-job kernel
+# (conv_jobs.hip dep_wait / dep_signal, FinalizeArgs.dep, batch_gather_dep_body)
+DEP_KERNEL = "jobs_multi_kILb1E"
+_AGENT_LD = re.compile(r"^global_load_dword\S*\b.*\bsc1$")
+_AGENT_ADD = re.compile(r"^global_atomic_add\b")
+_SC1_BUF_LD = re.compile(r"^buffer_load_dword(x4)?\b.*\bsc1$")
+_FLAT_AGENT = re.compile(r"^flat_(load|store|atomic)\S*\b(?!.*\bsc0\b).*\bsc1\b")
+
+
+def dep_sites(text: str, window: int = 40) -> Dict[str, list]:
+    """Instruction windows of the dependent launch's hand-off protocol:
+
+    * ``poll``: an agent-scope ``global_load_dword ... sc1`` within a few
+      instructions of an ``s_sleep`` (the bounded counter poll);
+    * ``release_add``: ``buffer_wbl2 sc1`` (agent release, plain-store
+      producers), ``s_waitcnt vmcnt(0)``, then a ``global_atomic_add`` (the
+      counter add) inside ``window`` instructions;
+    * ``drain_add``: ``s_waitcnt vmcnt(0)`` (explicit drain), ``s_barrier``
+      within 3 instructions, then a ``global_atomic_add`` inside ``window``;
+    * ``sc1_loads``: ``buffer_load_dword[x4] ... sc1`` (slab reads past L1);
+    * ``flat_agent``: flat accesses with agent-scope ``sc1`` (must be none:
+      every hand-off access is global or buffer).
+    """
+    ops = _ops(text)
+    out: Dict[str, list] = {"poll": [], "release_add": [], "drain_add": [], "sc1_loads": [], "flat_agent": []}
+    for i, o in enumerate(ops):
+        nxt = ops[i + 1:i + 1 + window]
+        if _AGENT_LD.match(o) and any(x.startswith("s_sleep") for x in ops[max(0, i - 3):i + 4]):
+            out["poll"].append(o)
+        if o == "buffer_wbl2 sc1" and nxt and _WAIT_VM0.match(nxt[0]):
+            a = [x for x in nxt if _AGENT_ADD.match(x)]
+            if a:
+                out["release_add"].append([o, nxt[0], a[0]])
+        if _WAIT_VM0.match(o) and "s_barrier" in nxt[:3]:
+            a = [x for x in nxt if _AGENT_ADD.match(x)]
+            if a:
+                out["drain_add"].append([o, "s_barrier", a[0]])
+        if _SC1_BUF_LD.match(o):
+            out["sc1_loads"].append(o)
+        if _FLAT_AGENT.match(o):
+            out["flat_agent"].append(o)
+    return out
+
+
 def main():
     for name, sub in COMM_KERNELS.items():
         text = disassemble(sub)
@@ -148,6 +192,13 @@ def main():
             print(f"  {k}: {len(v)} site(s)")
             for site in v[:2]:
                 print("    " + " ; ".join(site))
+    text = disassemble(DEP_KERNEL)
+    print(f"== {DEP_KERNEL}: {'not found' if text is None else str(len(_ops(text))) + ' instructions'}")
+    if text is not None:
+        for k, v in dep_sites(text).items():
+            print(f"  {k}: {len(v)} site(s)")
+            for site in v[:2]:
+                print("    " + (" ; ".join(site) if isinstance(site, list) else site))
 
 
 if __name__ == "__main__":

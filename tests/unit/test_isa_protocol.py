@@ -75,3 +75,28 @@ def test_every_publish_has_its_wait(sites):
     # all-gather flag 2e): each publish site pairs with a poll and a fence site
     j = sites["jobs_multi_k"]
     assert len(j["publish_drain"]) == len(j["flag_release"]) == len(j["poll_acquire"]) == len(j["fence_acquire"]) >= 2
+
+
+@pytest.fixture(scope="module")
+def dep():
+    text = isa.disassemble(isa.DEP_KERNEL)
+    assert text is not None, f"{isa.DEP_KERNEL} not found in {isa.SO}"
+    return isa.dep_sites(text)
+
+
+def test_dependent_jobs_poll_and_count_with_global_agent_accesses(dep):
+    # conv_jobs.hip dep_wait / dep_signal: the bounded poll is a relaxed agent
+    # (sc1) GLOBAL load beside its s_sleep; the producer's counter add follows
+    # its drain (vmcnt(0) + barrier) and, for plain-store producers, an agent
+    # release; no flat access carries the agent bit
+    assert dep["poll"], dep
+    assert dep["drain_add"], dep
+    assert dep["release_add"], dep
+    assert not dep["flat_agent"], dep["flat_agent"]
+
+
+def test_dependent_finalize_reads_slabs_past_l1(dep):
+    # FinalizeArgs.dep: the slabs handed off inside the launch are read with
+    # sc1 buffer loads (16-B vec4 units and 4-B scalar units)
+    assert any("dwordx4" in o for o in dep["sc1_loads"]), dep["sc1_loads"]
+    assert any("dwordx4" not in o for o in dep["sc1_loads"]), dep["sc1_loads"]
