@@ -49,10 +49,9 @@ def test_p2p_in_process_eager_and_graph(native_ext, s, two):
     """two = two_shot_min_bytes: -1 one-shot only, 0 two-shot for every bucket,
     16384 two-shot for the buckets of >= 4096 elements (mixed launch).
 
-    In-process "ranks" progress only while their streams sit on different
-    hardware queues (GPU_MAX_HW_QUEUES = 4 per process): the graph-replay part
-    runs for the first case only, before more streams exist; the two-shot
-    graph replays are covered by the multi-process test (one process per rank)."""
+    The graph-replay form runs in a fresh process
+    (test_p2p_in_process_graph_replay); the two-shot graph replays are covered
+    by the multi-process test (one process per rank)."""
     C = native_ext
     n = 200_003  # odd size: vector body + scalar tail; tiny first bucket = one block
     bounds = [0, 100, 4096, 70_000, n]
@@ -85,28 +84,62 @@ def test_p2p_in_process_eager_and_graph(native_ext, s, two):
         r.reset_iteration()
     torch.cuda.synchronize()
     torch.testing.assert_close(flats[1].cpu().double(), ref, rtol=0, atol=1e-6)
-    if two >= 0:
-        return
-    # hipGraph capture per "rank", replays on separate streams
-    graphs, streams = [], [torch.cuda.Stream() for _ in reds]
-    for r, st in zip(reds, streams):
-        st.wait_stream(torch.cuda.current_stream())
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=st):
-            r.launch_all()
-            r.wait_all()
-        graphs.append(g)
+
+
+_GRAPH_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from multidisttorch_amd.ops import native
+C = native.ensure_built()
+dev = torch.device("cuda", 0)
+n, bounds = 200_003, [0, 100, 4096, 70_000, 200_003]
+# the graph streams first, before anything else in this process exists: the two
+# in-process "ranks" progress only while their streams sit on different hardware
+# queues (GPU_MAX_HW_QUEUES = 4 per process, assigned in creation order)
+streams = [torch.cuda.Stream() for _ in range(2)]
+flats = [torch.zeros(n, device=dev) for _ in range(2)]
+reds = [C.XgmiP2PReducer(r, 2, flats[r], bounds, True, 0.0, 64, 5.0, -1) for r in range(2)]
+bases = [r.local_base() for r in reds]
+for r in reds:
+    r.connect_local(bases)
+graphs = []
+for r, st in zip(reds, streams):
+    st.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        r.launch_all()
+        r.wait_all()
+    graphs.append(g)
+torch.cuda.synchronize()
+for it in range(20, 23):
+    gen = torch.Generator().manual_seed(it)
+    vals = [torch.randn(n, generator=gen) for _ in flats]
+    for f, v in zip(flats, vals):
+        f.copy_(v.to(dev))
+    ref = sum(v.double() for v in vals) / 2
     torch.cuda.synchronize()
-    for it in range(20, 23):
-        ref = _fill(flats, it)
-        torch.cuda.synchronize()
-        for g, st in zip(graphs, streams):
-            with torch.cuda.stream(st):
-                g.replay()
-        torch.cuda.synchronize()
-        assert [r.status() for r in reds] == ok
-        assert _same(flats)
-        torch.testing.assert_close(flats[0].cpu().double(), ref, rtol=0, atol=1e-6)
+    for g, st in zip(graphs, streams):
+        with torch.cuda.stream(st):
+            g.replay()
+    torch.cuda.synchronize()
+    assert [r.status() for r in reds] == [0, 0], [r.status() for r in reds]
+    assert torch.equal(flats[0], flats[1])
+    torch.testing.assert_close(flats[0].cpu().double(), ref, rtol=0, atol=1e-6)
+print("GRAPH_OK", flush=True)
+"""
+
+
+def test_p2p_in_process_graph_replay(native_ext):
+    """hipGraph capture per in-process "rank", replays on separate streams, in
+    a fresh process whose first two streams are the replay streams (the
+    pytest process's stream history decides which hardware queue a new stream
+    gets, and two ranks on one queue wait on each other until the kernel's
+    timeout)."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, "-c", _GRAPH_CHILD, ROOT], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "GRAPH_OK" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
+
 
 
 def test_two_shot_is_bitwise_one_shot(native_ext):
