@@ -39,7 +39,7 @@ def main():
     C, p = tr.C, tr._plan28(B)
     names = ["enc1", "enc2", "enc_head", "dec_fc", "dec1", "dec2", "loss"]
     if a.merged:
-        assert tr.f28_fin_merge
+        tr.f28_fin_merge = True  # MDT_F28_FIN_MERGE's form for this trainer
         _, _, jobs, wait = tr._merged_pack28(p)
         names += (["gather"] if tr.f28_prefetch else []) + ["fin_" + n for n in tr._FIN_ORDER28]
     else:
