@@ -155,12 +155,13 @@ struct JLossStep {
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 // ------------------------------------------------------------ multi-job ----
-// Up to kMaxMultiJobs independent jobs of any supported kind in ONE launch,
-// dispatched per workgroup by a runtime switch (the fused 28x28 step's six
+// Up to 8 independent jobs (kMaxMultiJobs = 16 with dependencies, below) of
+// any supported kind in ONE launch, dispatched per workgroup by a runtime switch (the fused 28x28 step's six
 // weight gradients + its loss/step job). Unlike jobs_k it needs no
 // instantiation per combination; its register allocation is the maximum over
 // the bodies, which is what those bodies use anyway.
-// Dependencies between the jobs of ONE launch (null ctr = none). A job whose
+//
+// Dependencies between the jobs of ONE launch (jobs_multi_k<true>). A job whose
 // `wait` mask is set runs each of its workgroups only after every workgroup
 // of the masked jobs has finished; those count themselves done:
 //   producer: every wave `s_waitcnt vmcnt(0)` -> workgroup barrier -> one lane

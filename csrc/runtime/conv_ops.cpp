@@ -348,8 +348,8 @@ bool launch_jobs(const std::vector<Job*>& jobs) {
   return true;
 }
 
-// Pack recorded jobs (any supported kinds, up to 8) into a job table for ONE
-// jobs_multi_k launch: returns (uint8 CPU tensor image, grid). The caller keeps
+// Pack recorded jobs (any supported kinds, up to 8; up to 16 with `wait`) into
+// a job table for ONE jobs_multi_k launch: returns (uint8 CPU tensor image, grid). The caller keeps
 // the table in device memory for the lifetime of the plan (graph replays).
 std::tuple<at::Tensor, int64_t> pack_jobs_multi(const std::vector<Job*>& jobs,
                                                 const c10::optional<at::Tensor>& stamps,
