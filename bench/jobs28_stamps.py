@@ -51,7 +51,7 @@ def main():
     pack, grid = C.pack_jobs_multi(jobs, stamps=stamps, wait=wait, dep_ctr=tr.f28_dep if wait else None)
     assert grid == grid0
     if a.merged:
-        p[("merged", True)] = (pack.to(dev), grid, jobs, wait)
+        p[("merged", True, bool(tr.f28_prefetch))] = (pack.to(dev), grid, jobs, wait)
     else:
         p["jobs_pack"], p["jobs_grid"] = pack.to(dev), grid
     runs = []

@@ -1221,7 +1221,8 @@ class ConvVaeTrainer(GraphedEval):
         computed and the step loses a launch boundary. Bitwise the two-launch
         form: the same bodies, the same per-element summation order."""
         adam = not self.f28_skip_adam
-        hit = p.get(("merged", adam))
+        key = ("merged", adam, bool(self.f28_prefetch))
+        hit = p.get(key)
         if hit is not None:
             return hit
         C, st, names = self.C, self.state, p["names"]
@@ -1244,7 +1245,7 @@ class ConvVaeTrainer(GraphedEval):
             jobs.append(j)
             wait.append((1 << names.index(name)) | (1 << loss_i))
         pack, grid = C.pack_jobs_multi(jobs, wait=wait, dep_ctr=self.f28_dep)
-        hit = p[("merged", adam)] = (pack.to(self.device), grid, jobs, wait)
+        hit = p[key] = (pack.to(self.device), grid, jobs, wait)
         return hit
 
     def _step28(self, M):
