@@ -58,3 +58,12 @@ def test_conv_bucket_bounds_fall_on_layer_starts():
         assert b[0] == 0 and b[-1] == tr.numel and b == sorted(b)
         assert all(x in starts for x in b[:-1])
     assert len(tr.bucket_bounds(0.5)) > len(tr.bucket_bounds(8)) >= 2
+
+
+def test_merged_tail_finalizes_every_28x28_layer_once():
+    # MDT_F28_FIN_MERGE's job table (ConvVaeTrainer._merged_pack28) has one
+    # finalize job per layer of the 28x28 model, released by that layer's
+    # weight-gradient job: the order list must name each layer exactly once
+    names = [l.name for l in conv_vae_spec(28)]
+    order = ConvVaeTrainer._FIN_ORDER28
+    assert sorted(order) == sorted(names) and len(order) == len(set(order))
